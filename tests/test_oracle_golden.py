@@ -1,0 +1,139 @@
+"""Pin the CPU oracle (oracle/nav_oracle.c, oracle/td3_oracle.py) against vectors produced by the
+reference itself (tests/golden/make_golden.py). CPU only."""
+import numpy as np
+import pytest
+
+from conftest import golden
+
+
+def test_legacy_rng_stream_matches_numpy(orc):
+    # numpy legacy RandomState is the reference's RNG (environment.py:108-132, robot.py:111, 640)
+    for seed in (1707366464, 0, 1, 987654321):
+        rs = np.random.RandomState(seed)
+        o = orc.LegacyRandomState(seed)
+        assert [rs.random_sample() for _ in range(7)] == [o.random_sample() for _ in range(7)]
+        assert [rs.randint(0, 4) for _ in range(9)] == [o.randint(0, 4) for _ in range(9)]
+        assert [rs.normal(0, 1) for _ in range(9)] == [o.gauss() for _ in range(9)]
+        assert (rs.permutation(1500) == o.permutation(1500)).all()
+        assert (rs.choice(999, 100, replace=False) == o.permutation(999)[:100]).all()
+
+
+def test_dynamics_and_step_vs_reference(orc):
+    g = golden("dynamics.npz")
+    sp, an = g["speed"], g["angle"]
+    n = len(g["state"])
+    out = np.array([orc.dynamics(sp, an, g["state"][i], g["action"][i]) for i in range(n)])
+    ref = g["dynamics"]
+    nan = np.isnan(ref)
+    assert (np.isnan(out) == nan).all()
+    # atan2 may differ by 1 ulp (numpy's SIMD atan2 vs libm); the 1e-5 bar of north_star is far off
+    assert np.max(np.abs(out[~nan] - ref[~nan])) < 1e-12
+    assert np.mean(out[~nan] == ref[~nan]) > 0.9
+    for i in range(n):
+        s, ok = orc.step(sp, an, g["state"][i], g["action"][i])
+        assert ok == g["committed"][i]
+        assert np.max(np.abs(s - g["step"][i])) < 1e-12
+
+
+def test_init_goal_reset_stream_bit_exact(orc):
+    g = golden("rng_init.npz")
+    for k, seed in enumerate(g["seeds"]):
+        o = orc.LegacyRandomState(int(seed))
+        region, goal, side, draws = o.init_and_goal()
+        assert (region == g["region"][k]).all(), seed
+        assert (goal == g["goal"][k]).all(), seed
+        for j in range(3):
+            assert (o.reset(region) == g["resets"][k][j]).all()
+        assert [o.random_sample() for _ in range(4)] == list(g["tail"][k])
+
+
+def test_agent_trace_vs_reference(orc):
+    """Replay the reference's headless tick loop through the oracle's fused tick (same actions,
+    same reset states, same demo set): rewards, dones, flags and counters must match."""
+    t = golden("trace.npz")
+    p = orc.default_params()
+    types = t["tick_type"]
+    first = int(np.nonzero(types == 0)[0][0])
+    st = orc.VecAgentState(1)
+    c = t["counters"]
+    st.state[0] = t["tick_state"][first]
+    st.goal[0] = t["goal"]
+    st.region[0] = t["region"]
+    st.plan_index[0] = int(c[first][0])
+    st.path_length[0] = int(c[first][1])
+    st.episodes[0] = int(c[first][2])
+    st.noise_scale[0] = c[first][6]
+    st.meta[0] = 4  # demo_flag
+    demo = t["demo_set"]
+    n_checked = 0
+    for i in range(first, len(types)):
+        if types[i] != 0:
+            continue
+        a = t["tick_action"][i]
+        lo, hi = t["push_idx"][i]
+        assert hi - lo == 1
+        reset_state = None
+        if i + 1 < len(types) and types[i + 1] == 2:
+            reset_state = t["tick_next"][i + 1]
+        flags, ns, row, r = st.tick(p, t["speed"], t["angle"], demo, 0, a, reset_state)
+        assert np.max(np.abs(ns - t["push_s2"][lo])) < 1e-12
+        assert abs(r - t["push_r"][lo]) <= 1e-9 * max(1.0, abs(t["push_r"][lo]))
+        assert bool(flags & 1) == bool(t["push_d"][lo])
+        assert row[4] == np.float32(t["push_r"][lo])
+        # counters after the reference's NEXT tick (which is where its reset/increment lands)
+        if reset_state is not None:
+            cc = c[i + 1]
+            assert st.episodes[0] == int(cc[2]) and st.path_length[0] == int(cc[1])
+            assert st.noise_scale[0] == cc[6]
+            assert st.plan_index[0] == 1 and int(cc[0]) == 0
+            assert np.array_equal(st.state[0], t["tick_next"][i + 1])
+        else:
+            assert (st.meta[0] & 2) == 0
+        n_checked += 1
+    assert n_checked > 300
+
+
+def test_action_epilogue_and_actor_vs_reference(orc):
+    import torch
+    from oracle.td3_oracle import MLP, make_mlp_params
+    g = golden("actions.npz")
+    actor = MLP(make_mlp_params(int(g["actor_seed"]), [2, 200, 200, 200, 2]))
+    b = (g["states"] - g["goals"]).astype(np.float32)
+    with torch.no_grad():
+        res = actor.forward(torch.tensor(b)).numpy()
+    # batch-64 vs the reference's batch-1 GEMM: summation order differs (fp32)
+    assert np.allclose(res, g["residual"], rtol=2e-5, atol=1e-4)
+    for i in range(len(b)):
+        a = orc.act_epilogue(g["states"][i], g["goals"][i], g["residual"][i], g["sigmas"][i],
+                             g["z"][i])
+        assert (a == g["action_train"][i]).all()
+        a = orc.act_epilogue(g["states"][i], g["goals"][i], g["residual"][i], 0.0, None)
+        assert (a == g["action_test"][i]).all()
+
+
+def test_td3_oracle_vs_reference():
+    from oracle.td3_oracle import TD3Oracle, make_mlp_params, param_digest
+    g = golden("td3.npz")
+    ora = TD3Oracle(make_mlp_params(21, [2, 200, 200, 200, 2]),
+                    make_mlp_params(22, [4, 200, 200, 200, 1]),
+                    make_mlp_params(23, [4, 200, 200, 200, 1]))
+    it = {"s": 0, "n": 0}
+    S, A, R, S2, D, idx, noise = (g[k] for k in ("S", "A", "R", "S2", "D", "idx", "noise"))
+
+    def sample():
+        i = idx[it["s"]]; it["s"] += 1
+        return S[i], A[i], R[i], S2[i], D[i]
+
+    def nz():
+        x = noise[it["n"]]; it["n"] += 1
+        return x
+
+    closs, aloss = ora.td3_update(sample, nz, int(g["epochs"]))
+    np.testing.assert_allclose(np.array(closs), g["critic_loss"], rtol=1e-5)
+    np.testing.assert_allclose(np.array(aloss), g["actor_loss"], rtol=1e-5)
+    for name, net in ora.networks().items():
+        dig = param_digest(net)
+        for k, (s, q, ix, v) in enumerate(dig):
+            assert (ix == g[name + "_idx"][k]).all()
+            np.testing.assert_allclose(v, g[name + "_val"][k], rtol=0, atol=1e-7)
+            np.testing.assert_allclose(s, g[name + "_sum"][k], rtol=1e-6, atol=1e-5)
