@@ -1,0 +1,229 @@
+#!/usr/bin/env python3
+"""bench.py — env-steps/s of the vectorised residual-TD3 loop on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json config 3): 65 536 parallel envs per GPU, full residual-TD3 update with
+2 x 256 actor/critic MLPs. One bench step = one vector tick of every env (nav_act -> nav_agent_step
+-> nav_demo_reward) followed by `--updates` TD3 epochs (critic every epoch, actor + Polyak every
+2nd) at batch `--batch` sampled from the device replay ring. Synthetic seeded start/goal pairs
+(Philox, 64 tasks of 1 024 envs), synthetic Perlin-style fields and straight-line demonstration
+sets, random-init networks (no datasets or checkpoints exist offline).
+
+N > 1 (torch.distributed.run, one process per GPU): independent env blocks per rank (seed +
+rank), no data-path collective ("scaling": "weak"); `--shared-policy` adds the RCCL all-reduce of
+flat actor/critic gradients (BASELINE config 5). Rank 0 prints one JSON line.
+
+Besides `value`, the line carries `roofline` for the dominant kernel (HIP-event timed inside the
+timed region on the launch stream), the step kernel's HBM figure on a large-N sweep, and
+`cpu_baseline` (the oracle CPU port of the same loop, rank 0 only, bounded sample).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.join(HERE, "residual-td3-robot-navigation_amd"))
+
+import torch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP32_MFMA_PEAK_TFS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
+FP64_VALU_PEAK_TFS = 78.6    # MI355X spec FP64 vector
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--envs", type=int, default=65536)
+    ap.add_argument("--hidden", type=int, default=256)
+    ap.add_argument("--layers", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=32768)
+    ap.add_argument("--updates", type=int, default=2)
+    ap.add_argument("--envs-per-group", type=int, default=1024)
+    ap.add_argument("--seed", type=int, default=1707366464)
+    ap.add_argument("--shared-policy", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-sweep", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--breakdown", action="store_true", help="print the per-kernel table")
+    return ap.parse_args()
+
+
+def dist_setup(args):
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if ws > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return ws, rank, local
+
+
+def barrier(ws):
+    if ws > 1:
+        torch.distributed.barrier()
+
+
+def step_kernel_sweep(field, sizes, reps=20):
+    """Step-kernel HBM figure: nav_agent_step (fused tick) and nav_env_step (pure
+    Environment.step) alone at growing N, HIP-event timed on the launch stream."""
+    from nav import prof
+    from nav.vec_env import ReplayRing, VecEnv
+    out = []
+    for n in sizes:
+        env = VecEnv(n, field, seed=11, envs_per_group=n, demo_flag=False)
+        rep = ReplayRing(n, "cuda")
+        act = (torch.rand(n, 2, dtype=torch.float64, device="cuda") - 0.5) * 14
+        for _ in range(6):  # fill the 5-deep stuck history: steady-state traffic
+            env.agent_step(act, rep)
+            env.step(act)
+        t = prof.KernelTimer(["agent_step", "env_step"])
+        with prof.timing(t):
+            for _ in range(reps):
+                env.agent_step(act, rep)
+                env.step(act)
+        s = t.summary()
+        row = {"n_envs": n}
+        for k, bpe in (("agent_step", prof.AGENT_STEP_BYTES), ("env_step", prof.ENV_STEP_BYTES)):
+            us = s[k]["avg_us"]
+            row[k] = {"avg_us": round(us, 2), "bytes_per_env": bpe,
+                      "GBps": round(bpe * n / (us * 1e-6) / 1e9, 1),
+                      "env_steps_per_s": n / (us * 1e-6)}
+        out.append(row)
+        del env, rep, act
+        torch.cuda.empty_cache()
+    return out
+
+
+def cpu_baseline(args, trainer):
+    from oracle.cpu_loop import CPUPort, time_port
+    from oracle import oracle as O
+    from nav.fields import make_fields
+    n = args.envs
+    speed, angle = make_fields(args.seed)
+    pts = trainer.env.demo_xy.cpu().numpy()
+    off = trainer.env.demo_off.cpu().numpy() if trainer.env.demo_off is not None else \
+        [0, len(pts)]
+    port = CPUPort(n, args.hidden, args.layers, args.batch, args.updates,
+                   args.envs_per_group, args.seed, speed, angle, pts, off)
+    k, dt = time_port(port, args.cpu_budget, 6)
+    return {"value": k * n / dt, "unit": "env-steps/s", "cores": max(O.lib().orc_threads(),
+                                                                      torch.get_num_threads()),
+            "kind": "port",
+            "sample": f"{k} vector steps of the same workload ({n} envs, TD3 {args.updates} "
+                      f"epochs x batch {args.batch}, {args.layers}x{args.hidden}) on the oracle "
+                      f"CPU port (C OpenMP env tick + torch-CPU fp32 TD3), {dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    ws, rank, local = dist_setup(args)
+    from nav import prof
+    from nav._lib import lib, require_gpu
+    from nav.trainer import VecTrainer
+    require_gpu()
+    lib()
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    hook = None
+    if args.shared_policy and ws > 1:
+        def hook(g):  # RCCL all-reduce (sum) over xGMI, then mean
+            torch.distributed.all_reduce(g)
+            g.div_(ws)
+    tr = VecTrainer(n_envs=args.envs, hidden=args.hidden, n_hidden=args.layers, batch=args.batch,
+                    updates_per_step=args.updates, seed=args.seed + rank,
+                    envs_per_group=args.envs_per_group, device=dev, grad_hook=hook)
+    if args.shared_policy and ws > 1:
+        for net in tr.td3.networks().values():  # same initial policy on every rank
+            torch.distributed.broadcast(net.params, 0)
+            net.pack()
+    # warmup: first step fills the replay ring past one batch; then breakdown pass
+    for _ in range(max(args.warmup, 1)):
+        tr.step()
+    torch.cuda.synchronize()
+    bd = prof.KernelTimer()
+    with prof.timing(bd):
+        for _ in range(2):
+            tr.step()
+    breakdown = bd.summary()
+    dominant = max(breakdown, key=lambda k: breakdown[k]["total_ms"])
+
+    # ---- timed region
+    timer = prof.KernelTimer([dominant, "agent_step"])
+    barrier(ws)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with prof.timing(timer):
+        for _ in range(args.steps):
+            tr.step()
+    torch.cuda.synchronize()
+    barrier(ws)
+    dt = time.perf_counter() - t0
+    if ws > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = t.item()
+    ksum = timer.summary()
+    env_steps = args.envs * args.steps * ws
+    value = env_steps / dt
+
+    if rank == 0:
+        d = ksum[dominant]
+        is_bytes = dominant in ("agent_step", "env_step", "grad_reduce")
+        ach = d["work_per_launch"] / (d["avg_us"] * 1e-6)
+        if is_bytes:
+            roof = {"bound": "hbm", "kernel": dominant, "achieved": round(ach / 1e9, 1),
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / 1e9 / HBM_PEAK_GBS, 4), "traffic": None}
+        else:
+            tf = ach / 1e12
+            peak = FP64_VALU_PEAK_TFS if dominant == "demo_reward" else FP32_MFMA_PEAK_TFS
+            roof = {"bound": "valu" if dominant == "demo_reward" else "mfma",
+                    "kernel": dominant, "achieved": round(tf, 2), "peak": peak,
+                    "unit": "TFLOP/s", "frac": round(tf / peak, 4), "traffic": None,
+                    "flop_per_launch": d["work_per_launch"], "avg_us": round(d["avg_us"], 2),
+                    "launches": d["launches"]}
+        a = ksum.get("agent_step")
+        step_k = None
+        if a:
+            gbs = a["work_per_launch"] / (a["avg_us"] * 1e-6) / 1e9
+            step_k = {"kernel": "nav_agent_step", "n_envs": args.envs,
+                      "avg_us": round(a["avg_us"], 2), "bytes_per_env": prof.AGENT_STEP_BYTES,
+                      "GBps": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
+        sweep = None if args.no_sweep else step_kernel_sweep(
+            tr.field, [65536, 1 << 20, 1 << 22, 1 << 24])
+        cpu = None if args.no_cpu_baseline else cpu_baseline(args, tr)
+        line = {
+            "metric": "env-steps/sec at 65 536 parallel envs (full residual-TD3 update)",
+            "value": value, "unit": "env-steps/s", "n_gpus": ws, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": 1e3 * dt / args.steps,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "fp32 MLP (MFMA) / fp64 env state",
+            "data": "synthetic (Philox start/goal pairs, generated fields, straight-line demos)",
+            "config": {"workload": "config3: 65536 envs + residual-TD3 (2x256 MLPs)",
+                       "envs_per_gpu": args.envs, "envs_per_group": args.envs_per_group,
+                       "hidden": args.hidden, "layers": args.layers, "batch": args.batch,
+                       "td3_epochs_per_step": args.updates,
+                       "update_to_data": args.updates * args.batch / args.envs,
+                       "parallelism": ("dp%d-shared-policy" % ws if args.shared_policy and ws > 1
+                                       else "independent-env-blocks x%d" % ws)},
+            "roofline": roof,
+            "step_kernel": step_k,
+            "step_kernel_sweep": sweep,
+            "kernels": {k: {"avg_us": round(v["avg_us"], 2), "launches_per_step":
+                            v["launches"] / 2, "ms_per_step": v["total_ms"] / 2}
+                        for k, v in breakdown.items()},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if ws > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

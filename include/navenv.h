@@ -1,0 +1,221 @@
+/*
+ * navenv.h — C-ABI of libnavenv.so, the MI355X (gfx950) drop-in for the reference's hot path:
+ * the Environment.step()/reset() simulator (environment.py) and the residual-TD3 agent's per-step
+ * math and learner (robot.py) of benmcclusky/Residual-TD3-Robot-Navigation.
+ *
+ * Conventions (all entry points):
+ *  - plain pointers and sizes only; every array pointer is DEVICE memory owned by the caller
+ *    (torch tensors on the Python side), except `nav_params` / `nav_mlp` descriptors, which are
+ *    host structs passed by pointer and copied into the launch;
+ *  - asynchronous on the given stream (a hipStream_t passed as void*; NULL = default stream);
+ *    no allocation, no synchronisation inside a launch function (graph-capturable);
+ *  - return 0 on success, NAV_EINVAL for a bad argument (checked on the host before any launch),
+ *    or -(hipError_t) when a launch fails; nothing aborts;
+ *  - one caller thread per stream; the library keeps no global mutable state.
+ *
+ * Reference interface each entry replaces is cited as file:line of /root/reference.
+ */
+#ifndef NAVENV_H
+#define NAVENV_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NAV_ABI_VERSION 1
+#define NAV_EINVAL (-100000)
+
+#define NAV_WORLD_CELLS 100 /* field = float32 [100][100][2] (speed, angle), x-major: cell cx*100+cy
+                              (environment.py:99-100 dynamics_speed / dynamics_angle interleaved) */
+#define NAV_HIST 5          /* STUCK_STEPS, robot.py:40 */
+#define NAV_ROW 8           /* replay row: s0 s1 a0 a1 r s'0 s'1 done (float32) */
+
+/* Philox4x32-10 stream tags (counter word 2). key = (seed_lo, seed_hi). */
+#define NAV_TAG_INIT 1   /* ctr = (draw, stream_id, 1, 0)     set_init_and_goal draws   */
+#define NAV_TAG_RESET 2  /* ctr = (0, env, 2, episode)        reset draw                */
+#define NAV_TAG_NOISE 3  /* ctr = (0, env, 3, step)           exploration noise pair    */
+#define NAV_TAG_SAMPLE 4 /* ctr = (i, 0, 4, update)           replay sample index       */
+#define NAV_TAG_TNOISE 5 /* ctr = (row, 0, 5, update)         target-smoothing noise    */
+
+/* Constants of constants.py / robot.py as a POD (defaults in nav_default_params). */
+typedef struct nav_params {
+    double world_size;       /* constants.py:6  WORLD_SIZE = 100 */
+    double max_action;       /* constants.py:34 ROBOT_MAX_ACTION = 5 */
+    double init_region_size; /* constants.py:25 INIT_REGION_SIZE = 25 */
+    double goal_threshold;   /* constants.py:50 TEST_DISTANCE_THRESHOLD = 5 (robot.py:744) */
+    double goal_reward;      /* robot.py:42 GOAL_REWARD = 50 */
+    double stuck_threshold;  /* robot.py:39 STUCK_THRESHOLD = 2 */
+    double stuck_penalty;    /* robot.py:41 STUCK_PENALTY = 50 */
+    double demo_factor;      /* robot.py:43 DEMO_PROXIMITY_FACTOR = 10 */
+    double noise_decay;      /* robot.py:33 NOISE_DECAY = 0.75 */
+    int32_t path_length0;    /* robot.py:28 PATH_LENGTH = 50 */
+    int32_t path_increase;   /* robot.py:29 PATH_INCREASE = 20 */
+    uint32_t seed_lo, seed_hi; /* configuration.py:26 RANDOM_SEED by default */
+    int32_t max_goal_draws;  /* cap on environment.py:131's rejection loop (default 65536) */
+} nav_params;
+
+/* Per-env state, structure-of-arrays, n envs (device). */
+typedef struct nav_env_soa {
+    int64_t n;
+    double* state;        /* [n][2]  Environment.robot_state (environment.py:96)           */
+    double* goal;         /* [n][2]  Environment.goal_state / Robot.goal_state              */
+    double* region;       /* [n][4]  Environment.robot_init_region (left,right,bottom,top)  */
+    double* hist;         /* [5][n][2] Robot.previous_states ring (robot.py:425, 509-538)   */
+    uint32_t* meta;       /* [n] bit0 goal_reached, bit1 stuck_flag, bit2 demo_flag,
+                             bits 8-10 history count, bits 12-14 history head              */
+    int32_t* plan_index;  /* [n] Robot.plan_index (robot.py:424) — value at the NEXT step   */
+    int32_t* path_length; /* [n] Robot.path_length (robot.py:423)                            */
+    int32_t* episodes;    /* [n] Robot.num_episodes (robot.py:421)                           */
+    double* noise_scale;  /* [n] Robot.current_noise_scale (robot.py:422)                    */
+} nav_env_soa;
+
+/* Per-step outputs of nav_agent_step (device, nullable fields noted). */
+typedef struct nav_step_out {
+    double* next_state;   /* [n][2] next state BEFORE any auto-reset (Environment.step return) */
+    double* goal_term;    /* [n] -||s'-goal|| (robot.py:741), consumed by nav_demo_reward      */
+    uint8_t* flags;       /* [n] bit0 done, bit1 goal, bit2 stuck, bit3 ended, bit4 demo term  */
+    float* block_stats;   /* nullable: [gridDim][8] = sum reward, n_done, n_goal, n_stuck,
+                             n_ended, 0, 0, 0 (wave shuffles -> LDS, one row per block)       */
+} nav_step_out;
+
+/* Replay ring (device): rows [capacity][8] float32 (robot.py:58-124 ReplayBuffer). */
+typedef struct nav_replay {
+    float* rows;
+    int64_t capacity;
+} nav_replay;
+
+/* ReLU MLP (robot.py:128-206) in the device layout: one flat fp32 buffer per network,
+ * hidden width padded to a multiple of 32 with zeros (exact: relu(0)=0, zero rows/cols add 0):
+ *   W0 [hp][d_in], b0 [hp], {Wl [hp][hp], bl [hp]} x (n_hidden-1), Wo [d_out][hp], bo [d_out]
+ * plus `packed` = per hidden->hidden layer: Wf [hp/4][hp][4] (Wf[q][n][j] = W[n][4q+j]) then
+ * Wb [hp/4][hp][4] (Wb[q][k][j] = W[4q+j][k]); kept current by nav_adam / nav_polyak /
+ * nav_mlp_pack. */
+typedef struct nav_mlp {
+    int32_t d_in;       /* 2 actor (robot.py:145), 4 critic (robot.py:185) */
+    int32_t d_out;      /* 2 actor, 1 critic */
+    int32_t hidden;     /* logical width: 200 reference, 256 perf config */
+    int32_t hidden_pad; /* multiple of 32, <= 256 */
+    int32_t n_hidden;   /* hidden layers: 3 reference, 2 perf config */
+    float* params;      /* flat, nav_mlp_param_count floats */
+    float* packed;      /* nav_mlp_packed_count floats (may be NULL only for n_hidden == 1) */
+} nav_mlp;
+
+/* ---- version / descriptors ---- */
+int nav_abi_version(void);
+void nav_default_params(nav_params* p);
+int64_t nav_mlp_param_count(int32_t d_in, int32_t d_out, int32_t hidden_pad, int32_t n_hidden);
+int64_t nav_mlp_packed_count(int32_t hidden_pad, int32_t n_hidden);
+/* float offset of layer l's W and b inside the flat buffer (l = 0 .. n_hidden) */
+int nav_mlp_layer_offsets(const nav_mlp* net, int32_t layer, int64_t* w_off, int64_t* b_off);
+
+/* ---- Environment (environment.py) ---- */
+/* environment.py:107-135 set_init_and_goal per env, Philox stream_id = env / envs_per_group (so a
+ * group shares region and goal); also initialises the Robot fields to their values at the first
+ * training step after the demonstration phase (robot.py:443-489 trace: plan_index 5, path 50,
+ * episodes 5, noise 1, demo_flag as given) and draws the first reset (environment.py:209-216).
+ * draws_out (nullable) [n]: goal draws used, 0 = rejection cap hit. */
+int nav_env_init(const nav_params* p, const nav_env_soa* env, int32_t envs_per_group,
+                 int32_t demo_flag, int32_t* draws_out, void* stream);
+/* environment.py:209-216 Environment.reset: state = low + (high-low)*u for envs with mask != 0
+ * (mask NULL = all). u from `uniforms` [n][2] if given (e.g. the numpy stream of robot-learning.py:19,
+ * for reference-stream parity) else Philox (NAV_TAG_RESET, episode = episodes[e]). */
+int nav_env_reset(const nav_params* p, const nav_env_soa* env, const uint8_t* mask,
+                  const double* uniforms, void* stream);
+/* environment.py:201-206 Environment.step for n envs: state <- dynamics(state, action) when the
+ * result is inside the world. action [n][2] f64. next_state (nullable) receives the result. */
+int nav_env_step(const nav_params* p, const nav_env_soa* env, const float* field,
+                 const double* action, double* next_state, void* stream);
+/* environment.py:177-198 Environment.dynamics, pure: out = f(state, action), n pairs. */
+int nav_dynamics(const float* field, const double* state, const double* action, double* out,
+                 int64_t n, void* stream);
+
+/* ---- Robot per-step (robot.py) ---- */
+/* One training tick for every env, fused: Environment.step (environment.py:201-206) ->
+ * Robot.process_transition (robot.py:645-675: reward w/o demo term, check_if_stuck, done, push
+ * to the replay row (replay_base + e) % capacity) -> next tick's end-of-episode check and
+ * Robot.reset + Environment.reset (robot.py:479-506, environment.py:209-216). */
+int nav_agent_step(const nav_params* p, const nav_env_soa* env, const float* field,
+                   const double* action, const nav_replay* replay,
+                   int64_t replay_base, const nav_step_out* out, void* stream);
+/* robot.py:741-762 demo-proximity term for envs flagged by nav_agent_step:
+ * r = (goal_term + demo_factor * -min_j ||s' - d_j||) - stuck_penalty*stuck, written to the
+ * replay row. demo_xy [m][2] f64 per group: group g = env / envs_per_group uses
+ * demo_xy[demo_off[g] .. demo_off[g+1]) (demo_off NULL = one shared set of m points). */
+int nav_demo_reward(const nav_params* p, int64_t n, const double* next_state,
+                    const double* goal_term, const uint8_t* flags, const double* demo_xy,
+                    const int64_t* demo_off, int64_t m, int32_t envs_per_group,
+                    const nav_replay* replay, int64_t replay_base, double* reward_out,
+                    void* stream);
+/* Pure robot.py:727-762 compute_reward for n next-states, f64 out; goal_hit (nullable) [n]
+ * receives the goal_reached side effect (robot.py:745). */
+int nav_compute_reward(const nav_params* p, int64_t n, const double* next_state,
+                       const double* goal, const double* demo_xy, int64_t m, int32_t demo_flag,
+                       double* reward, uint8_t* goal_hit, void* stream);
+
+/* ---- Actor / critic MLPs on MFMA (robot.py:128-206) ---- */
+/* Action selection, fused: residual = actor(f32(state - goal)) (robot.py:598-624) and the
+ * epilogue a = clip(b + residual + noise, +-max_action) (robot.py:541-569). mode 0 = training
+ * (noise = noise_scale*max_action*z; z from `noise_z` [n][2] f64 if given, else Philox
+ * NAV_TAG_NOISE at `step`), mode 1 = testing (robot.py:572-595, no noise). action_out [n][2] f64;
+ * residual_out (nullable) [n][2] f32. */
+int nav_act(const nav_params* p, const nav_mlp* actor, int64_t n, const double* state,
+            const double* goal, const double* noise_scale, const double* noise_z,
+            uint32_t step, int32_t mode, double* action_out, float* residual_out, void* stream);
+
+/* Generic forward of up to 2 networks sharing one input (twin critics), rows [M]:
+ * x = in[m*ld_in + in_col + 0..d_in) (f32). out_mode 0: out[m*ld_out + out_col + j] = y;
+ * out_mode 1 (target policy smoothing, robot.py:336-339): out = clamp(y + clamp(policy_noise*eps,
+ * +-noise_clip), +-max_action) with eps from `eps` [M][2] f32 if given else Philox
+ * (NAV_TAG_TNOISE, counter). acts (nullable per net): [n_hidden][M][hp] saved post-ReLU
+ * activations for the backward pass. */
+int nav_mlp_forward(const nav_mlp* nets, int32_t n_nets, int64_t M, const float* in,
+                    int32_t ld_in, int32_t in_col, float* const* out, int32_t ld_out,
+                    int32_t out_col, int32_t out_mode, const float* eps, float policy_noise,
+                    float noise_clip, float max_action, uint32_t seed_lo, uint32_t seed_hi,
+                    uint32_t counter, float* const* acts, void* stream);
+/* Row-local backward of one network: given dL/dy [M][d_out] and the saved activations, writes
+ * dZ [n_hidden][M][hp] (dL/d pre-activation per hidden layer) and, if dx != NULL, dL/dx [M][d_in]. */
+int nav_mlp_backward(const nav_mlp* net, int64_t M, const float* dy, const float* acts,
+                     float* dz, float* dx, void* stream);
+/* Weight gradients of one network as `splits` partial slabs [splits][param_count] (row range of
+ * split s = [s*M/splits, (s+1)*M/splits)); combine with nav_grad_reduce. */
+int nav_mlp_wgrad(const nav_mlp* net, int64_t M, const float* in, int32_t ld_in, int32_t in_col,
+                  const float* acts, const float* dz, const float* dy, float* slabs,
+                  int32_t splits, void* stream);
+int nav_grad_reduce(const float* slabs, int32_t splits, int64_t count, float* grad, void* stream);
+/* torch.optim.Adam step (robot.py:236-239; torch 2.10 single-tensor semantics) on a flat buffer,
+ * step_size = lr/(1-b1^t), bc2_sqrt = sqrt(1-b2^t) precomputed by the caller; refreshes `packed`
+ * of `net` (net->params must equal params). */
+int nav_adam(const nav_mlp* net, const float* grad, float* m, float* v, float beta1, float beta2,
+             float eps, float step_size, float bc2_sqrt, void* stream);
+/* robot.py:293-310 soft update target <- target*(1-tau) + source*tau, refreshing target packed. */
+int nav_polyak(const nav_mlp* target, const nav_mlp* source, float tau, void* stream);
+/* rebuild `packed` from `params` (after a host-side weight load). */
+int nav_mlp_pack(const nav_mlp* net, void* stream);
+
+/* ---- TD3 glue (robot.py:312-398) ---- */
+/* ReplayBuffer.sample (robot.py:98-115): batch[b] = rows[idx[b]] with idx from `idx` if given,
+ * else uniform with replacement over [0, size) from Philox (NAV_TAG_SAMPLE, counter). */
+int nav_replay_sample(const nav_replay* replay, int64_t size, int64_t B, const int64_t* idx,
+                      uint32_t seed_lo, uint32_t seed_hi, uint32_t counter, float* batch,
+                      void* stream);
+/* train_critic target and loss gradients (robot.py:341-353): y = r + gamma*min(q1t,q2t)*(1-d);
+ * dq_i = 2*(q_i - y)/B; loss_part [gridDim][2] partial sums of (q_i - y)^2 (nullable). */
+int nav_td3_critic_loss(int64_t B, const float* batch, const float* q1t, const float* q2t,
+                        const float* q1, const float* q2, float gamma, float* dq1, float* dq2,
+                        float* y_out, float* loss_part, void* stream);
+/* Build the critic input [B][4] = (s, a) from a batch [B][8]. */
+int nav_batch_sa(int64_t B, const float* batch, float* sa, void* stream);
+/* train_actor (robot.py:386-390): dL/dq = -1/B everywhere; and the actor's dL/da from the
+ * critic's dL/dx [B][4] (columns 2..3). */
+int nav_fill(float* x, int64_t n, float value, void* stream);
+int nav_strided_copy(const float* src, int32_t ld_src, int32_t col_src, float* dst, int32_t ld_dst,
+                     int32_t col_dst, int64_t rows, int32_t cols, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NAVENV_H */

@@ -408,14 +408,16 @@ void orc_vec_agent_step_batch(const orc_params_t* p, const float* speed, const f
                               const double* goal, const double* region, double* hist,
                               uint32_t* meta, int32_t* plan_index, int32_t* path_length,
                               int32_t* episodes, double* noise_scale, const double* action,
-                              double* next_out, float* rows, int64_t cap, int64_t base) {
+                              double* next_out, float* rows, int64_t cap, int64_t base,
+                              int64_t env0) {
     /* hist here is [n][5][2] (env-major; the device layout differs, the values do not) */
 #ifdef _OPENMP
 #pragma omp parallel for schedule(static)
 #endif
     for (int64_t e = 0; e < n; ++e) {
         int64_t slot = (base + e) % cap;
-        orc_vec_agent_tick(p, speed, angle, demo, m, (uint32_t)e, state + 2 * e, goal + 2 * e,
+        orc_vec_agent_tick(p, speed, angle, demo, m, (uint32_t)(env0 + e), state + 2 * e,
+                           goal + 2 * e,
                            region + 4 * e, hist + 10 * e, meta + e, plan_index + e,
                            path_length + e, episodes + e, noise_scale + e, action + 2 * e,
                            next_out + 2 * e, rows + 8 * slot, NULL, NULL);

@@ -112,7 +112,7 @@ void orc_vec_agent_step_batch(const orc_params_t* p, const float* speed, const f
                               uint32_t* meta, int32_t* plan_index, int32_t* path_length,
                               int32_t* episodes, double* noise_scale, const double* action,
                               double* next_state_out, float* replay_rows, int64_t replay_cap,
-                              int64_t replay_base);
+                              int64_t replay_base, int64_t env0 /* global index of env 0 */);
 
 #ifdef __cplusplus
 }

@@ -85,7 +85,8 @@ def lib():
         L.orc_threads.restype = C.c_int
         L.orc_vec_agent_step_batch.argtypes = [C.POINTER(Params), _fp, _fp, _dp, C.c_int64,
                                                C.c_int64, _dp, _dp, _dp, _dp, _u32p, _i32p, _i32p,
-                                               _i32p, _dp, _dp, _dp, _fp, C.c_int64, C.c_int64]
+                                               _i32p, _dp, _dp, _dp, _fp, C.c_int64, C.c_int64,
+                                               C.c_int64]
         _lib = L
     return _lib
 
@@ -254,7 +255,7 @@ class VecAgentState:
             ptr(row, _fp), C.byref(r), None if rs is None else ptr(rs, _dp))
         return flags, ns, row, r.value
 
-    def step_batch(self, p, speed, angle, demo, action, rows, base):
+    def step_batch(self, p, speed, angle, demo, action, rows, base, env0=0):
         demo = np.ascontiguousarray(demo, np.float64).reshape(-1, 2)
         ns = np.zeros((self.n, 2))
         lib().orc_vec_agent_step_batch(
@@ -263,5 +264,5 @@ class VecAgentState:
             ptr(self.hist, _dp), ptr(self.meta, _u32p), ptr(self.plan_index, _i32p),
             ptr(self.path_length, _i32p), ptr(self.episodes, _i32p), ptr(self.noise_scale, _dp),
             ptr(np.ascontiguousarray(action, np.float64), _dp), ptr(ns, _dp), ptr(rows, _fp),
-            rows.shape[0], base)
+            rows.shape[0], base, env0)
         return ns

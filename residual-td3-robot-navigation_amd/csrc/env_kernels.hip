@@ -1,0 +1,466 @@
+// env_kernels.hip — the vectorised Environment (environment.py) and the Robot's per-step tick
+// (robot.py) as gfx950 kernels: one env per lane, structure-of-arrays state in HBM, f64 state
+// math (the reference's robot_state is float64), reward/done counts reduced per block through
+// wave shuffles and LDS.
+#include "nav_device.h"
+
+using namespace nav;
+
+namespace {
+
+constexpr uint32_t M_GOAL = 1u, M_STUCK = 2u, M_DEMO = 4u;
+constexpr uint8_t F_DONE = 1, F_GOAL = 2, F_STUCK = 4, F_ENDED = 8, F_DEMO = 16;
+
+NAV_DEV void region_of(int r, double u, double* reg) {
+    // environment.py:108-128 (left, right, bottom, top)
+    const double W = 100.0, S = 25.0;
+    const double v = 0.0 + (W - S - 0.0) * u;
+    double l, rr, b, t;
+    if (r == 0) { l = 0.0; rr = S; b = v; t = b + S; }
+    else if (r == 1) { l = v; rr = l + S; b = W - S; t = W; }
+    else if (r == 2) { l = W - S; rr = W; b = v; t = b + S; }
+    else { l = v; rr = l + S; b = 0.0; t = S; }
+    reg[0] = l; reg[1] = rr; reg[2] = b; reg[3] = t;
+}
+
+__global__ __launch_bounds__(kBlock) void k_env_init(nav_params p, nav_env_soa env, int32_t epg,
+                                                     int32_t demo_flag, int32_t* draws_out) {
+    const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (e >= env.n) return;
+    const uint32_t sid = (uint32_t)(e / epg);
+    // environment.py:107-135 on the Philox stream (NAV_TAG_INIT, stream id)
+    uint4 w = philox(0u, sid, NAV_TAG_INIT, 0u, p.seed_lo, p.seed_hi);
+    double reg[4];
+    region_of((int)(w.x & 3u), u01(w.z, w.w), reg);
+    const double mx = 0.5 * (reg[0] + reg[1]), my = 0.5 * (reg[2] + reg[3]);
+    double gx = 0.0, gy = 0.0;
+    int32_t used = 0;
+    for (int k = 1; k <= p.max_goal_draws; ++k) {
+        w = philox((uint32_t)k, sid, NAV_TAG_INIT, 0u, p.seed_lo, p.seed_hi);
+        gx = 5.0 + 90.0 * u01(w.x, w.y);
+        gy = 5.0 + 90.0 * u01(w.z, w.w);
+        if (norm2(gx - mx, gy - my) >= 90.0) { used = k; break; }
+    }
+    reinterpret_cast<double2*>(env.goal)[e] = make_double2(gx, gy);
+    double4* rg = reinterpret_cast<double4*>(env.region);
+    rg[e] = make_double4(reg[0], reg[1], reg[2], reg[3]);
+    // Robot state at the first training step after 3 demos (robot.py:443-489 trace)
+    const int32_t ep0 = 5;
+    env.plan_index[e] = 5;
+    env.path_length[e] = p.path_length0;
+    env.episodes[e] = ep0;
+    env.noise_scale[e] = 1.0;  // robot.py:32 INITIAL_NOISE
+    env.meta[e] = demo_flag ? M_DEMO : 0u;
+    // environment.py:209-216 first reset on the reset stream of this env
+    w = philox(0u, (uint32_t)e, NAV_TAG_RESET, (uint32_t)ep0, p.seed_lo, p.seed_hi);
+    reinterpret_cast<double2*>(env.state)[e] = region_sample(reg, u01(w.x, w.y), u01(w.z, w.w));
+    if (draws_out) draws_out[e] = used;
+}
+
+__global__ __launch_bounds__(kBlock) void k_env_reset(nav_params p, nav_env_soa env,
+                                                      const uint8_t* mask, const double2* uni) {
+    const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (e >= env.n) return;
+    if (mask && !mask[e]) return;
+    double u0, u1;
+    if (uni) {
+        const double2 u = uni[e];
+        u0 = u.x; u1 = u.y;
+    } else {
+        const uint4 w = philox(0u, (uint32_t)e, NAV_TAG_RESET, (uint32_t)env.episodes[e],
+                               p.seed_lo, p.seed_hi);
+        u0 = u01(w.x, w.y); u1 = u01(w.z, w.w);
+    }
+    const double4 r = reinterpret_cast<const double4*>(env.region)[e];
+    const double reg[4] = {r.x, r.y, r.z, r.w};
+    reinterpret_cast<double2*>(env.state)[e] = region_sample(reg, u0, u1);
+}
+
+__global__ __launch_bounds__(kBlock) void k_env_step(int64_t n, double2* __restrict__ state,
+                                                     const float2* __restrict__ field,
+                                                     const double2* __restrict__ action,
+                                                     double2* __restrict__ next_out) {
+    // environment.py:201-206: 16 B state in, 16 B action in, 16 B state out per env
+    const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (e >= n) return;
+    const double2 s = state[e];
+    const double2 nx = dynamics(field, s, action[e]);
+    const bool ok = in_world(nx);
+    if (ok) state[e] = nx;
+    if (next_out) next_out[e] = ok ? nx : s;
+}
+
+__global__ __launch_bounds__(kBlock) void k_dynamics(int64_t n, const float2* __restrict__ field,
+                                                     const double2* __restrict__ s,
+                                                     const double2* __restrict__ a,
+                                                     double2* __restrict__ out) {
+    const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (e >= n) return;
+    out[e] = dynamics(field, s[e], a[e]);
+}
+
+// One training tick per env (see navenv.h nav_agent_step).
+__global__ __launch_bounds__(kBlock) void k_agent_step(nav_params p, nav_env_soa env,
+                                                       const float2* __restrict__ field,
+                                                       const double2* __restrict__ action,
+                                                       float4* __restrict__ rows, int64_t cap,
+                                                       int64_t base, nav_step_out out) {
+    const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    float st_r = 0.f, st_done = 0.f, st_goal = 0.f, st_stuck = 0.f, st_end = 0.f;
+    if (e < env.n) {
+        double2* state = reinterpret_cast<double2*>(env.state);
+        double2* hist = reinterpret_cast<double2*>(env.hist);
+        const double2 s = state[e];
+        const double2 a = action[e];
+        const double2 g = reinterpret_cast<const double2*>(env.goal)[e];
+        uint32_t meta = env.meta[e];
+        int32_t plan = env.plan_index[e];
+        const int32_t path = env.path_length[e];
+
+        // environment.py:201-206
+        double2 ns = dynamics(field, s, a);
+        if (!in_world(ns)) ns = s;
+
+        // robot.py:727-762 (demo term added by nav_demo_reward when flagged)
+        bool goal_reached = (meta & M_GOAL) != 0;
+        const double gt = -norm2(ns.x - g.x, ns.y - g.y);
+        double r;
+        bool demo_term = false;
+        if (gt >= -p.goal_threshold) {
+            goal_reached = true;
+            r = p.goal_reward;
+        } else {
+            r = gt;
+            demo_term = (meta & M_DEMO) != 0;
+        }
+
+        // robot.py:509-538 check_if_stuck on the pre-step state; ring of 5 in hist [5][n]
+        int cnt = (int)((meta >> 8) & 7u), head = (int)((meta >> 12) & 7u);
+        bool stuck = false;
+        if (cnt >= NAV_HIST) {
+            bool all = true;
+#pragma unroll
+            for (int k = 0; k < NAV_HIST; ++k) {
+                const double2 h = hist[(int64_t)k * env.n + e];
+                const double d = norm2(s.x - h.x, s.y - h.y);
+                all = all && (d < p.stuck_threshold);
+            }
+            if (all) {
+                stuck = true;
+                cnt = 0;
+            } else {
+                head = head == NAV_HIST - 1 ? 0 : head + 1;
+                cnt -= 1;
+            }
+        }
+        {
+            int slot = head + cnt;
+            if (slot >= NAV_HIST) slot -= NAV_HIST;
+            hist[(int64_t)slot * env.n + e] = s;
+            cnt += 1;
+        }
+        bool stuck_flag = (meta & M_STUCK) != 0;
+        if (stuck) {
+            stuck_flag = true;
+            if (!demo_term) r -= p.stuck_penalty;
+        }
+        const bool done = plan == path - 1;  // robot.py:672
+
+        // ReplayBuffer.push (robot.py:79-96) as one 32-B row
+        const int64_t slot = (base + e) % cap;
+        rows[2 * slot] = make_float4((float)s.x, (float)s.y, (float)a.x, (float)a.y);
+        rows[2 * slot + 1] = make_float4((float)r, (float)ns.x, (float)ns.y, done ? 1.f : 0.f);
+
+        // next tick: robot.py:479-487 end check -> Robot.reset (492-506) + Environment.reset
+        const bool ended = done || goal_reached || stuck_flag;
+        const uint32_t dflag = meta & M_DEMO;
+        if (ended) {
+            const int32_t ep = env.episodes[e] + 1;
+            env.episodes[e] = ep;
+            env.path_length[e] = path + p.path_increase;
+            env.noise_scale[e] = env.noise_scale[e] * p.noise_decay;
+            plan = 1;  // Robot.reset sets 0, the next tick's increment makes it 1
+            goal_reached = false;
+            stuck_flag = false;
+            const uint4 w = philox(0u, (uint32_t)e, NAV_TAG_RESET, (uint32_t)ep, p.seed_lo,
+                                   p.seed_hi);
+            const double4 rg = reinterpret_cast<const double4*>(env.region)[e];
+            const double reg[4] = {rg.x, rg.y, rg.z, rg.w};
+            state[e] = region_sample(reg, u01(w.x, w.y), u01(w.z, w.w));
+        } else {
+            plan += 1;
+            state[e] = ns;
+        }
+        env.plan_index[e] = plan;
+        env.meta[e] = (goal_reached ? M_GOAL : 0u) | (stuck_flag ? M_STUCK : 0u) | dflag |
+                      ((uint32_t)cnt << 8) | ((uint32_t)head << 12);
+        if (out.next_state) reinterpret_cast<double2*>(out.next_state)[e] = ns;
+        if (out.goal_term) out.goal_term[e] = gt;
+        if (out.flags)
+            out.flags[e] = (uint8_t)((done ? F_DONE : 0) | (gt >= -p.goal_threshold ? F_GOAL : 0) |
+                                     (stuck ? F_STUCK : 0) | (ended ? F_ENDED : 0) |
+                                     (demo_term ? F_DEMO : 0));
+        st_r = (float)r;
+        st_done = done ? 1.f : 0.f;
+        st_goal = gt >= -p.goal_threshold ? 1.f : 0.f;
+        st_stuck = stuck ? 1.f : 0.f;
+        st_end = ended ? 1.f : 0.f;
+    }
+    if (out.block_stats) {
+        // per-block reduction: wave shuffles -> LDS -> one 32-B row per block (deterministic)
+        __shared__ float part[kBlock / 64][5];
+        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+        const float v0 = wave_sum(st_r), v1 = wave_sum(st_done), v2 = wave_sum(st_goal);
+        const float v3 = wave_sum(st_stuck), v4 = wave_sum(st_end);
+        if (lane == 0) {
+            part[wv][0] = v0; part[wv][1] = v1; part[wv][2] = v2; part[wv][3] = v3;
+            part[wv][4] = v4;
+        }
+        __syncthreads();
+        if (threadIdx.x < 8) {
+            float acc = 0.f;
+            if (threadIdx.x < 5)
+                for (int w = 0; w < kBlock / 64; ++w) acc += part[w][threadIdx.x];
+            out.block_stats[(int64_t)blockIdx.x * 8 + threadIdx.x] = acc;
+        }
+    }
+}
+
+// robot.py:753 demo-proximity min distance; points staged through LDS in chunks and read by
+// broadcast (every lane of the block reads the same point). f64 math as scipy's cdist.
+constexpr int kDemoChunk = 2048;
+
+NAV_DEV double demo_min_global(const double2* __restrict__ d, int64_t m, double x, double y) {
+    double best = __builtin_inf();
+    for (int64_t j = 0; j < m; ++j) {
+        const double2 q = d[j];
+        const double dx = x - q.x, dy = y - q.y;
+        const double v = dx * dx + dy * dy;
+        best = v < best ? v : best;
+    }
+    return best;
+}
+
+__global__ __launch_bounds__(kBlock) void k_demo_reward(nav_params p, int64_t n,
+                                                        const double2* __restrict__ ns,
+                                                        const double* __restrict__ gterm,
+                                                        const uint8_t* __restrict__ flags,
+                                                        const double2* __restrict__ demo,
+                                                        const int64_t* __restrict__ off,
+                                                        int64_t m_shared, int32_t epg,
+                                                        float* __restrict__ rows, int64_t cap,
+                                                        int64_t base, double* reward_out) {
+    __shared__ double2 pts[kDemoChunk];
+    const int64_t e0 = (int64_t)blockIdx.x * kBlock;
+    const int64_t e = e0 + threadIdx.x;
+    const bool live = e < n;
+    const uint8_t f = live ? flags[e] : 0;
+    const bool want = live && (f & F_DEMO);
+    double x = 0.0, y = 0.0;
+    if (live) {
+        const double2 s = ns[e];
+        x = s.x; y = s.y;
+    }
+    // group range of this env, and whether the whole block shares it
+    const int64_t last = (e0 + kBlock - 1 < n ? e0 + kBlock - 1 : n - 1);
+    const int64_t g0 = off ? e0 / epg : 0, g1 = off ? last / epg : 0;
+    double best = __builtin_inf();
+    if (g0 == g1) {
+        const int64_t lo = off ? off[g0] : 0, hi = off ? off[g0 + 1] : m_shared;
+        const int any = __syncthreads_or(want ? 1 : 0);
+        if (any) {
+            for (int64_t c = lo; c < hi; c += kDemoChunk) {
+                const int cn = (int)(hi - c < kDemoChunk ? hi - c : kDemoChunk);
+                __syncthreads();
+                for (int i = threadIdx.x; i < cn; i += kBlock) pts[i] = demo[c + i];
+                __syncthreads();
+                if (want) {
+                    int j = 0;
+                    double b0 = best, b1 = __builtin_inf();
+                    for (; j + 1 < cn; j += 2) {
+                        const double2 q0 = pts[j], q1 = pts[j + 1];
+                        const double dx0 = x - q0.x, dy0 = y - q0.y;
+                        const double dx1 = x - q1.x, dy1 = y - q1.y;
+                        const double v0 = dx0 * dx0 + dy0 * dy0;
+                        const double v1 = dx1 * dx1 + dy1 * dy1;
+                        b0 = v0 < b0 ? v0 : b0;
+                        b1 = v1 < b1 ? v1 : b1;
+                    }
+                    if (j < cn) {
+                        const double2 q0 = pts[j];
+                        const double dx0 = x - q0.x, dy0 = y - q0.y;
+                        const double v0 = dx0 * dx0 + dy0 * dy0;
+                        b0 = v0 < b0 ? v0 : b0;
+                    }
+                    best = b0 < b1 ? b0 : b1;
+                }
+            }
+        }
+    } else if (want) {
+        const int64_t g = e / epg;
+        best = demo_min_global(demo + off[g], off[g + 1] - off[g], x, y);
+    }
+    if (!want) return;
+    // robot.py:756-760 then the stuck penalty of robot.py:667-669
+    const double mn = sqrt(best);
+    double r = gterm[e] + p.demo_factor * (-mn);
+    if (f & F_STUCK) r -= p.stuck_penalty;
+    const int64_t slot = (base + e) % cap;
+    rows[slot * NAV_ROW + 4] = (float)r;
+    if (reward_out) reward_out[e] = r;
+}
+
+__global__ __launch_bounds__(kBlock) void k_compute_reward(nav_params p, int64_t n,
+                                                           const double2* __restrict__ ns,
+                                                           const double2* __restrict__ goal,
+                                                           const double2* __restrict__ demo,
+                                                           int64_t m, int32_t demo_flag,
+                                                           double* reward, uint8_t* hit) {
+    const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (e >= n) return;
+    const double2 s = ns[e], g = goal[e];
+    const double gt = -norm2(s.x - g.x, s.y - g.y);
+    double r;
+    uint8_t h = 0;
+    if (gt >= -p.goal_threshold) {
+        r = p.goal_reward;
+        h = 1;
+    } else if (m == 0) {
+        r = gt;
+    } else {
+        const double mn = sqrt(demo_min_global(demo, m, s.x, s.y));
+        r = gt + p.demo_factor * (demo_flag ? -mn : 0.0);
+    }
+    reward[e] = r;
+    if (hit) hit[e] = h;
+}
+
+inline int blocks_for(int64_t n) { return (int)((n + kBlock - 1) / kBlock); }
+inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+}  // namespace
+
+extern "C" {
+
+int nav_abi_version(void) { return NAV_ABI_VERSION; }
+
+void nav_default_params(nav_params* p) {
+    if (!p) return;
+    p->world_size = 100.0;
+    p->max_action = 5.0;
+    p->init_region_size = 25.0;
+    p->goal_threshold = 5.0;
+    p->goal_reward = 50.0;
+    p->stuck_threshold = 2.0;
+    p->stuck_penalty = 50.0;
+    p->demo_factor = 10.0;
+    p->noise_decay = 0.75;
+    p->path_length0 = 50;
+    p->path_increase = 20;
+    p->seed_lo = 1707366464u;
+    p->seed_hi = 0u;
+    p->max_goal_draws = 1 << 16;
+}
+
+static bool env_ok(const nav_env_soa* e) {
+    return e && e->n >= 0 && e->n < (int64_t)1 << 31 && (e->n == 0 || (e->state && e->goal &&
+           e->region && e->hist && e->meta && e->plan_index && e->path_length && e->episodes &&
+           e->noise_scale));
+}
+
+int nav_env_init(const nav_params* p, const nav_env_soa* env, int32_t epg, int32_t demo_flag,
+                 int32_t* draws_out, void* stream) {
+    if (!p || !env_ok(env) || epg <= 0 || p->max_goal_draws <= 0) return NAV_EINVAL;
+    if (env->n == 0) return 0;
+    hipLaunchKernelGGL(k_env_init, dim3(blocks_for(env->n)), dim3(kBlock), 0, S(stream), *p, *env,
+                       epg, demo_flag, draws_out);
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_env_reset(const nav_params* p, const nav_env_soa* env, const uint8_t* mask,
+                  const double* uniforms, void* stream) {
+    if (!p || !env_ok(env)) return NAV_EINVAL;
+    if (env->n == 0) return 0;
+    hipLaunchKernelGGL(k_env_reset, dim3(blocks_for(env->n)), dim3(kBlock), 0, S(stream), *p,
+                       *env, mask, reinterpret_cast<const double2*>(uniforms));
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_env_step(const nav_params* p, const nav_env_soa* env, const float* field,
+                 const double* action, double* next_state, void* stream) {
+    if (!p || !env || env->n < 0 || !field || (env->n && (!env->state || !action)))
+        return NAV_EINVAL;
+    if (env->n == 0) return 0;
+    hipLaunchKernelGGL(k_env_step, dim3(blocks_for(env->n)), dim3(kBlock), 0, S(stream), env->n,
+                       reinterpret_cast<double2*>(env->state),
+                       reinterpret_cast<const float2*>(field),
+                       reinterpret_cast<const double2*>(action),
+                       reinterpret_cast<double2*>(next_state));
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_dynamics(const float* field, const double* state, const double* action, double* out,
+                 int64_t n, void* stream) {
+    if (n < 0 || (n && (!field || !state || !action || !out))) return NAV_EINVAL;
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_dynamics, dim3(blocks_for(n)), dim3(kBlock), 0, S(stream), n,
+                       reinterpret_cast<const float2*>(field),
+                       reinterpret_cast<const double2*>(state),
+                       reinterpret_cast<const double2*>(action), reinterpret_cast<double2*>(out));
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_agent_step(const nav_params* p, const nav_env_soa* env, const float* field,
+                   const double* action, const nav_replay* replay, int64_t replay_base,
+                   const nav_step_out* out, void* stream) {
+    if (!p || !env_ok(env) || !field || !action || !replay || !replay->rows ||
+        replay->capacity <= 0 || replay_base < 0 || !out)
+        return NAV_EINVAL;
+    if (env->n == 0) return 0;
+    hipLaunchKernelGGL(k_agent_step, dim3(blocks_for(env->n)), dim3(kBlock), 0, S(stream), *p,
+                       *env, reinterpret_cast<const float2*>(field),
+                       reinterpret_cast<const double2*>(action),
+                       reinterpret_cast<float4*>(replay->rows), replay->capacity,
+                       replay_base % replay->capacity, *out);
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_demo_reward(const nav_params* p, int64_t n, const double* next_state,
+                    const double* goal_term, const uint8_t* flags, const double* demo_xy,
+                    const int64_t* demo_off, int64_t m, int32_t epg, const nav_replay* replay,
+                    int64_t replay_base, double* reward_out, void* stream) {
+    if (!p || n < 0 || !replay || !replay->rows || replay->capacity <= 0 || replay_base < 0)
+        return NAV_EINVAL;
+    if (n && (!next_state || !goal_term || !flags)) return NAV_EINVAL;
+    if (demo_off && epg <= 0) return NAV_EINVAL;
+    if (!demo_off && m > 0 && !demo_xy) return NAV_EINVAL;
+    if (n == 0 || (!demo_off && m == 0)) return 0;
+    hipLaunchKernelGGL(k_demo_reward, dim3(blocks_for(n)), dim3(kBlock), 0, S(stream), *p, n,
+                       reinterpret_cast<const double2*>(next_state), goal_term, flags,
+                       reinterpret_cast<const double2*>(demo_xy), demo_off, m, epg > 0 ? epg : 1,
+                       replay->rows, replay->capacity, replay_base % replay->capacity,
+                       reward_out);
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_compute_reward(const nav_params* p, int64_t n, const double* next_state,
+                       const double* goal, const double* demo_xy, int64_t m, int32_t demo_flag,
+                       double* reward, uint8_t* goal_hit, void* stream) {
+    if (!p || n < 0 || m < 0 || (n && (!next_state || !goal || !reward)) || (m && !demo_xy))
+        return NAV_EINVAL;
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_compute_reward, dim3(blocks_for(n)), dim3(kBlock), 0, S(stream), *p, n,
+                       reinterpret_cast<const double2*>(next_state),
+                       reinterpret_cast<const double2*>(goal),
+                       reinterpret_cast<const double2*>(demo_xy), m, demo_flag, reward, goal_hit);
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,972 @@
+// mlp_kernels.hip — the residual-TD3 actor/critic MLPs (robot.py:128-206) and their learner
+// (robot.py:209-398) on gfx950.
+//
+// Forward / row-backward: one 256-thread workgroup = 4 waves = 128 rows; each wave owns 32 rows
+// and keeps them in LDS (fp32, row stride hp+4 so b128 fragment reads are conflict-free) across
+// all layers. Hidden x hidden layers run on v_mfma_f32_32x32x2_f32 (exact fp32): A fragments
+// from the wave's LDS rows, B fragments from an LDS-staged, double-buffered 8-deep K chunk of the
+// pre-packed weight image (one barrier per chunk). The thin input layer (K = 2 or 4) and output
+// layer (N = 1 or 2) run on the VALU. Weight gradients: a split-M MFMA kernel writing partial
+// slabs (deterministic), reduced in a fixed order.
+#include "nav_device.h"
+
+using namespace nav;
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kMaxLayers = 9;
+constexpr int TM = 128;  // rows per workgroup
+
+struct MlpDev {
+    const float* params;
+    const float* packed;
+    int d_in, d_out, hp, n_hidden;
+    int64_t count;
+    int64_t w_off[kMaxLayers], b_off[kMaxLayers];
+};
+
+inline int64_t r4(int64_t x) { return (x + 3) & ~(int64_t)3; }
+
+bool make_dev(const nav_mlp* n, MlpDev* d) {
+    if (!n || n->d_in < 1 || n->d_in > 4 || n->d_out < 1 || n->d_out > 2 || n->hidden_pad < 32 ||
+        n->hidden_pad > 256 || (n->hidden_pad & 31) || n->n_hidden < 1 ||
+        n->n_hidden >= kMaxLayers || !n->params || (n->n_hidden > 1 && !n->packed) ||
+        n->hidden < 1 || n->hidden > n->hidden_pad)
+        return false;
+    const int hp = n->hidden_pad;
+    d->params = n->params;
+    d->packed = n->packed;
+    d->d_in = n->d_in;
+    d->d_out = n->d_out;
+    d->hp = hp;
+    d->n_hidden = n->n_hidden;
+    int64_t o = 0;
+    for (int l = 0; l <= n->n_hidden; ++l) {
+        const int64_t in = l == 0 ? n->d_in : hp, out = l == n->n_hidden ? n->d_out : hp;
+        d->w_off[l] = o;
+        o += r4(in * out);
+        d->b_off[l] = o;
+        o += r4(out);
+    }
+    d->count = o;
+    return true;
+}
+
+inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+NAV_DEV f32x16 mfma(float a, float b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// acc[t] += A[32 rows of the wave][hp] * B[hp][32t .. 32t+32), B from a packed image
+// [hp/4][hp][4] (element (k, n) at ((k>>2)*hp + n)*4 + (k&3)). The k order inside a chunk is
+// permuted consistently for A and B (lane half h takes k = 8q + 4h + s at MFMA s).
+template <int NT>
+NAV_DEV void gemm_rows(const float* __restrict__ A, int S_, const float* __restrict__ Bp,
+                       float* __restrict__ wbuf, f32x16 (&acc)[NT]) {
+    constexpr int hp = NT * 32;
+    constexpr int CH = 8 * hp;          // floats per chunk (2 quads)
+    constexpr int nq = hp / 8;
+    constexpr int PER = (2 * hp + kBlock - 1) / kBlock;  // float4 per thread per chunk
+    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+        for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+    float4 st[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int i = tid + kBlock * j;
+        if (i < 2 * hp) st[j] = reinterpret_cast<const float4*>(Bp)[i];
+    }
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int i = tid + kBlock * j;
+        if (i < 2 * hp) reinterpret_cast<float4*>(wbuf)[i] = st[j];
+    }
+    __syncthreads();
+    const float* arow = A + l32 * S_ + 4 * h;
+    for (int q = 0; q < nq; ++q) {
+        if (q + 1 < nq) {
+#pragma unroll
+            for (int j = 0; j < PER; ++j) {
+                const int i = tid + kBlock * j;
+                if (i < 2 * hp) st[j] = reinterpret_cast<const float4*>(Bp + (q + 1) * CH)[i];
+            }
+        }
+        const float* wb = wbuf + (q & 1) * CH + (h * hp + l32) * 4;
+        const float4 av = *reinterpret_cast<const float4*>(arow + 8 * q);
+        float4 bv[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) bv[t] = *reinterpret_cast<const float4*>(wb + 128 * t);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = mfma(av.x, bv[t].x, acc[t]);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = mfma(av.y, bv[t].y, acc[t]);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = mfma(av.z, bv[t].z, acc[t]);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = mfma(av.w, bv[t].w, acc[t]);
+        if (q + 1 < nq) {
+            float* nb = wbuf + ((q + 1) & 1) * CH;
+#pragma unroll
+            for (int j = 0; j < PER; ++j) {
+                const int i = tid + kBlock * j;
+                if (i < 2 * hp) reinterpret_cast<float4*>(nb)[i] = st[j];
+            }
+        }
+        __syncthreads();
+    }
+}
+
+NAV_DEV int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
+
+enum { IN_F32 = 0, IN_BASELINE = 1 };
+enum { OUT_F32 = 0, OUT_TARGET = 1, OUT_ACT = 2 };
+
+struct FwdArgs {
+    MlpDev net[2];
+    int64_t M;
+    const float* in;
+    int ld_in, in_col;
+    float* out[2];
+    int ld_out, out_col;
+    float* acts[2];
+    // OUT_TARGET
+    const float* eps;
+    float policy_noise, noise_clip, max_action;
+    uint32_t seed_lo, seed_hi, counter;
+    // IN_BASELINE / OUT_ACT
+    const double* state;
+    const double* goal;
+    const double* noise_scale;
+    const double* noise_z;
+    uint32_t step;
+    int act_mode;
+    double max_action_d;
+    double* action_out;
+};
+
+NAV_DEV size_t lds_floats(int hp) { return (size_t)TM * (hp + 4) + 16 * hp + 512; }
+inline size_t lds_bytes(int hp) { return ((size_t)TM * (hp + 4) + 16 * hp + 512) * 4; }
+
+template <int NT, int IN_MODE, int OUT_MODE>
+__global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    constexpr int hp = NT * 32, SS = hp + 4;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, l32 = lane & 31;
+    const MlpDev& net = a.net[blockIdx.y];
+    float* act_save = a.acts[blockIdx.y];
+    const int64_t M = a.M;
+    const int64_t row0 = (int64_t)blockIdx.x * TM + wv * 32;
+    float* wbuf = smem + TM * SS;
+    float* xin = wbuf + 16 * hp + wv * 128;
+    float* my = smem + wv * 32 * SS;
+    const int d_in = net.d_in, d_out = net.d_out, nh = net.n_hidden;
+
+    // ---- input rows -> xin[32][4]
+    if (lane < 32) {
+        const int64_t r = row0 + lane;
+        float x[4] = {0.f, 0.f, 0.f, 0.f};
+        if (r < M) {
+            if (IN_MODE == IN_F32) {
+                const float* src = a.in + r * a.ld_in + a.in_col;
+                for (int k = 0; k < d_in; ++k) x[k] = src[k];
+            } else {
+                // robot.py:556 baseline = state - goal, then torch.FloatTensor (f64 -> f32)
+                const double2 s = reinterpret_cast<const double2*>(a.state)[r];
+                const double2 g = reinterpret_cast<const double2*>(a.goal)[r];
+                x[0] = (float)(s.x - g.x);
+                x[1] = (float)(s.y - g.y);
+            }
+        }
+        *reinterpret_cast<float4*>(xin + lane * 4) = make_float4(x[0], x[1], x[2], x[3]);
+    }
+    __syncthreads();
+
+    // ---- layer 0 (K = d_in) on the VALU
+    {
+        const float* W0 = net.params + net.w_off[0];
+        const float* b0 = net.params + net.b_off[0];
+        for (int c = lane; c < hp; c += 64) {
+            float w[4] = {0.f, 0.f, 0.f, 0.f};
+            for (int k = 0; k < d_in; ++k) w[k] = W0[c * d_in + k];
+            const float b = b0[c];
+            for (int r = 0; r < 32; ++r) {
+                const float4 x = *reinterpret_cast<const float4*>(xin + r * 4);
+                float v = b;
+                v = fmaf(x.x, w[0], v);
+                if (d_in > 1) v = fmaf(x.y, w[1], v);
+                if (d_in > 2) v = fmaf(x.z, w[2], v);
+                if (d_in > 3) v = fmaf(x.w, w[3], v);
+                v = fmaxf(v, 0.f);
+                my[r * SS + c] = v;
+                if (act_save && row0 + r < M) act_save[(row0 + r) * hp + c] = v;
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- hidden x hidden layers on MFMA
+    for (int L = 1; L < nh; ++L) {
+        f32x16 acc[NT];
+        gemm_rows<NT>(my, SS, net.packed + (int64_t)(L - 1) * 2 * hp * hp, wbuf, acc);
+        const float* bL = net.params + net.b_off[L];
+        float* save = act_save ? act_save + (int64_t)L * M * hp : nullptr;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int c = 32 * t + l32;
+            const float b = bL[c];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int r = acc_row(i, h);
+                const float v = fmaxf(acc[t][i] + b, 0.f);
+                my[r * SS + c] = v;
+                if (save && row0 + r < M) save[(row0 + r) * hp + c] = v;
+            }
+        }
+        __syncthreads();
+    }
+
+    // ---- output layer (N = d_out <= 2) on the VALU: lane = (row l32, output h)
+    const int64_t r = row0 + l32;
+    const int j = h;
+    float y = 0.f;
+    if (j < d_out) {
+        const float* Wo = net.params + net.w_off[nh] + j * hp;
+        const float* ar = my + l32 * SS;
+        float acc0 = 0.f, acc1 = 0.f;
+        for (int k = 0; k < hp; k += 8) {
+            const float4 x0 = *reinterpret_cast<const float4*>(ar + k);
+            const float4 x1 = *reinterpret_cast<const float4*>(ar + k + 4);
+            const float4 w0 = *reinterpret_cast<const float4*>(Wo + k);
+            const float4 w1 = *reinterpret_cast<const float4*>(Wo + k + 4);
+            acc0 = fmaf(x0.x, w0.x, acc0); acc0 = fmaf(x0.y, w0.y, acc0);
+            acc0 = fmaf(x0.z, w0.z, acc0); acc0 = fmaf(x0.w, w0.w, acc0);
+            acc1 = fmaf(x1.x, w1.x, acc1); acc1 = fmaf(x1.y, w1.y, acc1);
+            acc1 = fmaf(x1.z, w1.z, acc1); acc1 = fmaf(x1.w, w1.w, acc1);
+        }
+        y = (acc0 + acc1) + net.params[net.b_off[nh] + j];
+    }
+    if (r >= M || j >= d_out) return;
+    if (OUT_MODE == OUT_F32) {
+        a.out[blockIdx.y][r * a.ld_out + a.out_col + j] = y;
+    } else if (OUT_MODE == OUT_TARGET) {
+        // robot.py:338-339 target policy smoothing
+        float e;
+        if (a.eps) {
+            e = a.eps[r * 2 + j];
+        } else {
+            const double2 z = gauss_pair(philox((uint32_t)r, 0u, NAV_TAG_TNOISE, a.counter,
+                                                a.seed_lo, a.seed_hi));
+            e = (float)(j == 0 ? z.x : z.y);
+        }
+        float nz = e * a.policy_noise;
+        nz = fminf(fmaxf(nz, -a.noise_clip), a.noise_clip);
+        float v = y + nz;
+        v = fminf(fmaxf(v, -a.max_action), a.max_action);
+        a.out[blockIdx.y][r * a.ld_out + a.out_col + j] = v;
+    } else {
+        // robot.py:556-567 (training) / 586-593 (testing)
+        const double s = a.state[r * 2 + j], g = a.goal[r * 2 + j];
+        double c = (s - g) + (double)y;
+        if (a.act_mode == 0) {
+            double z;
+            if (a.noise_z) {
+                z = a.noise_z[r * 2 + j];
+            } else {
+                const double2 zz = gauss_pair(philox(0u, (uint32_t)r, NAV_TAG_NOISE, a.step,
+                                                     a.seed_lo, a.seed_hi));
+                z = j == 0 ? zz.x : zz.y;
+            }
+            c = c + (a.noise_scale[r] * a.max_action_d) * z;
+        }
+        a.action_out[r * 2 + j] = clipd(c, -a.max_action_d, a.max_action_d);
+        if (a.out[0]) a.out[0][r * 2 + j] = y;
+    }
+}
+
+// ---------------- row-local backward ----------------
+struct BwdArgs {
+    MlpDev net;
+    int64_t M;
+    const float* dy;
+    const float* acts;
+    float* dz;
+    float* dx;
+};
+
+template <int NT>
+__global__ __launch_bounds__(kBlock, 1) void k_mlp_bwd(BwdArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    constexpr int hp = NT * 32, SS = hp + 4;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, l32 = lane & 31;
+    const MlpDev& net = a.net;
+    const int64_t M = a.M;
+    const int64_t row0 = (int64_t)blockIdx.x * TM + wv * 32;
+    float* wbuf = smem + TM * SS;
+    float* xin = wbuf + 16 * hp + wv * 128;
+    float* my = smem + wv * 32 * SS;
+    const int d_in = net.d_in, d_out = net.d_out, nh = net.n_hidden;
+    const int64_t MH = M * hp;
+
+    if (lane < 32) {
+        const int64_t r = row0 + lane;
+        float x[4] = {0.f, 0.f, 0.f, 0.f};
+        if (r < M)
+            for (int j = 0; j < d_out; ++j) x[j] = a.dy[r * d_out + j];
+        *reinterpret_cast<float4*>(xin + lane * 4) = make_float4(x[0], x[1], x[2], x[3]);
+    }
+    __syncthreads();
+
+    // top hidden layer: dz = (dy . Wo) * (act > 0)
+    {
+        const float* Wo = net.params + net.w_off[nh];
+        const float* act = a.acts + (int64_t)(nh - 1) * MH;
+        float* dzo = a.dz + (int64_t)(nh - 1) * MH;
+        for (int c = lane; c < hp; c += 64) {
+            const float w0 = Wo[c], w1 = d_out > 1 ? Wo[hp + c] : 0.f;
+            for (int r = 0; r < 32; ++r) {
+                const float4 g = *reinterpret_cast<const float4*>(xin + r * 4);
+                float v = g.x * w0;
+                if (d_out > 1) v = fmaf(g.y, w1, v);
+                const int64_t gr = row0 + r;
+                if (gr < M) {
+                    if (!(act[gr * hp + c] > 0.f)) v = 0.f;
+                    dzo[gr * hp + c] = v;
+                } else {
+                    v = 0.f;
+                }
+                my[r * SS + c] = v;
+            }
+        }
+    }
+    __syncthreads();
+
+    // hidden layers, top-down: dz_{L-1} = (dz_L . W_L) * (act_{L-1} > 0), B = packed Wb_L
+    for (int L = nh - 1; L >= 1; --L) {
+        f32x16 acc[NT];
+        gemm_rows<NT>(my, SS, net.packed + (int64_t)(L - 1) * 2 * hp * hp + (int64_t)hp * hp,
+                      wbuf, acc);
+        const float* act = a.acts + (int64_t)(L - 1) * MH;
+        float* dzo = a.dz + (int64_t)(L - 1) * MH;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int c = 32 * t + l32;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int r = acc_row(i, h);
+                const int64_t gr = row0 + r;
+                float v = acc[t][i];
+                if (gr < M) {
+                    if (!(act[gr * hp + c] > 0.f)) v = 0.f;
+                    dzo[gr * hp + c] = v;
+                } else {
+                    v = 0.f;
+                }
+                my[r * SS + c] = v;
+            }
+        }
+        __syncthreads();
+    }
+
+    // dx = dz_0 . W0 : lane = (row l32, inputs h and h+2)
+    if (a.dx) {
+        const float* W0 = net.params + net.w_off[0];
+        const int64_t r = row0 + l32;
+        const float* zr = my + l32 * SS;
+        for (int j = h; j < d_in; j += 2) {
+            float acc = 0.f;
+            for (int c = 0; c < hp; ++c) acc = fmaf(zr[c], W0[c * d_in + j], acc);
+            if (r < M) a.dx[r * d_in + j] = acc;
+        }
+    }
+}
+
+// ---------------- weight gradients (split-M partial slabs) ----------------
+struct WgradArgs {
+    MlpDev net;
+    int64_t M;
+    const float* in;
+    int ld_in, in_col;
+    const float* acts;
+    const float* dz;
+    const float* dy;
+    float* slabs;
+    int splits;
+};
+
+constexpr int WG_MC = 32;   // rows per staged chunk
+constexpr int WG_LD = 68;   // LDS row stride of the staged 64-column panels
+
+// dW_L[n][k] = sum_m dz_L[m][n] * act_{L-1}[m][k] for hidden x hidden layers; grid = (tiles of
+// 64x64, splits, layer-1). Each wave owns one 32x32 MFMA tile of the 64x64 workgroup tile.
+__global__ __launch_bounds__(kBlock) void k_wgrad_hidden(WgradArgs a) {
+    __shared__ __attribute__((aligned(16))) float pa[2][WG_MC][WG_LD];
+    __shared__ __attribute__((aligned(16))) float pb[2][WG_MC][WG_LD];
+    const MlpDev& net = a.net;
+    const int hp = net.hp;
+    const int tiles = (hp + 63) / 64;
+    const int tn = blockIdx.x / tiles, tk = blockIdx.x % tiles;
+    const int L = blockIdx.z + 1;
+    const int64_t MH = a.M * hp;
+    const float* P = a.dz + (int64_t)L * MH;         // dz of layer L (its pre-activation)
+    const float* Q = a.acts + (int64_t)(L - 1) * MH;  // input of layer L
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, l32 = lane & 31;
+    const int nloc = 32 * (wv >> 1), kloc = 32 * (wv & 1);
+    const int n0 = tn * 64, k0 = tk * 64;
+    const int64_t per = (a.M + a.splits - 1) / a.splits;
+    const int64_t m_lo = (int64_t)blockIdx.y * per;
+    const int64_t m_hi = m_lo + per < a.M ? m_lo + per : a.M;
+    f32x16 acc;
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+    // staging: 32 rows x 64 cols per panel = 512 float4 per panel; thread -> 2 per panel
+    auto load = [&](int64_t m0, float4 (&ra)[2], float4 (&rb)[2]) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int i = tid + kBlock * j;
+            const int rr = i >> 4, cc = (i & 15) * 4;
+            const int64_t m = m0 + rr;
+            float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+            ra[j] = z;
+            rb[j] = z;
+            if (m < m_hi) {
+                if (n0 + cc < hp) ra[j] = *reinterpret_cast<const float4*>(P + m * hp + n0 + cc);
+                if (k0 + cc < hp) rb[j] = *reinterpret_cast<const float4*>(Q + m * hp + k0 + cc);
+            }
+        }
+    };
+    auto store = [&](int buf, float4 (&ra)[2], float4 (&rb)[2]) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int i = tid + kBlock * j;
+            const int rr = i >> 4, cc = (i & 15) * 4;
+            *reinterpret_cast<float4*>(&pa[buf][rr][cc]) = ra[j];
+            *reinterpret_cast<float4*>(&pb[buf][rr][cc]) = rb[j];
+        }
+    };
+    float4 ra[2], rb[2];
+    const int nch = (int)((m_hi - m_lo + WG_MC - 1) / WG_MC);
+    if (nch > 0) {
+        load(m_lo, ra, rb);
+        store(0, ra, rb);
+    }
+    __syncthreads();
+    for (int c = 0; c < nch; ++c) {
+        if (c + 1 < nch) load(m_lo + (int64_t)(c + 1) * WG_MC, ra, rb);
+        const int buf = c & 1;
+#pragma unroll
+        for (int s = 0; s < WG_MC / 2; ++s) {
+            const float av = pa[buf][2 * s + h][nloc + l32];
+            const float bv = pb[buf][2 * s + h][kloc + l32];
+            acc = mfma(av, bv, acc);
+        }
+        if (c + 1 < nch) store(buf ^ 1, ra, rb);
+        __syncthreads();
+    }
+    const int nb = n0 + nloc, kb = k0 + kloc;
+    if (nb >= hp || kb >= hp) return;
+    float* out = a.slabs + (int64_t)blockIdx.y * net.count + net.w_off[L];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) out[(int64_t)(nb + acc_row(i, h)) * hp + kb + l32] = acc[i];
+}
+
+// Thin reductions: every bias, layer-0 weights (K = d_in) and output weights (N = d_out).
+// grid = (n_hidden + 1 jobs, splits); thread = column.
+__global__ __launch_bounds__(kBlock) void k_wgrad_small(WgradArgs a) {
+    const MlpDev& net = a.net;
+    const int hp = net.hp, nh = net.n_hidden, job = blockIdx.x, c = threadIdx.x;
+    const int64_t per = (a.M + a.splits - 1) / a.splits;
+    const int64_t m_lo = (int64_t)blockIdx.y * per;
+    const int64_t m_hi = m_lo + per < a.M ? m_lo + per : a.M;
+    const int64_t MH = a.M * hp;
+    float* out = a.slabs + (int64_t)blockIdx.y * net.count;
+    if (job < nh) {
+        if (c >= hp) return;
+        const float* P = a.dz + (int64_t)job * MH;
+        float sb = 0.f, sw[4] = {0.f, 0.f, 0.f, 0.f};
+        const int d_in = net.d_in;
+        for (int64_t m = m_lo; m < m_hi; ++m) {
+            const float g = P[m * hp + c];
+            sb += g;
+            if (job == 0) {
+                const float* x = a.in + m * a.ld_in + a.in_col;
+                for (int k = 0; k < d_in; ++k) sw[k] = fmaf(g, x[k], sw[k]);
+            }
+        }
+        out[net.b_off[job] + c] = sb;
+        if (job == 0)
+            for (int k = 0; k < d_in; ++k) out[net.w_off[0] + c * d_in + k] = sw[k];
+    } else {
+        const int d_out = net.d_out;
+        if (c < hp) {
+            const float* A = a.acts + (int64_t)(nh - 1) * MH;
+            float s0 = 0.f, s1 = 0.f;
+            for (int64_t m = m_lo; m < m_hi; ++m) {
+                const float x = A[m * hp + c];
+                s0 = fmaf(a.dy[m * d_out], x, s0);
+                if (d_out > 1) s1 = fmaf(a.dy[m * d_out + 1], x, s1);
+            }
+            out[net.w_off[nh] + c] = s0;
+            if (d_out > 1) out[net.w_off[nh] + hp + c] = s1;
+        }
+        if (c < d_out) {
+            float s = 0.f;
+            for (int64_t m = m_lo; m < m_hi; ++m) s += a.dy[m * d_out + c];
+            out[net.b_off[nh] + c] = s;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_grad_reduce(const float4* __restrict__ slabs,
+                                                        int splits, int64_t n4,
+                                                        float4* __restrict__ grad) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n4;
+         i += (int64_t)gridDim.x * kBlock) {
+        float4 s = slabs[i];
+        for (int k = 1; k < splits; ++k) {
+            const float4 v = slabs[(int64_t)k * n4 + i];
+            s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+        }
+        grad[i] = s;
+    }
+}
+
+// ---------------- optimizer / target update, refreshing the packed images ----------------
+struct PackInfo {
+    int hp, n_hidden;
+    int64_t w_off[kMaxLayers];
+    float* packed;
+};
+
+NAV_DEV void repack(const PackInfo& pk, int64_t i, float4 v) {
+    // i = flat float index of v.x (multiple of 4)
+    for (int L = 1; L < pk.n_hidden; ++L) {
+        const int64_t off = pk.w_off[L], sz = (int64_t)pk.hp * pk.hp;
+        if (i >= off && i < off + sz) {
+            const int64_t e = i - off;
+            const int n = (int)(e / pk.hp), k = (int)(e % pk.hp);
+            float* Wf = pk.packed + (int64_t)(L - 1) * 2 * sz;
+            float* Wb = Wf + sz;
+            *reinterpret_cast<float4*>(Wf + ((int64_t)(k >> 2) * pk.hp + n) * 4) = v;
+            float* d = Wb + ((int64_t)(n >> 2) * pk.hp + k) * 4 + (n & 3);
+            d[0] = v.x; d[4] = v.y; d[8] = v.z; d[12] = v.w;
+            return;
+        }
+    }
+}
+
+NAV_DEV float adam1(float& p, float g, float& m, float& v, float b1w, float b2, float omb2,
+                    float eps, float step_size, float bc2s) {
+    // torch 2.10 _single_tensor_adam: m.lerp_(g, 1-b1); v.mul_(b2).addcmul_(g, g, 1-b2);
+    // denom = v.sqrt()/bc2_sqrt + eps; p.addcdiv_(m, denom, -step_size)
+    m = fmaf(b1w, g - m, m);
+    v = v * b2 + (omb2 * g) * g;
+    const float denom = sqrtf(v) / bc2s + eps;
+    p = p + (-step_size) * (m / denom);
+    return p;
+}
+
+__global__ __launch_bounds__(kBlock) void k_adam(float4* __restrict__ p,
+                                                 const float4* __restrict__ g, float4* m,
+                                                 float4* v, int64_t n4, float b1w, float b2,
+                                                 float omb2, float eps, float ss, float bc2s,
+                                                 PackInfo pk) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n4;
+         i += (int64_t)gridDim.x * kBlock) {
+        float4 pp = p[i], gg = g[i], mm = m[i], vv = v[i];
+        adam1(pp.x, gg.x, mm.x, vv.x, b1w, b2, omb2, eps, ss, bc2s);
+        adam1(pp.y, gg.y, mm.y, vv.y, b1w, b2, omb2, eps, ss, bc2s);
+        adam1(pp.z, gg.z, mm.z, vv.z, b1w, b2, omb2, eps, ss, bc2s);
+        adam1(pp.w, gg.w, mm.w, vv.w, b1w, b2, omb2, eps, ss, bc2s);
+        p[i] = pp; m[i] = mm; v[i] = vv;
+        if (pk.packed) repack(pk, i * 4, pp);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_polyak(float4* __restrict__ t,
+                                                   const float4* __restrict__ s, int64_t n4,
+                                                   float omt, float tau, PackInfo pk) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n4;
+         i += (int64_t)gridDim.x * kBlock) {
+        float4 a = t[i];
+        const float4 b = s[i];
+        // robot.py:309 target*(1-tau) + source*tau (two products, one sum)
+        a.x = a.x * omt + b.x * tau;
+        a.y = a.y * omt + b.y * tau;
+        a.z = a.z * omt + b.z * tau;
+        a.w = a.w * omt + b.w * tau;
+        t[i] = a;
+        if (pk.packed) repack(pk, i * 4, a);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_pack(const float4* __restrict__ p, int64_t n4,
+                                                 PackInfo pk) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n4;
+         i += (int64_t)gridDim.x * kBlock)
+        repack(pk, i * 4, p[i]);
+}
+
+// ---------------- TD3 glue ----------------
+__global__ __launch_bounds__(kBlock) void k_replay_sample(const float4* __restrict__ rows,
+                                                          int64_t size, int64_t B,
+                                                          const int64_t* __restrict__ idx,
+                                                          uint32_t s0, uint32_t s1, uint32_t ctr,
+                                                          float4* __restrict__ batch) {
+    const int64_t b = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (b >= B) return;
+    int64_t k;
+    if (idx) {
+        k = idx[b];
+    } else {
+        const uint4 w = philox((uint32_t)b, 0u, NAV_TAG_SAMPLE, ctr, s0, s1);
+        k = (int64_t)(((uint64_t)w.x * (uint64_t)size) >> 32);
+    }
+    batch[2 * b] = rows[2 * k];
+    batch[2 * b + 1] = rows[2 * k + 1];
+}
+
+__global__ __launch_bounds__(kBlock) void k_critic_loss(int64_t B, const float* __restrict__ bt,
+                                                        const float* q1t, const float* q2t,
+                                                        const float* q1, const float* q2,
+                                                        float gamma, float norm, float* dq1,
+                                                        float* dq2, float* y_out,
+                                                        float* loss_part) {
+    const int64_t b = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    float l1 = 0.f, l2 = 0.f;
+    if (b < B) {
+        // robot.py:331-345: y = r + gamma * min(q1', q2') * (1 - done)
+        const float r = bt[b * NAV_ROW + 4], d = bt[b * NAV_ROW + 7];
+        const float nd = 1.0f - d;
+        const float mn = fminf(q1t[b], q2t[b]);
+        const float y = r + (gamma * mn) * nd;
+        // torch mse_loss backward: (q - y) * (2/B)
+        const float e1 = q1[b] - y, e2 = q2[b] - y;
+        dq1[b] = e1 * norm;
+        dq2[b] = e2 * norm;
+        if (y_out) y_out[b] = y;
+        l1 = e1 * e1;
+        l2 = e2 * e2;
+    }
+    if (loss_part) {
+        __shared__ float part[kBlock / 64][2];
+        const float s1 = wave_sum(l1), s2 = wave_sum(l2);
+        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+        if (lane == 0) { part[wv][0] = s1; part[wv][1] = s2; }
+        __syncthreads();
+        if (threadIdx.x < 2) {
+            float acc = 0.f;
+            for (int w = 0; w < kBlock / 64; ++w) acc += part[w][threadIdx.x];
+            loss_part[(int64_t)blockIdx.x * 2 + threadIdx.x] = acc;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_fill(float* x, int64_t n, float v) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) x[i] = v;
+}
+
+__global__ __launch_bounds__(kBlock) void k_strided_copy(const float* __restrict__ src, int lds,
+                                                         int cs, float* __restrict__ dst, int ldd,
+                                                         int cd, int64_t rows, int cols) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= rows * cols) return;
+    const int64_t r = i / cols;
+    const int c = (int)(i % cols);
+    dst[r * ldd + cd + c] = src[r * lds + cs + c];
+}
+
+inline int blocks_for(int64_t n) { return (int)((n + kBlock - 1) / kBlock); }
+inline int grid_stride_blocks(int64_t n) {
+    const int64_t b = (n + kBlock - 1) / kBlock;
+    return (int)(b < 2048 ? (b > 0 ? b : 1) : 2048);
+}
+
+PackInfo pack_info(const MlpDev& d, float* packed) {
+    PackInfo pk;
+    pk.hp = d.hp;
+    pk.n_hidden = d.n_hidden;
+    for (int l = 0; l < kMaxLayers; ++l) pk.w_off[l] = l <= d.n_hidden ? d.w_off[l] : 0;
+    pk.packed = d.n_hidden > 1 ? packed : nullptr;
+    return pk;
+}
+
+// ---- launch helpers (template dispatch on NT = hp / 32) ----
+template <int IN_MODE, int OUT_MODE>
+int launch_fwd(const FwdArgs& a, int n_nets, hipStream_t st) {
+    const int hp = a.net[0].hp;
+    const size_t lds = lds_bytes(hp);
+    const dim3 grid((unsigned)((a.M + TM - 1) / TM), (unsigned)n_nets);
+#define NAV_FWD_CASE(NT_)                                                                        \
+    case NT_: {                                                                                  \
+        auto k = k_mlp_fwd<NT_, IN_MODE, OUT_MODE>;                                              \
+        hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,          \
+                            (int)lds);                                                           \
+        hipLaunchKernelGGL(k, grid, dim3(kBlock), lds, st, a);                                   \
+        break;                                                                                   \
+    }
+    switch (hp / 32) {
+        NAV_FWD_CASE(1) NAV_FWD_CASE(2) NAV_FWD_CASE(3) NAV_FWD_CASE(4)
+        NAV_FWD_CASE(5) NAV_FWD_CASE(6) NAV_FWD_CASE(7) NAV_FWD_CASE(8)
+        default: return NAV_EINVAL;
+    }
+#undef NAV_FWD_CASE
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int launch_bwd(const BwdArgs& a, hipStream_t st) {
+    const int hp = a.net.hp;
+    const size_t lds = lds_bytes(hp);
+    const dim3 grid((unsigned)((a.M + TM - 1) / TM));
+#define NAV_BWD_CASE(NT_)                                                                        \
+    case NT_: {                                                                                  \
+        auto k = k_mlp_bwd<NT_>;                                                                 \
+        hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,          \
+                            (int)lds);                                                           \
+        hipLaunchKernelGGL(k, grid, dim3(kBlock), lds, st, a);                                   \
+        break;                                                                                   \
+    }
+    switch (hp / 32) {
+        NAV_BWD_CASE(1) NAV_BWD_CASE(2) NAV_BWD_CASE(3) NAV_BWD_CASE(4)
+        NAV_BWD_CASE(5) NAV_BWD_CASE(6) NAV_BWD_CASE(7) NAV_BWD_CASE(8)
+        default: return NAV_EINVAL;
+    }
+#undef NAV_BWD_CASE
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t nav_mlp_param_count(int32_t d_in, int32_t d_out, int32_t hp, int32_t n_hidden) {
+    nav_mlp n{d_in, d_out, hp, hp, n_hidden, reinterpret_cast<float*>(16),
+              reinterpret_cast<float*>(16)};
+    MlpDev d;
+    if (!make_dev(&n, &d)) return NAV_EINVAL;
+    return d.count;
+}
+
+int64_t nav_mlp_packed_count(int32_t hp, int32_t n_hidden) {
+    if (hp < 32 || hp > 256 || (hp & 31) || n_hidden < 1) return NAV_EINVAL;
+    return (int64_t)(n_hidden - 1) * 2 * hp * hp;
+}
+
+int nav_mlp_layer_offsets(const nav_mlp* net, int32_t layer, int64_t* w_off, int64_t* b_off) {
+    MlpDev d;
+    if (!make_dev(net, &d) || layer < 0 || layer > net->n_hidden) return NAV_EINVAL;
+    if (w_off) *w_off = d.w_off[layer];
+    if (b_off) *b_off = d.b_off[layer];
+    return 0;
+}
+
+int nav_act(const nav_params* p, const nav_mlp* actor, int64_t n, const double* state,
+            const double* goal, const double* noise_scale, const double* noise_z, uint32_t step,
+            int32_t mode, double* action_out, float* residual_out, void* stream) {
+    FwdArgs a{};
+    if (!p || !make_dev(actor, &a.net[0]) || actor->d_in != 2 || actor->d_out != 2 || n < 0 ||
+        (mode != 0 && mode != 1))
+        return NAV_EINVAL;
+    if (n == 0) return 0;
+    if (!state || !goal || !action_out || (mode == 0 && !noise_scale)) return NAV_EINVAL;
+    a.M = n;
+    a.state = state;
+    a.goal = goal;
+    a.noise_scale = noise_scale;
+    a.noise_z = noise_z;
+    a.step = step;
+    a.act_mode = mode;
+    a.max_action_d = p->max_action;
+    a.action_out = action_out;
+    a.out[0] = residual_out;
+    a.seed_lo = p->seed_lo;
+    a.seed_hi = p->seed_hi;
+    return launch_fwd<IN_BASELINE, OUT_ACT>(a, 1, S(stream));
+}
+
+int nav_mlp_forward(const nav_mlp* nets, int32_t n_nets, int64_t M, const float* in,
+                    int32_t ld_in, int32_t in_col, float* const* out, int32_t ld_out,
+                    int32_t out_col, int32_t out_mode, const float* eps, float policy_noise,
+                    float noise_clip, float max_action, uint32_t seed_lo, uint32_t seed_hi,
+                    uint32_t counter, float* const* acts, void* stream) {
+    FwdArgs a{};
+    if (!nets || n_nets < 1 || n_nets > 2 || M < 0 || !out) return NAV_EINVAL;
+    for (int i = 0; i < n_nets; ++i) {
+        if (!make_dev(&nets[i], &a.net[i]) || !out[i]) return NAV_EINVAL;
+        if (a.net[i].hp != a.net[0].hp || a.net[i].d_in != a.net[0].d_in) return NAV_EINVAL;
+        a.out[i] = out[i];
+        a.acts[i] = acts ? acts[i] : nullptr;
+    }
+    if (M == 0) return 0;
+    if (!in || in_col < 0 || in_col + a.net[0].d_in > ld_in || out_col < 0 ||
+        out_col + a.net[0].d_out > ld_out)
+        return NAV_EINVAL;
+    a.M = M;
+    a.in = in;
+    a.ld_in = ld_in;
+    a.in_col = in_col;
+    a.ld_out = ld_out;
+    a.out_col = out_col;
+    a.eps = eps;
+    a.policy_noise = policy_noise;
+    a.noise_clip = noise_clip;
+    a.max_action = max_action;
+    a.seed_lo = seed_lo;
+    a.seed_hi = seed_hi;
+    a.counter = counter;
+    if (out_mode == 0) return launch_fwd<IN_F32, OUT_F32>(a, n_nets, S(stream));
+    if (out_mode == 1) {
+        if (a.net[0].d_out != 2) return NAV_EINVAL;
+        return launch_fwd<IN_F32, OUT_TARGET>(a, n_nets, S(stream));
+    }
+    return NAV_EINVAL;
+}
+
+int nav_mlp_backward(const nav_mlp* net, int64_t M, const float* dy, const float* acts,
+                     float* dz, float* dx, void* stream) {
+    BwdArgs a{};
+    if (!make_dev(net, &a.net) || M < 0) return NAV_EINVAL;
+    if (M == 0) return 0;
+    if (!dy || !acts || !dz) return NAV_EINVAL;
+    a.M = M;
+    a.dy = dy;
+    a.acts = acts;
+    a.dz = dz;
+    a.dx = dx;
+    return launch_bwd(a, S(stream));
+}
+
+int nav_mlp_wgrad(const nav_mlp* net, int64_t M, const float* in, int32_t ld_in, int32_t in_col,
+                  const float* acts, const float* dz, const float* dy, float* slabs,
+                  int32_t splits, void* stream) {
+    WgradArgs a{};
+    if (!make_dev(net, &a.net) || M < 1 || splits < 1 || !in || !acts || !dz || !dy || !slabs ||
+        in_col < 0 || in_col + net->d_in > ld_in)
+        return NAV_EINVAL;
+    a.M = M;
+    a.in = in;
+    a.ld_in = ld_in;
+    a.in_col = in_col;
+    a.acts = acts;
+    a.dz = dz;
+    a.dy = dy;
+    a.slabs = slabs;
+    a.splits = splits;
+    const int hp = a.net.hp;
+    if (a.net.n_hidden > 1) {
+        const int tiles = (hp + 63) / 64;
+        hipLaunchKernelGGL(k_wgrad_hidden, dim3(tiles * tiles, splits, a.net.n_hidden - 1),
+                           dim3(kBlock), 0, S(stream), a);
+        NAV_CHECK_LAUNCH();
+    }
+    hipLaunchKernelGGL(k_wgrad_small, dim3(a.net.n_hidden + 1, splits), dim3(kBlock), 0,
+                       S(stream), a);
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_grad_reduce(const float* slabs, int32_t splits, int64_t count, float* grad,
+                    void* stream) {
+    if (!slabs || !grad || splits < 1 || count < 0 || (count & 3)) return NAV_EINVAL;
+    if (count == 0) return 0;
+    const int64_t n4 = count / 4;
+    hipLaunchKernelGGL(k_grad_reduce, dim3(grid_stride_blocks(n4)), dim3(kBlock), 0, S(stream),
+                       reinterpret_cast<const float4*>(slabs), splits, n4,
+                       reinterpret_cast<float4*>(grad));
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_adam(const nav_mlp* net, const float* grad, float* m, float* v, float beta1, float beta2,
+             float eps, float step_size, float bc2_sqrt, void* stream) {
+    MlpDev d;
+    if (!make_dev(net, &d) || !grad || !m || !v) return NAV_EINVAL;
+    const int64_t n4 = d.count / 4;
+    hipLaunchKernelGGL(k_adam, dim3(grid_stride_blocks(n4)), dim3(kBlock), 0, S(stream),
+                       reinterpret_cast<float4*>(net->params),
+                       reinterpret_cast<const float4*>(grad), reinterpret_cast<float4*>(m),
+                       reinterpret_cast<float4*>(v), n4, 1.0f - beta1, beta2, 1.0f - beta2, eps,
+                       step_size, bc2_sqrt, pack_info(d, net->packed));
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_polyak(const nav_mlp* target, const nav_mlp* source, float tau, void* stream) {
+    MlpDev dt, ds;
+    if (!make_dev(target, &dt) || !make_dev(source, &ds) || dt.count != ds.count ||
+        dt.hp != ds.hp || dt.n_hidden != ds.n_hidden)
+        return NAV_EINVAL;
+    const int64_t n4 = dt.count / 4;
+    hipLaunchKernelGGL(k_polyak, dim3(grid_stride_blocks(n4)), dim3(kBlock), 0, S(stream),
+                       reinterpret_cast<float4*>(target->params),
+                       reinterpret_cast<const float4*>(source->params), n4, 1.0f - tau, tau,
+                       pack_info(dt, target->packed));
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_mlp_pack(const nav_mlp* net, void* stream) {
+    MlpDev d;
+    if (!make_dev(net, &d)) return NAV_EINVAL;
+    if (d.n_hidden < 2) return 0;
+    const int64_t n4 = d.count / 4;
+    hipLaunchKernelGGL(k_pack, dim3(grid_stride_blocks(n4)), dim3(kBlock), 0, S(stream),
+                       reinterpret_cast<const float4*>(net->params), n4,
+                       pack_info(d, net->packed));
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_replay_sample(const nav_replay* replay, int64_t size, int64_t B, const int64_t* idx,
+                      uint32_t seed_lo, uint32_t seed_hi, uint32_t counter, float* batch,
+                      void* stream) {
+    if (!replay || !replay->rows || size < 1 || size > replay->capacity ||
+        size > ((int64_t)1 << 32) || B < 0 || !batch)
+        return NAV_EINVAL;
+    if (B == 0) return 0;
+    hipLaunchKernelGGL(k_replay_sample, dim3(blocks_for(B)), dim3(kBlock), 0, S(stream),
+                       reinterpret_cast<const float4*>(replay->rows), size, B, idx, seed_lo,
+                       seed_hi, counter, reinterpret_cast<float4*>(batch));
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_td3_critic_loss(int64_t B, const float* batch, const float* q1t, const float* q2t,
+                        const float* q1, const float* q2, float gamma, float* dq1, float* dq2,
+                        float* y_out, float* loss_part, void* stream) {
+    if (B < 1 || !batch || !q1t || !q2t || !q1 || !q2 || !dq1 || !dq2) return NAV_EINVAL;
+    const float norm = (float)(2.0 / (double)B);
+    hipLaunchKernelGGL(k_critic_loss, dim3(blocks_for(B)), dim3(kBlock), 0, S(stream), B, batch,
+                       q1t, q2t, q1, q2, gamma, norm, dq1, dq2, y_out, loss_part);
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_batch_sa(int64_t B, const float* batch, float* sa, void* stream) {
+    return nav_strided_copy(batch, NAV_ROW, 0, sa, 4, 0, B, 4, stream);
+}
+
+int nav_fill(float* x, int64_t n, float value, void* stream) {
+    if (n < 0 || (n && !x)) return NAV_EINVAL;
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_fill, dim3(blocks_for(n)), dim3(kBlock), 0, S(stream), x, n, value);
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_strided_copy(const float* src, int32_t ld_src, int32_t col_src, float* dst,
+                     int32_t ld_dst, int32_t col_dst, int64_t rows, int32_t cols, void* stream) {
+    if (rows < 0 || cols < 0 || (rows && cols && (!src || !dst))) return NAV_EINVAL;
+    if (rows == 0 || cols == 0) return 0;
+    hipLaunchKernelGGL(k_strided_copy, dim3(blocks_for(rows * cols)), dim3(kBlock), 0, S(stream),
+                       src, ld_src, col_src, dst, ld_dst, col_dst, rows, cols);
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+}  // extern "C"

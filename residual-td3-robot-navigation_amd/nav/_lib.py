@@ -1,0 +1,168 @@
+"""ctypes binding of libnavenv.so (include/navenv.h) — the only way this package computes.
+
+Loaded after `import torch` so the library binds torch's already-loaded HIP runtime
+(libamdhip64.so.7, same SONAME as /opt/rocm's). There is no fallback: if the library is missing or
+a call fails, an exception is raised.
+"""
+import ctypes as C
+import os
+
+import torch  # noqa: F401  (must be loaded first: provides the HIP runtime)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libnavenv.so")
+NAV_EINVAL = -100000
+ABI_VERSION = 1
+
+_dp = C.POINTER(C.c_double)
+_vp = C.c_void_p
+
+
+class NavParams(C.Structure):
+    _fields_ = [
+        ("world_size", C.c_double), ("max_action", C.c_double), ("init_region_size", C.c_double),
+        ("goal_threshold", C.c_double), ("goal_reward", C.c_double),
+        ("stuck_threshold", C.c_double), ("stuck_penalty", C.c_double),
+        ("demo_factor", C.c_double), ("noise_decay", C.c_double),
+        ("path_length0", C.c_int32), ("path_increase", C.c_int32),
+        ("seed_lo", C.c_uint32), ("seed_hi", C.c_uint32), ("max_goal_draws", C.c_int32),
+    ]
+
+
+class NavEnvSoa(C.Structure):
+    _fields_ = [
+        ("n", C.c_int64), ("state", _vp), ("goal", _vp), ("region", _vp), ("hist", _vp),
+        ("meta", _vp), ("plan_index", _vp), ("path_length", _vp), ("episodes", _vp),
+        ("noise_scale", _vp),
+    ]
+
+
+class NavStepOut(C.Structure):
+    _fields_ = [("next_state", _vp), ("goal_term", _vp), ("flags", _vp), ("block_stats", _vp)]
+
+
+class NavReplay(C.Structure):
+    _fields_ = [("rows", _vp), ("capacity", C.c_int64)]
+
+
+class NavMlp(C.Structure):
+    _fields_ = [
+        ("d_in", C.c_int32), ("d_out", C.c_int32), ("hidden", C.c_int32),
+        ("hidden_pad", C.c_int32), ("n_hidden", C.c_int32), ("params", _vp), ("packed", _vp),
+    ]
+
+
+# (name, restype, argtypes) for every entry point of include/navenv.h
+_P = C.POINTER
+SIGNATURES = [
+    ("nav_abi_version", C.c_int, []),
+    ("nav_default_params", None, [_P(NavParams)]),
+    ("nav_mlp_param_count", C.c_int64, [C.c_int32] * 4),
+    ("nav_mlp_packed_count", C.c_int64, [C.c_int32] * 2),
+    ("nav_mlp_layer_offsets", C.c_int, [_P(NavMlp), C.c_int32, _P(C.c_int64), _P(C.c_int64)]),
+    ("nav_env_init", C.c_int, [_P(NavParams), _P(NavEnvSoa), C.c_int32, C.c_int32, _vp, _vp]),
+    ("nav_env_reset", C.c_int, [_P(NavParams), _P(NavEnvSoa), _vp, _vp, _vp]),
+    ("nav_env_step", C.c_int, [_P(NavParams), _P(NavEnvSoa), _vp, _vp, _vp, _vp]),
+    ("nav_dynamics", C.c_int, [_vp, _vp, _vp, _vp, C.c_int64, _vp]),
+    ("nav_agent_step", C.c_int, [_P(NavParams), _P(NavEnvSoa), _vp, _vp, _P(NavReplay),
+                                 C.c_int64, _P(NavStepOut), _vp]),
+    ("nav_demo_reward", C.c_int, [_P(NavParams), C.c_int64, _vp, _vp, _vp, _vp, _vp, C.c_int64,
+                                  C.c_int32, _P(NavReplay), C.c_int64, _vp, _vp]),
+    ("nav_compute_reward", C.c_int, [_P(NavParams), C.c_int64, _vp, _vp, _vp, C.c_int64,
+                                     C.c_int32, _vp, _vp, _vp]),
+    ("nav_act", C.c_int, [_P(NavParams), _P(NavMlp), C.c_int64, _vp, _vp, _vp, _vp, C.c_uint32,
+                          C.c_int32, _vp, _vp, _vp]),
+    ("nav_mlp_forward", C.c_int, [_P(NavMlp), C.c_int32, C.c_int64, _vp, C.c_int32, C.c_int32,
+                                  _P(_vp), C.c_int32, C.c_int32, C.c_int32, _vp, C.c_float,
+                                  C.c_float, C.c_float, C.c_uint32, C.c_uint32, C.c_uint32,
+                                  _P(_vp), _vp]),
+    ("nav_mlp_backward", C.c_int, [_P(NavMlp), C.c_int64, _vp, _vp, _vp, _vp, _vp]),
+    ("nav_mlp_wgrad", C.c_int, [_P(NavMlp), C.c_int64, _vp, C.c_int32, C.c_int32, _vp, _vp, _vp,
+                                _vp, C.c_int32, _vp]),
+    ("nav_grad_reduce", C.c_int, [_vp, C.c_int32, C.c_int64, _vp, _vp]),
+    ("nav_adam", C.c_int, [_P(NavMlp), _vp, _vp, _vp, C.c_float, C.c_float, C.c_float,
+                           C.c_float, C.c_float, _vp]),
+    ("nav_polyak", C.c_int, [_P(NavMlp), _P(NavMlp), C.c_float, _vp]),
+    ("nav_mlp_pack", C.c_int, [_P(NavMlp), _vp]),
+    ("nav_replay_sample", C.c_int, [_P(NavReplay), C.c_int64, C.c_int64, _vp, C.c_uint32,
+                                    C.c_uint32, C.c_uint32, _vp, _vp]),
+    ("nav_td3_critic_loss", C.c_int, [C.c_int64, _vp, _vp, _vp, _vp, _vp, C.c_float, _vp, _vp,
+                                      _vp, _vp, _vp]),
+    ("nav_batch_sa", C.c_int, [C.c_int64, _vp, _vp, _vp]),
+    ("nav_fill", C.c_int, [_vp, C.c_int64, C.c_float, _vp]),
+    ("nav_strided_copy", C.c_int, [_vp, C.c_int32, C.c_int32, _vp, C.c_int32, C.c_int32,
+                                   C.c_int64, C.c_int32, _vp]),
+]
+
+# Entry points that return int64 counts (negative = error) rather than a status code.
+_COUNT_FNS = {"nav_mlp_param_count", "nav_mlp_packed_count"}
+
+
+class NavError(RuntimeError):
+    pass
+
+
+class _Checked:
+    def __init__(self, name, fn):
+        self.name, self.fn = name, fn
+
+    def __call__(self, *args):
+        r = self.fn(*args)
+        if self.fn.restype is C.c_int and r != 0 and self.name != "nav_abi_version":
+            what = "invalid argument" if r == NAV_EINVAL else f"HIP error {-r}"
+            raise NavError(f"{self.name} failed: {what}")
+        if self.name in _COUNT_FNS and r < 0:
+            raise NavError(f"{self.name}: invalid argument")
+        return r
+
+
+class _Lib:
+    def __init__(self, path=LIB_PATH):
+        if not os.path.exists(path):
+            raise NavError(f"{path} is missing: build it with `make -C "
+                           f"residual-td3-robot-navigation_amd` (or __graft_entry__.build())")
+        self.raw = C.CDLL(path)
+        for name, res, args in SIGNATURES:
+            fn = getattr(self.raw, name)
+            fn.restype = res
+            fn.argtypes = args
+            setattr(self, name, _Checked(name, fn))
+        v = self.nav_abi_version()
+        if v != ABI_VERSION:
+            raise NavError(f"libnavenv ABI {v} != {ABI_VERSION}")
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        _lib = _Lib()
+    return _lib
+
+
+def require_gpu():
+    if not torch.cuda.is_available():
+        raise NavError("nav needs a ROCm GPU (MI355X); no HIP device is visible")
+
+
+def ptr(t):
+    """Device pointer of a contiguous tensor (or None)."""
+    if t is None:
+        return None
+    assert t.is_contiguous(), "nav tensors must be contiguous"
+    return C.c_void_p(t.data_ptr())
+
+
+def stream_handle(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return C.c_void_p(s.cuda_stream)
+
+
+def params_struct(**kw):
+    p = NavParams()
+    lib().nav_default_params(C.byref(p))
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p

@@ -1,0 +1,85 @@
+"""Per-kernel timing with HIP events on the launch stream, and the algorithmic work counts the
+roofline figures use.
+
+`with timing(KernelTimer(...)):` activates a timer; every libnavenv launch site in nav/ wraps its
+launch in `region(name, work)`, which records a start/stop event pair on the current stream (the
+stream the kernel is launched on) when the timer tracks that name. Nothing is recorded otherwise.
+"""
+import contextlib
+from collections import defaultdict
+
+import torch
+
+# ---- algorithmic bytes per env-step (HBM-bound kernels) ----
+# nav_env_step: state r/w (16 + 16) + action (16)
+ENV_STEP_BYTES = 48
+# nav_agent_step, steady state (history full, no reset): reads state 16, action 16, goal 16,
+# meta 4, plan 4, path 4, history 5 x 16 = 80 (140); writes history slot 16, replay row 32,
+# state 16, plan 4, meta 4, next_state 16, goal_term 8, flags 1 (97)
+AGENT_STEP_BYTES = 237
+
+
+def mlp_fwd_flops(d_in, d_out, h, nh, rows):
+    return 2.0 * rows * (d_in * h + (nh - 1) * h * h + h * d_out)
+
+
+def mlp_bwd_flops(d_in, d_out, h, nh, rows, dx=False):
+    return 2.0 * rows * (d_out * h + (nh - 1) * h * h + (h * d_in if dx else 0))
+
+
+def mlp_wgrad_flops(d_in, d_out, h, nh, rows):
+    return 2.0 * rows * (d_in * h + (nh - 1) * h * h + h * d_out)
+
+
+def demo_flops(n_env, m):
+    # per point: 2 sub, 2 mul, 1 add, 1 min (f64)
+    return 6.0 * n_env * m
+
+
+class KernelTimer:
+    def __init__(self, names=None):
+        self.names = None if names is None else set(names)
+        self.rec = defaultdict(list)
+
+    def wants(self, name):
+        return self.names is None or name in self.names
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for name, lst in self.rec.items():
+            ms = [s.elapsed_time(e) for s, e, _ in lst]
+            work = sum(w for _, _, w in lst)
+            out[name] = {"launches": len(ms), "total_ms": sum(ms),
+                         "avg_us": 1e3 * sum(ms) / len(ms), "work": work,
+                         "work_per_launch": work / len(ms)}
+        return out
+
+
+_active = None
+
+
+@contextlib.contextmanager
+def timing(timer):
+    global _active
+    prev, _active = _active, timer
+    try:
+        yield timer
+    finally:
+        _active = prev
+
+
+@contextlib.contextmanager
+def region(name, work=0.0):
+    t = _active
+    if t is None or not t.wants(name):
+        yield
+        return
+    s = torch.cuda.Event(enable_timing=True)
+    e = torch.cuda.Event(enable_timing=True)
+    s.record()
+    try:
+        yield
+    finally:
+        e.record()
+        t.rec[name].append((s, e, work))

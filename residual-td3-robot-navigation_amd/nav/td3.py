@@ -1,0 +1,229 @@
+"""Residual-TD3 learner on the GPU (robot.py:209-398), every FLOP in libnavenv.so kernels.
+
+Method names follow the reference: td3_update, train_critic, train_actor, soft_update. Networks
+live as DeviceMLP flat buffers; Adam moments live beside them; torch only allocates memory and
+provides the stream. Sampling: robot.py:98-115 draws `batch_size` rows without replacement from a
+<=10 000-row buffer; here rows are drawn with replacement by Philox (NAV_TAG_SAMPLE) from the
+device ring, or taken from an injected index tensor (parity tests, the N=1 drop-in).
+"""
+import ctypes as C
+import math
+
+import torch
+
+from . import config as K
+from . import prof
+from ._lib import lib, ptr, stream_handle
+from .mlp import DeviceMLP, forward
+
+
+class _Adam:
+    """torch.optim.Adam state for one flat parameter buffer (robot.py:236-239)."""
+
+    def __init__(self, net, lr, betas=(0.9, 0.999), eps=1e-8):
+        self.net, self.lr, self.b1, self.b2, self.eps = net, lr, betas[0], betas[1], eps
+        self.m = torch.zeros_like(net.params)
+        self.v = torch.zeros_like(net.params)
+        self.step_count = 0
+
+    def step(self, grad, stream=None):
+        self.step_count += 1
+        bc1 = 1 - self.b1 ** self.step_count
+        bc2 = 1 - self.b2 ** self.step_count
+        d = self.net.desc()
+        lib().nav_adam(C.byref(d), ptr(grad), ptr(self.m), ptr(self.v), self.b1, self.b2,
+                       self.eps, self.lr / bc1, math.sqrt(bc2), stream_handle(stream))
+
+    def state_dict(self):
+        return {"m": self.m.cpu(), "v": self.v.cpu(), "t": self.step_count}
+
+    def load_state_dict(self, sd):
+        self.m.copy_(sd["m"]); self.v.copy_(sd["v"]); self.step_count = sd["t"]
+
+
+class TD3:
+    def __init__(self, cfg=None, device="cuda", seed=K.RANDOM_SEED, actor=None, critic1=None,
+                 critic2=None, grad_hook=None):
+        self.cfg = cfg or K.TD3Config()
+        c = self.cfg
+        nc = c.net
+        self.device = torch.device(device)
+        mk = lambda di, do: DeviceMLP(di, do, nc.hidden, nc.n_hidden, self.device)  # noqa: E731
+        g = torch.Generator().manual_seed(seed)
+        self.actor_network = actor or mk(2, 2).init_kaiming(g)
+        self.critic_network_1 = critic1 or mk(4, 1).init_kaiming(g)
+        self.critic_network_2 = critic2 or mk(4, 1).init_kaiming(g)
+        # robot.py:232-234 deep copies
+        self.target_actor = mk(2, 2).copy_from(self.actor_network)
+        self.target_critic_network_1 = mk(4, 1).copy_from(self.critic_network_1)
+        self.target_critic_network_2 = mk(4, 1).copy_from(self.critic_network_2)
+        self.actor_optimizer = _Adam(self.actor_network, c.actor_lr)
+        self.critic_optimizer_1 = _Adam(self.critic_network_1, c.critic_lr)
+        self.critic_optimizer_2 = _Adam(self.critic_network_2, c.critic_lr)
+        self.seed = seed
+        self.update_counter = 0  # Philox counter for sampling / smoothing noise
+        self.grad_hook = grad_hook  # e.g. RCCL all-reduce of flat grads (shared policy)
+        self._B = 0
+        self.actor_losses, self.critic_losses = [], []
+
+    # ---- workspace, sized per batch
+    def _workspace(self, B):
+        if B == self._B:
+            return
+        d, hp, nh = self.device, self.actor_network.hp, self.actor_network.n_hidden
+        f = lambda *s: torch.zeros(*s, dtype=torch.float32, device=d)  # noqa: E731
+        self.batch = f(B, 8)
+        self.batch2 = f(B, 8)
+        self.sa = f(B, 4)
+        self.tgt_in = f(B, 4)
+        self.q1t, self.q2t, self.q1, self.q2 = f(B), f(B), f(B), f(B)
+        self.dq1, self.dq2, self.y = f(B), f(B), f(B)
+        self.acts1, self.acts2 = f(nh, B, hp), f(nh, B, hp)
+        self.dz1, self.dz2 = f(nh, B, hp), f(nh, B, hp)
+        self.acts_a, self.dz_a = f(nh, B, hp), f(nh, B, hp)
+        self.dx = f(B, 4)
+        self.da = f(B, 2)
+        self.loss_part = f((B + 255) // 256, 2)
+        self.splits = max(1, min(64, B // 512))
+        cmax = max(self.actor_network.count, self.critic_network_1.count)
+        self.slabs = f(self.splits, cmax)
+        self.grad_a = f(self.actor_network.count)
+        self.grad_c1 = f(self.critic_network_1.count)
+        self.grad_c2 = f(self.critic_network_1.count)
+        self._B = B
+
+    def _grads(self, net, M, inp, ld_in, in_col, acts, dz, dy, grad, s):
+        with prof.region("mlp_wgrad", prof.mlp_wgrad_flops(net.d_in, net.d_out, net.hidden,
+                                                             net.n_hidden, M)):
+            lib().nav_mlp_wgrad(C.byref(net.desc()), M, ptr(inp), ld_in, in_col, ptr(acts),
+                                ptr(dz), ptr(dy), ptr(self.slabs), self.splits, s)
+        with prof.region("grad_reduce", 4.0 * (self.splits + 1) * net.count):
+            lib().nav_grad_reduce(ptr(self.slabs), self.splits, net.count, ptr(grad), s)
+        if self.grad_hook is not None:
+            self.grad_hook(grad)
+
+    def _bwd(self, net, M, dy, acts, dz, dx, s):
+        with prof.region("mlp_bwd", prof.mlp_bwd_flops(net.d_in, net.d_out, net.hidden,
+                                                         net.n_hidden, M, dx is not None)):
+            lib().nav_mlp_backward(C.byref(net.desc()), M, ptr(dy), ptr(acts), ptr(dz), ptr(dx),
+                                   s)
+
+    def _sample(self, replay, B, out, idx=None, stream=None):
+        """ReplayBuffer.sample (robot.py:98-115) into a [B][8] batch."""
+        rd = replay.desc()
+        ctr = self.update_counter * 2 + (0 if out is self.batch else 1)
+        lib().nav_replay_sample(C.byref(rd), len(replay), B, ptr(idx),
+                                self.seed & 0xFFFFFFFF, (self.seed >> 32) & 0xFFFFFFFF, ctr,
+                                ptr(out), stream_handle(stream))
+
+    # robot.py:312-366
+    def train_critic(self, replay, idx=None, eps=None, stream=None):
+        c = self.cfg
+        B = c.batch_size
+        self._workspace(B)
+        s = stream_handle(stream)
+        self._sample(replay, B, self.batch, idx, stream)
+        bt = self.batch
+        # target action with smoothing noise: tgt_in = (s', clamp(pi'(s') + clip(eps*.2), +-5))
+        lib().nav_strided_copy(ptr(bt), 8, 5, ptr(self.tgt_in), 4, 0, B, 2, s)
+        forward([self.target_actor], bt, 8, 5, [self.tgt_in], 4, 2, B, out_mode=1, eps=eps,
+                policy_noise=c.policy_noise, noise_clip=c.noise_clip, max_action=c.max_action,
+                seed=(self.seed & 0xFFFFFFFF, (self.seed >> 32) & 0xFFFFFFFF),
+                counter=self.update_counter, stream=stream)
+        forward([self.target_critic_network_1, self.target_critic_network_2], self.tgt_in, 4, 0,
+                [self.q1t, self.q2t], 1, 0, B, stream=stream)
+        lib().nav_batch_sa(B, ptr(bt), ptr(self.sa), s)
+        forward([self.critic_network_1, self.critic_network_2], self.sa, 4, 0,
+                [self.q1, self.q2], 1, 0, B, acts=[self.acts1, self.acts2], stream=stream)
+        lib().nav_td3_critic_loss(B, ptr(bt), ptr(self.q1t), ptr(self.q2t), ptr(self.q1),
+                                  ptr(self.q2), c.gamma, ptr(self.dq1), ptr(self.dq2),
+                                  ptr(self.y), ptr(self.loss_part), s)
+        for net, opt, acts, dz, dq, grad in (
+                (self.critic_network_1, self.critic_optimizer_1, self.acts1, self.dz1, self.dq1,
+                 self.grad_c1),
+                (self.critic_network_2, self.critic_optimizer_2, self.acts2, self.dz2, self.dq2,
+                 self.grad_c2)):
+            self._bwd(net, B, dq, acts, dz, None, s)
+            self._grads(net, B, self.sa, 4, 0, acts, dz, dq, grad, s)
+            opt.step(grad, stream)
+
+    def critic_loss_values(self):
+        """(loss1, loss2) of the last train_critic (mean squared TD error), synchronising."""
+        t = self.loss_part.sum(0) / self._B
+        return t[0].item(), t[1].item()
+
+    # robot.py:369-398
+    def train_actor(self, replay, idx=None, stream=None):
+        c = self.cfg
+        B = c.batch_size
+        self._workspace(B)
+        s = stream_handle(stream)
+        self._sample(replay, B, self.batch2, idx, stream)
+        bt = self.batch2
+        lib().nav_strided_copy(ptr(bt), 8, 0, ptr(self.sa), 4, 0, B, 2, s)
+        forward([self.actor_network], bt, 8, 0, [self.sa], 4, 2, B, acts=[self.acts_a],
+                stream=stream)
+        forward([self.critic_network_1], self.sa, 4, 0, [self.q1], 1, 0, B, acts=[self.acts1],
+                stream=stream)
+        # d(-mean Q)/dQ = -1/B; backprop through critic 1 to its action input
+        lib().nav_fill(ptr(self.dq1), B, -1.0 / B, s)
+        self._bwd(self.critic_network_1, B, self.dq1, self.acts1, self.dz1, self.dx, s)
+        lib().nav_strided_copy(ptr(self.dx), 4, 2, ptr(self.da), 2, 0, B, 2, s)
+        net = self.actor_network
+        self._bwd(net, B, self.da, self.acts_a, self.dz_a, None, s)
+        self._grads(net, B, bt, 8, 0, self.acts_a, self.dz_a, self.da, self.grad_a, s)
+        self.actor_optimizer.step(self.grad_a, stream)
+
+    def actor_loss_value(self):
+        return -(self.q1.sum() / self._B).item()
+
+    # robot.py:293-310
+    def soft_update(self, target, source, tau, stream=None):
+        lib().nav_polyak(C.byref(target.desc()), C.byref(source.desc()), tau,
+                         stream_handle(stream))
+
+    def soft_update_all(self, stream=None):
+        t = self.cfg.tau
+        self.soft_update(self.target_actor, self.actor_network, t, stream)
+        self.soft_update(self.target_critic_network_1, self.critic_network_1, t, stream)
+        self.soft_update(self.target_critic_network_2, self.critic_network_2, t, stream)
+
+    # robot.py:258-285
+    def td3_update(self, replay, num_epochs=None, idx_fn=None, eps_fn=None, stream=None,
+                   track_losses=False):
+        n = self.cfg.num_epochs if num_epochs is None else num_epochs
+        if len(replay) < 1:
+            return
+        for epoch in range(n):
+            self.train_critic(replay, idx=idx_fn() if idx_fn else None,
+                              eps=eps_fn() if eps_fn else None, stream=stream)
+            if track_losses:
+                self.critic_losses.append(sum(self.critic_loss_values()) / 2)
+            if epoch % self.cfg.policy_update_delay == 0:
+                self.train_actor(replay, idx=idx_fn() if idx_fn else None, stream=stream)
+                if track_losses:
+                    self.actor_losses.append(self.actor_loss_value())
+                self.soft_update_all(stream)
+            self.update_counter += 1
+
+    def networks(self):
+        return {"actor": self.actor_network, "critic1": self.critic_network_1,
+                "critic2": self.critic_network_2, "target_actor": self.target_actor,
+                "target_critic1": self.target_critic_network_1,
+                "target_critic2": self.target_critic_network_2}
+
+    def state_dict(self):
+        sd = {k: v.state_dict() for k, v in self.networks().items()}
+        sd["opt"] = {k: o.state_dict() for k, o in (("actor", self.actor_optimizer),
+                                                     ("critic1", self.critic_optimizer_1),
+                                                     ("critic2", self.critic_optimizer_2))}
+        sd["update_counter"] = self.update_counter
+        return sd
+
+    def load_state_dict(self, sd):
+        for k, v in self.networks().items():
+            v.load_state_dict(sd[k])
+        self.actor_optimizer.load_state_dict(sd["opt"]["actor"])
+        self.critic_optimizer_1.load_state_dict(sd["opt"]["critic1"])
+        self.critic_optimizer_2.load_state_dict(sd["opt"]["critic2"])
+        self.update_counter = sd["update_counter"]

@@ -1,0 +1,80 @@
+"""Vectorised residual-TD3 training loop on one GPU (the MI355X form of robot-learning.py's
+training mode, robot-learning.py:54-101, for n independent envs at once).
+
+One `step()` = one vector tick: every env selects an action (actor MLP + baseline + exploration
+noise, nav_act), takes one environment step with the fused reward / stuck / done / replay-push /
+auto-reset tick (nav_agent_step + nav_demo_reward), then the learner runs `updates_per_step`
+TD3 epochs (robot.py:272-285: critic every epoch, actor + Polyak every `policy_update_delay`-th)
+on batches sampled from the device replay ring. The reference's schedule (100 epochs of batch
+100 at every episode end) does not map onto 65 536 asynchronous envs; the update-to-data ratio
+here is updates_per_step * batch / n_envs sampled transitions per collected transition.
+"""
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import config as K
+from . import prof
+from ._lib import lib, ptr, stream_handle
+from .demos import synthetic_group_demo_sets
+from .fields import make_fields
+from .td3 import TD3
+from .vec_env import ReplayRing, VecEnv, make_field
+
+
+class VecTrainer:
+    def __init__(self, n_envs=65536, hidden=256, n_hidden=2, batch=32768, updates_per_step=2,
+                 replay_capacity=None, seed=K.RANDOM_SEED, envs_per_group=1024, demos=True,
+                 device="cuda", field=None, grad_hook=None):
+        self.n = int(n_envs)
+        self.device = torch.device(device)
+        self.seed = int(seed)
+        if field is None:
+            speed, angle = make_fields(self.seed)
+            field = make_field(speed, angle, self.device)
+        self.field = field
+        epg = int(envs_per_group) if envs_per_group else self.n
+        self.env = VecEnv(self.n, field, seed=self.seed, envs_per_group=epg, demo_flag=demos,
+                          device=self.device)
+        if demos:
+            G = (self.n + epg - 1) // epg
+            firsts = torch.arange(G, device=self.device) * epg
+            regions = self.env.region[firsts].cpu().numpy()
+            goals = self.env.goal[firsts].cpu().numpy()
+            pts, off = synthetic_group_demo_sets(regions, goals, self.seed)
+            self.env.set_demo(pts, off if G > 1 else None)
+        cfg = K.TD3Config(batch_size=int(batch), num_epochs=int(updates_per_step),
+                          net=K.NetConfig(hidden=hidden, n_hidden=n_hidden))
+        self.td3 = TD3(cfg, device=self.device, seed=self.seed, grad_hook=grad_hook)
+        cap = replay_capacity or max(4 * self.n, 2 * int(batch), K.BUFFER_SIZE)
+        self.replay = ReplayRing(cap, self.device)
+        self.action = torch.zeros(self.n, 2, dtype=torch.float64, device=self.device)
+        self.steps = 0
+        self.updates_per_step = int(updates_per_step)
+
+    # robot.py:541-569 for every env
+    def act(self, training=True, stream=None):
+        net = self.td3.actor_network
+        a = net.desc()
+        with prof.region("act", prof.mlp_fwd_flops(2, 2, net.hidden, net.n_hidden, self.n)):
+            lib().nav_act(C.byref(self.env.p), C.byref(a), self.n, ptr(self.env.state),
+                          ptr(self.env.goal), ptr(self.env.noise_scale), None, self.steps,
+                          0 if training else 1, ptr(self.action), None, stream_handle(stream))
+        return self.action
+
+    def collect(self, stream=None):
+        self.act(True, stream)
+        self.env.agent_step(self.action, self.replay, stream)
+        self.steps += 1
+
+    def learn(self, stream=None):
+        if len(self.replay) >= self.td3.cfg.batch_size and self.updates_per_step > 0:
+            self.td3.td3_update(self.replay, self.updates_per_step, stream=stream)
+
+    def step(self, stream=None):
+        self.collect(stream)
+        self.learn(stream)
+
+    def env_steps(self):
+        return self.steps * self.n

@@ -1,0 +1,139 @@
+"""Vectorised Environment + Robot per-step state on one GPU (environment.py, robot.py:413-538).
+
+`VecEnv` owns the structure-of-arrays per-env state as torch tensors (device memory) and drives the
+gfx950 kernels of libnavenv.so through the C-ABI. One env = one lane; n envs advance per launch.
+"""
+import ctypes as C
+
+import torch
+
+from . import config as K
+from . import prof
+from ._lib import (NavEnvSoa, NavReplay, NavStepOut, lib, params_struct, ptr, require_gpu,
+                   stream_handle)
+
+
+def make_field(speed, angle, device="cuda"):
+    """Interleave Environment.dynamics_speed / dynamics_angle ([100,100] float32, x-major) into the
+    kernels' [100][100][2] table."""
+    s = torch.as_tensor(speed, dtype=torch.float32)
+    a = torch.as_tensor(angle, dtype=torch.float32)
+    assert s.shape == (100, 100) and a.shape == (100, 100)
+    return torch.stack([s, a], dim=-1).contiguous().to(device)
+
+
+class ReplayRing:
+    """ReplayBuffer (robot.py:58-124) as a device ring of 32-byte rows
+    (s0 s1 a0 a1 r s'0 s'1 done, float32)."""
+
+    def __init__(self, capacity, device="cuda"):
+        self.capacity = int(capacity)
+        self.rows = torch.zeros(self.capacity, 8, dtype=torch.float32, device=device)
+        self.position = 0  # next write slot (robot.py:77)
+        self.size = 0
+
+    def desc(self):
+        return NavReplay(self.rows.data_ptr(), self.capacity)
+
+    def advance(self, n):
+        base = self.position
+        self.position = (self.position + n) % self.capacity
+        self.size = min(self.size + n, self.capacity)
+        return base
+
+    def __len__(self):
+        return self.size
+
+
+class VecEnv:
+    def __init__(self, n, field, seed=K.RANDOM_SEED, envs_per_group=1, demo_flag=True,
+                 device="cuda", init=True, **param_overrides):
+        require_gpu()
+        self.n = int(n)
+        self.device = torch.device(device)
+        self.field = field
+        self.p = params_struct(seed_lo=seed & 0xFFFFFFFF, seed_hi=(seed >> 32) & 0xFFFFFFFF,
+                               **param_overrides)
+        self.envs_per_group = int(envs_per_group)
+        d, n = self.device, self.n
+        f64, i32 = torch.float64, torch.int32
+        self.state = torch.zeros(n, 2, dtype=f64, device=d)
+        self.goal = torch.zeros(n, 2, dtype=f64, device=d)
+        self.region = torch.zeros(n, 4, dtype=f64, device=d)
+        self.hist = torch.zeros(5, n, 2, dtype=f64, device=d)
+        self.meta = torch.zeros(n, dtype=torch.int32, device=d)  # uint32 bits
+        self.plan_index = torch.zeros(n, dtype=i32, device=d)
+        self.path_length = torch.zeros(n, dtype=i32, device=d)
+        self.episodes = torch.zeros(n, dtype=i32, device=d)
+        self.noise_scale = torch.zeros(n, dtype=f64, device=d)
+        # per-step outputs
+        self.next_state = torch.zeros(n, 2, dtype=f64, device=d)
+        self.goal_term = torch.zeros(n, dtype=f64, device=d)
+        self.flags = torch.zeros(n, dtype=torch.uint8, device=d)
+        self.block_stats = torch.zeros((n + 255) // 256, 8, dtype=torch.float32, device=d)
+        self.goal_draws = torch.zeros(n, dtype=i32, device=d)
+        self.soa = NavEnvSoa(n, *[t.data_ptr() for t in (
+            self.state, self.goal, self.region, self.hist, self.meta, self.plan_index,
+            self.path_length, self.episodes, self.noise_scale)])
+        self.out = NavStepOut(self.next_state.data_ptr(), self.goal_term.data_ptr(),
+                              self.flags.data_ptr(), self.block_stats.data_ptr())
+        self.demo_xy = None
+        self.demo_off = None
+        if init:
+            self.init(demo_flag)
+
+    # environment.py:107-135 + robot.py:413-438 (vectorised, Philox)
+    def init(self, demo_flag=True, stream=None):
+        lib().nav_env_init(C.byref(self.p), C.byref(self.soa), self.envs_per_group,
+                           int(bool(demo_flag)), ptr(self.goal_draws), stream_handle(stream))
+
+    # environment.py:209-216
+    def reset(self, mask=None, uniforms=None, stream=None):
+        lib().nav_env_reset(C.byref(self.p), C.byref(self.soa), ptr(mask), ptr(uniforms),
+                            stream_handle(stream))
+        return self.state
+
+    # environment.py:201-206 (pure Environment.step over all envs)
+    def step(self, action, next_state=None, stream=None):
+        with prof.region("env_step", float(prof.ENV_STEP_BYTES * self.n)):
+            lib().nav_env_step(C.byref(self.p), C.byref(self.soa), ptr(self.field), ptr(action),
+                               ptr(next_state), stream_handle(stream))
+        return self.state
+
+    def dynamics(self, state, action, out=None, stream=None):
+        out = out if out is not None else torch.empty_like(state)
+        lib().nav_dynamics(ptr(self.field), ptr(state), ptr(action), ptr(out), state.shape[0],
+                           stream_handle(stream))
+        return out
+
+    # demonstration set used by the demo-proximity reward (robot.py:749-757)
+    def set_demo(self, demo_xy, demo_off=None):
+        self.demo_xy = torch.as_tensor(demo_xy, dtype=torch.float64).reshape(-1, 2).contiguous()
+        self.demo_xy = self.demo_xy.to(self.device)
+        self.demo_off = None
+        if demo_off is not None:
+            self.demo_off = torch.as_tensor(demo_off, dtype=torch.int64).to(self.device)
+
+    # one fused training tick (robot.py:443-506, 645-675 + environment.py:201-216)
+    def agent_step(self, action, replay, stream=None, reward_out=None):
+        base = replay.position
+        s = stream_handle(stream)
+        rd = replay.desc()
+        with prof.region("agent_step", float(prof.AGENT_STEP_BYTES * self.n)):
+            lib().nav_agent_step(C.byref(self.p), C.byref(self.soa), ptr(self.field),
+                                 ptr(action), C.byref(rd), base, C.byref(self.out), s)
+        if self.demo_xy is not None and self.demo_xy.shape[0] > 0:
+            m = self.demo_xy.shape[0] if self.demo_off is None else 0
+            m_per = self.demo_xy.shape[0] if self.demo_off is None else \
+                self.demo_xy.shape[0] / max(1, self.demo_off.shape[0] - 1)
+            with prof.region("demo_reward", prof.demo_flops(self.n, m_per)):
+                lib().nav_demo_reward(C.byref(self.p), self.n, ptr(self.next_state),
+                                      ptr(self.goal_term), ptr(self.flags), ptr(self.demo_xy),
+                                      ptr(self.demo_off), m, self.envs_per_group, C.byref(rd),
+                                      base, ptr(reward_out), s)
+        replay.advance(self.n)
+        return base
+
+    def stats(self):
+        """Sum of the per-block rows: reward (w/o demo term), done, goal, stuck, ended."""
+        return self.block_stats.sum(0)[:5].tolist()

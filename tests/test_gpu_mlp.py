@@ -1,0 +1,266 @@
+"""GPU parity of the MFMA MLP kernels and the TD3 learner.
+
+Numerics bar: the kernels compute in exact fp32 (v_mfma_f32_32x32x2_f32 is an fp32 fma chain);
+against a torch fp32 reference of the same op the only difference is summation order, so outputs
+and gradients agree to rtol 1e-4 / atol scaled by the operand magnitudes (stated per test)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def nav():
+    from nav import _lib
+    _lib.require_gpu()
+    _lib.lib()
+    import nav as navpkg
+    return navpkg
+
+
+def torch_mlp(layers, x):
+    h = x
+    for i, (W, b) in enumerate(layers):
+        h = torch.nn.functional.linear(h, W, b)
+        if i < len(layers) - 1:
+            h = torch.relu(h)
+    return h
+
+
+def make_net(d_in, d_out, hidden, nh, seed):
+    from nav.mlp import DeviceMLP
+    from oracle.td3_oracle import make_mlp_params
+    p = make_mlp_params(seed, [d_in] + [hidden] * nh + [d_out])
+    net = DeviceMLP(d_in, d_out, hidden, nh, DEV).load(p)
+    return net, [(torch.tensor(W), torch.tensor(b)) for W, b in p]
+
+
+@pytest.mark.parametrize("d_in,d_out,hidden,nh", [(2, 2, 200, 3), (4, 1, 200, 3), (2, 2, 256, 2),
+                                                  (4, 1, 256, 2), (4, 1, 64, 1), (2, 2, 96, 4)])
+@pytest.mark.parametrize("M", [1, 100, 1000, 4097])
+def test_forward_vs_torch(nav, d_in, d_out, hidden, nh, M):
+    from nav.mlp import forward
+    net, layers = make_net(d_in, d_out, hidden, nh, 5)
+    x = torch.randn(M, d_in) * 20
+    out = torch.zeros(M, d_out, device=DEV)
+    acts = torch.zeros(nh, M, net.hp, device=DEV)
+    forward([net], x.to(DEV).contiguous(), d_in, 0, [out], d_out, 0, M, acts=[acts])
+    ref = torch_mlp(layers, x)
+    scale = ref.abs().max().item() + 1
+    assert torch.allclose(out.cpu(), ref, rtol=1e-4, atol=1e-5 * scale)
+    # saved activations = post-ReLU hidden outputs, zero in the padded columns
+    h = x
+    for l in range(nh):
+        h = torch.relu(torch.nn.functional.linear(h, *layers[l]))
+        a = acts[l].cpu()
+        assert torch.allclose(a[:, :hidden], h, rtol=1e-4, atol=1e-5 * (h.abs().max() + 1))
+        assert (a[:, hidden:] == 0).all()
+
+
+def test_twin_forward_and_target_smoothing(nav):
+    from nav.mlp import forward
+    c1, L1 = make_net(4, 1, 200, 3, 7)
+    c2, L2 = make_net(4, 1, 200, 3, 8)
+    M = 999
+    x = torch.randn(M, 4) * 10
+    o1, o2 = torch.zeros(M, 1, device=DEV), torch.zeros(M, 1, device=DEV)
+    forward([c1, c2], x.to(DEV), 4, 0, [o1, o2], 1, 0, M)
+    for o, L in ((o1, L1), (o2, L2)):
+        r = torch_mlp(L, x)
+        assert torch.allclose(o.cpu(), r, rtol=1e-4, atol=1e-5 * (r.abs().max() + 1))
+    # robot.py:338-339 smoothing epilogue with injected eps
+    a, La = make_net(2, 2, 200, 3, 9)
+    s = torch.rand(M, 8) * 100
+    eps = torch.randn(M, 2)
+    out = torch.zeros(M, 4, device=DEV)
+    forward([a], s.to(DEV), 8, 5, [out], 4, 2, M, out_mode=1, eps=eps.to(DEV))
+    ref = (torch_mlp(La, s[:, 5:7]) + (eps * 0.2).clamp(-0.5, 0.5)).clamp(-5, 5)
+    assert torch.allclose(out[:, 2:].cpu(), ref, rtol=1e-4, atol=1e-4)
+    assert (out[:, :2] == 0).all()
+
+
+def test_act_vs_reference_golden(nav, orc):
+    """Robot.get_next_action_training/testing (robot.py:541-595) on the reference's goldens."""
+    from nav._lib import lib, params_struct, ptr, stream_handle
+    from nav.mlp import DeviceMLP
+    from oracle.td3_oracle import make_mlp_params
+    g = golden("actions.npz")
+    actor = DeviceMLP(2, 2, 200, 3, DEV).load(make_mlp_params(int(g["actor_seed"]),
+                                                               [2, 200, 200, 200, 2]))
+    n = len(g["states"])
+    st = torch.tensor(g["states"], device=DEV)
+    gl = torch.tensor(g["goals"], device=DEV)
+    sig = torch.tensor(g["sigmas"], device=DEV)
+    z = torch.tensor(g["z"], device=DEV)
+    act = torch.zeros(n, 2, dtype=torch.float64, device=DEV)
+    res = torch.zeros(n, 2, device=DEV)
+    p = params_struct()
+    d = actor.desc()
+    lib().nav_act(C.byref(p), C.byref(d), n, ptr(st), ptr(gl), ptr(sig), ptr(z), 0, 0, ptr(act),
+                  ptr(res), stream_handle())
+    r = res.cpu().numpy()
+    assert np.allclose(r, g["residual"], rtol=2e-5, atol=1e-4)
+    a = act.cpu().numpy()
+    # epilogue exact given the residual the device computed
+    for i in range(n):
+        assert np.array_equal(a[i], orc.act_epilogue(g["states"][i], g["goals"][i], r[i],
+                                                     g["sigmas"][i], g["z"][i]))
+    assert np.allclose(a, g["action_train"], rtol=0, atol=2e-4)
+    lib().nav_act(C.byref(p), C.byref(d), n, ptr(st), ptr(gl), None, None, 0, 1, ptr(act),
+                  None, stream_handle())
+    assert np.allclose(act.cpu().numpy(), g["action_test"], rtol=0, atol=2e-4)
+
+
+@pytest.mark.parametrize("d_in,d_out,hidden,nh,M", [(4, 1, 200, 3, 100), (2, 2, 200, 3, 777),
+                                                    (4, 1, 256, 2, 5000), (2, 2, 256, 2, 4096),
+                                                    (4, 1, 64, 1, 300)])
+def test_backward_and_weight_grads_vs_autograd(nav, d_in, d_out, hidden, nh, M):
+    from nav._lib import lib, ptr, stream_handle
+    from nav.mlp import forward
+    net, layers = make_net(d_in, d_out, hidden, nh, 11)
+    x = (torch.randn(M, d_in) * 10).contiguous()
+    dy = torch.randn(M, d_out) / M
+    out = torch.zeros(M, d_out, device=DEV)
+    acts = torch.zeros(nh, M, net.hp, device=DEV)
+    xd = x.to(DEV)
+    forward([net], xd, d_in, 0, [out], d_out, 0, M, acts=[acts])
+    dz = torch.zeros(nh, M, net.hp, device=DEV)
+    dx = torch.zeros(M, d_in, device=DEV)
+    s = stream_handle()
+    dyd = dy.to(DEV)
+    lib().nav_mlp_backward(C.byref(net.desc()), M, ptr(dyd), ptr(acts), ptr(dz), ptr(dx), s)
+    splits = 7
+    slabs = torch.zeros(splits, net.count, device=DEV)
+    grad = torch.zeros(net.count, device=DEV)
+    lib().nav_mlp_wgrad(C.byref(net.desc()), M, ptr(xd), d_in, 0, ptr(acts), ptr(dz), ptr(dyd),
+                        ptr(slabs), splits, s)
+    lib().nav_grad_reduce(ptr(slabs), splits, net.count, ptr(grad), s)
+    # torch autograd reference
+    tl = [(W.clone().requires_grad_(True), b.clone().requires_grad_(True)) for W, b in layers]
+    xr = x.clone().requires_grad_(True)
+    y = torch_mlp(tl, xr)
+    (y * dy).sum().backward()
+    assert torch.allclose(dx.cpu(), xr.grad, rtol=1e-3, atol=1e-6 * (xr.grad.abs().max() + 1e-3))
+    from nav.mlp import layer_offsets
+    offs, _ = layer_offsets(d_in, d_out, net.hp, nh)
+    gflat = grad.cpu()
+    for l, ((W, b), (w_off, b_off, fo, fi)) in enumerate(zip(tl, offs)):
+        o, i = W.shape
+        gW = gflat[w_off:w_off + fo * fi].view(fo, fi)
+        tol = 1e-5 * (W.grad.abs().max() + 1e-6)
+        assert torch.allclose(gW[:o, :i], W.grad, rtol=1e-3, atol=tol), l
+        assert (gW[o:, :] == 0).all() and (gW[:, i:] == 0).all()
+        gb = gflat[b_off:b_off + o]
+        assert torch.allclose(gb, b.grad, rtol=1e-3, atol=1e-5 * (b.grad.abs().max() + 1e-6)), l
+
+
+def test_adam_and_polyak_vs_oracle(nav):
+    from nav.td3 import _Adam
+    from oracle.td3_oracle import Adam
+    net, layers = make_net(4, 1, 200, 3, 12)
+    tgt, _ = make_net(4, 1, 200, 3, 13)
+    opt = _Adam(net, 1e-3)
+    ref_t = [t for W, b in layers for t in (W.clone(), b.clone())]
+    ref_opt = Adam(ref_t, 1e-3)
+    from nav.mlp import layer_offsets
+    offs, _ = layer_offsets(4, 1, net.hp, 3)
+    for step in range(3):
+        grads = [torch.randn_like(t) for t in ref_t]
+        flat = torch.zeros(net.count)
+        for l, (w_off, b_off, fo, fi) in enumerate(offs):
+            gW, gb = grads[2 * l], grads[2 * l + 1]
+            flat[w_off:w_off + fo * fi].view(fo, fi)[:gW.shape[0], :gW.shape[1]] = gW
+            flat[b_off:b_off + gb.shape[0]] = gb
+        opt.step(flat.to(DEV))
+        ref_opt.step(grads)
+    got = net.export()
+    for l, (W, b) in enumerate(got):
+        assert torch.allclose(W, ref_t[2 * l], rtol=0, atol=2e-7)
+        assert torch.allclose(b, ref_t[2 * l + 1], rtol=0, atol=2e-7)
+    # packed images follow the params: a forward through the updated net matches torch
+    from nav.mlp import forward
+    x = torch.randn(300, 4)
+    o = torch.zeros(300, 1, device=DEV)
+    forward([net], x.to(DEV), 4, 0, [o], 1, 0, 300)
+    ref = torch_mlp(got, x)
+    assert torch.allclose(o.cpu(), ref, rtol=1e-4, atol=1e-5 * (ref.abs().max() + 1))
+    # Polyak (robot.py:309)
+    from nav._lib import lib, stream_handle
+    before = [(W.clone(), b.clone()) for W, b in tgt.export()]
+    lib().nav_polyak(C.byref(tgt.desc()), C.byref(net.desc()), 0.001, stream_handle())
+    after = tgt.export()
+    for (W0, b0), (W1, b1), (Ws, bs) in zip(before, after, got):
+        assert torch.equal(W1, W0 * (1.0 - 0.001) + Ws * 0.001)
+        assert torch.equal(b1, b0 * (1.0 - 0.001) + bs * 0.001)
+
+
+def test_td3_update_vs_oracle_and_reference(nav):
+    """TD3.td3_update (robot.py:258-398) with the reference golden's weights, batches and noise:
+    losses and post-update parameters vs the oracle (and the reference's own digests)."""
+    from nav.td3 import TD3
+    from nav import config as K
+    from nav.mlp import DeviceMLP
+    from nav.vec_env import ReplayRing
+    from oracle.td3_oracle import TD3Oracle, make_mlp_params, param_digest
+    g = golden("td3.npz")
+    pa = make_mlp_params(21, [2, 200, 200, 200, 2])
+    p1 = make_mlp_params(22, [4, 200, 200, 200, 1])
+    p2 = make_mlp_params(23, [4, 200, 200, 200, 1])
+    mk = lambda di, do, p: DeviceMLP(di, do, 200, 3, DEV).load(p)  # noqa: E731
+    cfg = K.TD3Config(batch_size=int(g["B"]), num_epochs=int(g["epochs"]))
+    td3 = TD3(cfg, DEV, actor=mk(2, 2, pa), critic1=mk(4, 1, p1), critic2=mk(4, 1, p2))
+    S, A, R, S2, D = (g[k] for k in ("S", "A", "R", "S2", "D"))
+    rep = ReplayRing(len(S), DEV)
+    rows = np.concatenate([S, A, R[:, None], S2, D[:, None].astype(np.float64)], 1)
+    rep.rows.copy_(torch.tensor(rows, dtype=torch.float32))
+    rep.size = len(S)
+    idx = [torch.tensor(i, dtype=torch.int64, device=DEV) for i in g["idx"]]
+    eps = [torch.tensor(e, device=DEV) for e in g["noise"]]
+    it = {"s": 0, "n": 0}
+
+    def idx_fn():
+        x = idx[it["s"]]; it["s"] += 1
+        return x
+
+    def eps_fn():
+        x = eps[it["n"]]; it["n"] += 1
+        return x
+
+    td3.td3_update(rep, idx_fn=idx_fn, eps_fn=eps_fn, track_losses=True)
+    torch.cuda.synchronize()
+    closs = np.array(td3.critic_losses)
+    np.testing.assert_allclose(closs, g["critic_loss"].mean(1), rtol=1e-4)
+    np.testing.assert_allclose(np.array(td3.actor_losses), g["actor_loss"], rtol=1e-4)
+    # oracle run on the same inputs, full parameter comparison
+    ora = TD3Oracle(pa, p1, p2)
+    it2 = {"s": 0, "n": 0}
+
+    def sample():
+        i = g["idx"][it2["s"]]; it2["s"] += 1
+        return S[i], A[i], R[i], S2[i], D[i]
+
+    def nz():
+        x = g["noise"][it2["n"]]; it2["n"] += 1
+        return x
+
+    ora.td3_update(sample, nz, int(g["epochs"]))
+    mine = td3.networks()
+    for name, onet in ora.networks().items():
+        got = mine[name].export()
+        ref = onet.params
+        for (W, b), (Wr, br) in zip(got, ref):
+            # one Adam step moves a weight by ~lr = 1e-5; summation-order noise in the grads
+            # only matters where |g| ~ eps: compare with an absolute bar well under lr
+            assert torch.allclose(W, Wr, rtol=0, atol=2e-7), name
+            assert torch.allclose(b, br, rtol=0, atol=2e-7), name
+        # and the reference's own digests (sampled entries)
+        dig = param_digest([t for wb in got for t in wb])
+        for k, (_, _, ix, v) in enumerate(dig):
+            assert (ix == g[name + "_idx"][k]).all()
+            np.testing.assert_allclose(v, g[name + "_val"][k], rtol=0, atol=3e-7)
