@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--no-sweep", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--breakdown", action="store_true", help="print the per-kernel table")
+    ap.add_argument("--sweep-only", type=int, default=0,
+                    help="only run the step-kernel sweep at this N (profiling helper)")
     return ap.parse_args()
 
 
@@ -130,6 +132,12 @@ def main():
     lib()
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if args.sweep_only:
+        from nav.fields import make_fields
+        from nav.vec_env import make_field
+        print(json.dumps(step_kernel_sweep(make_field(*make_fields(args.seed), dev),
+                                           [args.sweep_only])), flush=True)
+        return
     hook = None
     if args.shared_policy and ws > 1:
         def hook(g):  # RCCL all-reduce (sum) over xGMI, then mean

@@ -169,16 +169,19 @@ int nav_act(const nav_params* p, const nav_mlp* actor, int64_t n, const double* 
  * x = in[m*ld_in + in_col + 0..d_in) (f32). out_mode 0: out[m*ld_out + out_col + j] = y;
  * out_mode 1 (target policy smoothing, robot.py:336-339): out = clamp(y + clamp(policy_noise*eps,
  * +-noise_clip), +-max_action) with eps from `eps` [M][2] f32 if given else Philox
- * (NAV_TAG_TNOISE, counter). acts (nullable per net): [n_hidden][M][hp] saved post-ReLU
- * activations for the backward pass. */
+ * (NAV_TAG_TNOISE, counter). acts (nullable, per net): [n_hidden][M][hp] saved post-ReLU
+ * activations (for nav_mlp_wgrad); masks (nullable, per net): nav_mlp_mask_count u16 words of
+ * ReLU-derivative bits (for nav_mlp_backward). */
 int nav_mlp_forward(const nav_mlp* nets, int32_t n_nets, int64_t M, const float* in,
                     int32_t ld_in, int32_t in_col, float* const* out, int32_t ld_out,
                     int32_t out_col, int32_t out_mode, const float* eps, float policy_noise,
                     float noise_clip, float max_action, uint32_t seed_lo, uint32_t seed_hi,
-                    uint32_t counter, float* const* acts, void* stream);
-/* Row-local backward of one network: given dL/dy [M][d_out] and the saved activations, writes
+                    uint32_t counter, float* const* acts, uint16_t* const* masks, void* stream);
+/* u16 words of the ReLU mask image for M rows (layout: [n_hidden][row tiles][hp/32][64]). */
+int64_t nav_mlp_mask_count(int32_t hidden_pad, int32_t n_hidden, int64_t M);
+/* Row-local backward of one network: given dL/dy [M][d_out] and the forward's ReLU masks, writes
  * dZ [n_hidden][M][hp] (dL/d pre-activation per hidden layer) and, if dx != NULL, dL/dx [M][d_in]. */
-int nav_mlp_backward(const nav_mlp* net, int64_t M, const float* dy, const float* acts,
+int nav_mlp_backward(const nav_mlp* net, int64_t M, const float* dy, const uint16_t* masks,
                      float* dz, float* dx, void* stream);
 /* Weight gradients of one network as `splits` partial slabs [splits][param_count] (row range of
  * split s = [s*M/splits, (s+1)*M/splits)); combine with nav_grad_reduce. */

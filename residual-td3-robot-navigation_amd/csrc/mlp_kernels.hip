@@ -1,13 +1,14 @@
 // mlp_kernels.hip — the residual-TD3 actor/critic MLPs (robot.py:128-206) and their learner
 // (robot.py:209-398) on gfx950.
 //
-// Forward / row-backward: one 256-thread workgroup = 4 waves = 128 rows; each wave owns 32 rows
-// and keeps them in LDS (fp32, row stride hp+4 so b128 fragment reads are conflict-free) across
-// all layers. Hidden x hidden layers run on v_mfma_f32_32x32x2_f32 (exact fp32): A fragments
-// from the wave's LDS rows, B fragments from an LDS-staged, double-buffered 8-deep K chunk of the
-// pre-packed weight image (one barrier per chunk). The thin input layer (K = 2 or 4) and output
-// layer (N = 1 or 2) run on the VALU. Weight gradients: a split-M MFMA kernel writing partial
-// slabs (deterministic), reduced in a fixed order.
+// Forward / row-backward: one 256-thread workgroup = 4 waves = a 128-row block kept in LDS (fp32,
+// row stride hp+4 so b128 fragment reads are conflict-free) across all layers. Hidden x hidden
+// layers run on v_mfma_f32_32x32x2_f32 (exact fp32): every wave owns 1-2 32-column tiles of all
+// 128 rows; A fragments come from the shared LDS rows, B fragments stream from the L2-resident
+// pre-packed weight image with a 2-step register prefetch, so the K loop has no barrier. The thin
+// input layer (K = 2 or 4) and output layer (N = 1 or 2) run on the VALU; ReLU derivatives travel
+// from forward to backward as C-layout bit masks. Weight gradients: one launch per network over
+// row splits writing deterministic partial slabs, reduced in a fixed order.
 #include "nav_device.h"
 
 using namespace nav;
@@ -60,70 +61,74 @@ NAV_DEV f32x16 mfma(float a, float b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
 
-// acc[t] += A[32 rows of the wave][hp] * B[hp][32t .. 32t+32), B from a packed image
-// [hp/4][hp][4] (element (k, n) at ((k>>2)*hp + n)*4 + (k&3)). The k order inside a chunk is
-// permuted consistently for A and B (lane half h takes k = 8q + 4h + s at MFMA s).
+NAV_DEV int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
+
+// Column tiles of a wave: wave w owns 32-column tiles t = w and w + 4 (when < NT) of every
+// 128-row block, for all 4 row tiles: acc[rt][j] is the 32x32 tile (rows rt*32.., cols t_j*32..).
 template <int NT>
-NAV_DEV void gemm_rows(const float* __restrict__ A, int S_, const float* __restrict__ Bp,
-                       float* __restrict__ wbuf, f32x16 (&acc)[NT]) {
+struct WaveCols {
+    int t0, t1;
+    bool has0, has1;
+    NAV_DEV WaveCols(int wv) : t0(wv), t1(wv + 4), has0(wv < NT), has1(wv + 4 < NT) {}
+};
+
+// acc[rt][j] = A[128 rows][hp] (LDS, row stride S_) x B[hp][tile t_j], B from a packed image in
+// global memory [hp/4][hp][4] (element (k, n) at ((k>>2)*hp + n)*4 + (k&3)) — L2-resident, read
+// once per workgroup, prefetched two K-steps ahead in registers. No barrier inside the K loop:
+// the LDS rows are read-only during the product. K order inside an 8-deep step is permuted the
+// same way for A and B (lane half h covers k = 8q + 4h + s at MFMA s).
+template <int NT>
+NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const float* __restrict__ Bp,
+                       f32x16 (&acc)[4][2]) {
     constexpr int hp = NT * 32;
-    constexpr int CH = 8 * hp;          // floats per chunk (2 quads)
     constexpr int nq = hp / 8;
-    constexpr int PER = (2 * hp + kBlock - 1) / kBlock;  // float4 per thread per chunk
-    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
+    const WaveCols<NT> wc(wv);
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
-        for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
-    float4 st[PER];
+    for (int rt = 0; rt < 4; ++rt)
 #pragma unroll
-    for (int j = 0; j < PER; ++j) {
-        const int i = tid + kBlock * j;
-        if (i < 2 * hp) st[j] = reinterpret_cast<const float4*>(Bp)[i];
-    }
+        for (int j = 0; j < 2; ++j)
 #pragma unroll
-    for (int j = 0; j < PER; ++j) {
-        const int i = tid + kBlock * j;
-        if (i < 2 * hp) reinterpret_cast<float4*>(wbuf)[i] = st[j];
-    }
-    __syncthreads();
+            for (int i = 0; i < 16; ++i) acc[rt][j][i] = 0.f;
+    if (!wc.has0) return;
+    const float4* B0 = reinterpret_cast<const float4*>(Bp) + (size_t)h * hp + wc.t0 * 32 + l32;
+    const float4* B1 = reinterpret_cast<const float4*>(Bp) + (size_t)h * hp + wc.t1 * 32 + l32;
+    constexpr size_t STEP = 2 * (size_t)hp;  // float4 per 8-deep K step
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 p0 = B0[0], p1 = nq > 1 ? B0[STEP] : z4;
+    float4 r0 = wc.has1 ? B1[0] : z4, r1 = (wc.has1 && nq > 1) ? B1[STEP] : z4;
     const float* arow = A + l32 * S_ + 4 * h;
     for (int q = 0; q < nq; ++q) {
-        if (q + 1 < nq) {
-#pragma unroll
-            for (int j = 0; j < PER; ++j) {
-                const int i = tid + kBlock * j;
-                if (i < 2 * hp) st[j] = reinterpret_cast<const float4*>(Bp + (q + 1) * CH)[i];
-            }
+        const float4 c0 = p0, c1 = r0;
+        p0 = p1;
+        r0 = r1;
+        if (q + 2 < nq) {
+            p1 = B0[(q + 2) * STEP];
+            if (wc.has1) r1 = B1[(q + 2) * STEP];
         }
-        const float* wb = wbuf + (q & 1) * CH + (h * hp + l32) * 4;
-        const float4 av = *reinterpret_cast<const float4*>(arow + 8 * q);
-        float4 bv[NT];
+        float4 a[4];
 #pragma unroll
-        for (int t = 0; t < NT; ++t) bv[t] = *reinterpret_cast<const float4*>(wb + 128 * t);
-#pragma unroll
-        for (int t = 0; t < NT; ++t) acc[t] = mfma(av.x, bv[t].x, acc[t]);
-#pragma unroll
-        for (int t = 0; t < NT; ++t) acc[t] = mfma(av.y, bv[t].y, acc[t]);
-#pragma unroll
-        for (int t = 0; t < NT; ++t) acc[t] = mfma(av.z, bv[t].z, acc[t]);
-#pragma unroll
-        for (int t = 0; t < NT; ++t) acc[t] = mfma(av.w, bv[t].w, acc[t]);
-        if (q + 1 < nq) {
-            float* nb = wbuf + ((q + 1) & 1) * CH;
-#pragma unroll
-            for (int j = 0; j < PER; ++j) {
-                const int i = tid + kBlock * j;
-                if (i < 2 * hp) reinterpret_cast<float4*>(nb)[i] = st[j];
-            }
-        }
-        __syncthreads();
+        for (int rt = 0; rt < 4; ++rt)
+            a[rt] = *reinterpret_cast<const float4*>(arow + rt * 32 * S_ + 8 * q);
+#define NAV_MF(S, C)                                                                     \
+    _Pragma("unroll") for (int rt = 0; rt < 4; ++rt) {                                  \
+        acc[rt][0] = mfma(a[rt].S, c0.S, acc[rt][0]);                                   \
+        if (NT >= 8 || wc.has1) acc[rt][1] = mfma(a[rt].S, c1.S, acc[rt][1]);           \
+    }
+        NAV_MF(x, 0) NAV_MF(y, 1) NAV_MF(z, 2) NAV_MF(w, 3)
+#undef NAV_MF
     }
 }
 
-NAV_DEV int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
-
 enum { IN_F32 = 0, IN_BASELINE = 1 };
 enum { OUT_F32 = 0, OUT_TARGET = 1, OUT_ACT = 2 };
+
+// ReLU masks: one 16-bit word per (row tile, column tile, lane) holding the lane's 16 C-layout
+// elements' (value > 0) bits; [n_hidden][row tiles][NT][64]. The backward reads 2 bytes per 16
+// elements instead of the 64 bytes of saved activations.
+NAV_DEV size_t mask_idx(int64_t rowtile, int NT_, int t, int lane) {
+    return ((size_t)rowtile * NT_ + t) * 64 + lane;
+}
 
 struct FwdArgs {
     MlpDev net[2];
@@ -133,6 +138,7 @@ struct FwdArgs {
     float* out[2];
     int ld_out, out_col;
     float* acts[2];
+    uint16_t* masks[2];
     // OUT_TARGET
     const float* eps;
     float policy_noise, noise_clip, max_action;
@@ -148,8 +154,44 @@ struct FwdArgs {
     double* action_out;
 };
 
-NAV_DEV size_t lds_floats(int hp) { return (size_t)TM * (hp + 4) + 16 * hp + 512; }
-inline size_t lds_bytes(int hp) { return ((size_t)TM * (hp + 4) + 16 * hp + 512) * 4; }
+inline size_t lds_bytes(int hp) { return ((size_t)TM * (hp + 4) + TM * 4) * 4; }
+
+// Store a layer's C-layout result into the LDS rows (the next layer's A operand) and its ReLU
+// mask bits. Global copies of the rows are written afterwards by copy_rows (coalesced).
+template <int NT>
+NAV_DEV void store_layer(f32x16 (&acc)[4][2], float* act, int S_, uint16_t* mask, int64_t rt0) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
+    const WaveCols<NT> wc(wv);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        if (!(j == 0 ? wc.has0 : wc.has1)) continue;
+        const int t = j == 0 ? wc.t0 : wc.t1;
+        float* col = act + t * 32 + l32 + 4 * h * S_;
+#pragma unroll
+        for (int rt = 0; rt < 4; ++rt) {
+            uint32_t bits = 0;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const float v = acc[rt][j][i];
+                col[(rt * 32 + (i & 3) + 8 * (i >> 2)) * S_] = v;
+                bits |= (v > 0.f ? 1u : 0u) << i;
+            }
+            if (mask) mask[mask_idx(rt0 + rt, NT, t, lane)] = (uint16_t)bits;
+        }
+    }
+}
+
+// 128 LDS rows -> global [M][hp] rows row0.., float4 per lane (1 KiB per wave instruction).
+template <int NT>
+NAV_DEV void copy_rows(const float* act, int S_, float* g, int64_t row0, int64_t M) {
+    constexpr int hp = NT * 32, Q4 = hp / 4;
+    for (int idx = threadIdx.x; idx < TM * Q4; idx += kBlock) {
+        const int r = idx / Q4, c4 = idx - r * Q4;
+        if (row0 + r < M)
+            *reinterpret_cast<float4*>(g + (row0 + r) * hp + 4 * c4) =
+                *reinterpret_cast<const float4*>(act + r * S_ + 4 * c4);
+    }
+}
 
 template <int NT, int IN_MODE, int OUT_MODE>
 __global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
@@ -158,21 +200,26 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, l32 = lane & 31;
     const MlpDev& net = a.net[blockIdx.y];
     float* act_save = a.acts[blockIdx.y];
+    uint16_t* masks = a.masks[blockIdx.y];
     const int64_t M = a.M;
-    const int64_t row0 = (int64_t)blockIdx.x * TM + wv * 32;
-    float* wbuf = smem + TM * SS;
-    float* xin = wbuf + 16 * hp + wv * 128;
-    float* my = smem + wv * 32 * SS;
+    const int64_t row0 = (int64_t)blockIdx.x * TM;
+    const int64_t rt0 = (int64_t)blockIdx.x * 4;
+    const int64_t n_rt = ((M + TM - 1) / TM) * 4;
+    float* act = smem;
+    float* xin = smem + TM * SS;  // [128][4]
     const int d_in = net.d_in, d_out = net.d_out, nh = net.n_hidden;
+    const WaveCols<NT> wc(wv);
 
-    // ---- input rows -> xin[32][4]
-    if (lane < 32) {
-        const int64_t r = row0 + lane;
+    // ---- input rows -> xin
+    if (tid < TM) {
+        const int64_t r = row0 + tid;
         float x[4] = {0.f, 0.f, 0.f, 0.f};
         if (r < M) {
             if (IN_MODE == IN_F32) {
                 const float* src = a.in + r * a.ld_in + a.in_col;
-                for (int k = 0; k < d_in; ++k) x[k] = src[k];
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (k < d_in) x[k] = src[k];
             } else {
                 // robot.py:556 baseline = state - goal, then torch.FloatTensor (f64 -> f32)
                 const double2 s = reinterpret_cast<const double2*>(a.state)[r];
@@ -181,62 +228,79 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
                 x[1] = (float)(s.y - g.y);
             }
         }
-        *reinterpret_cast<float4*>(xin + lane * 4) = make_float4(x[0], x[1], x[2], x[3]);
+        *reinterpret_cast<float4*>(xin + tid * 4) = make_float4(x[0], x[1], x[2], x[3]);
     }
     __syncthreads();
 
-    // ---- layer 0 (K = d_in) on the VALU
+    // ---- layer 0 (K = d_in) on the VALU, written in the C layout of the wave's column tiles
     {
         const float* W0 = net.params + net.w_off[0];
         const float* b0 = net.params + net.b_off[0];
-        for (int c = lane; c < hp; c += 64) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            if (!(j == 0 ? wc.has0 : wc.has1)) continue;
+            const int t = j == 0 ? wc.t0 : wc.t1;
+            const int c = t * 32 + l32;
             float w[4] = {0.f, 0.f, 0.f, 0.f};
-            for (int k = 0; k < d_in; ++k) w[k] = W0[c * d_in + k];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (k < d_in) w[k] = W0[c * d_in + k];
             const float b = b0[c];
-            for (int r = 0; r < 32; ++r) {
-                const float4 x = *reinterpret_cast<const float4*>(xin + r * 4);
-                float v = b;
-                v = fmaf(x.x, w[0], v);
-                if (d_in > 1) v = fmaf(x.y, w[1], v);
-                if (d_in > 2) v = fmaf(x.z, w[2], v);
-                if (d_in > 3) v = fmaf(x.w, w[3], v);
-                v = fmaxf(v, 0.f);
-                my[r * SS + c] = v;
-                if (act_save && row0 + r < M) act_save[(row0 + r) * hp + c] = v;
+            float* col = act + c + 4 * h * SS;
+            const float* xr = xin + 4 * h * 4;
+#pragma unroll 1
+            for (int rt = 0; rt < 4; ++rt) {
+                uint32_t bits = 0;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int ro = rt * 32 + (i & 3) + 8 * (i >> 2);
+                    const float4 x = *reinterpret_cast<const float4*>(xr + ro * 4);
+                    float v = b;
+                    v = fmaf(x.x, w[0], v);
+                    v = fmaf(x.y, w[1], v);
+                    v = fmaf(x.z, w[2], v);
+                    v = fmaf(x.w, w[3], v);
+                    v = fmaxf(v, 0.f);
+                    col[ro * SS] = v;
+                    bits |= (v > 0.f ? 1u : 0u) << i;
+                }
+                if (masks) masks[mask_idx(rt0 + rt, NT, t, lane)] = (uint16_t)bits;
             }
         }
     }
     __syncthreads();
+    if (act_save) copy_rows<NT>(act, SS, act_save, row0, M);
 
     // ---- hidden x hidden layers on MFMA
     for (int L = 1; L < nh; ++L) {
-        f32x16 acc[NT];
-        gemm_rows<NT>(my, SS, net.packed + (int64_t)(L - 1) * 2 * hp * hp, wbuf, acc);
+        f32x16 acc[4][2];
+        gemm_cols<NT>(act, SS, net.packed + (int64_t)(L - 1) * 2 * hp * hp, acc);
         const float* bL = net.params + net.b_off[L];
-        float* save = act_save ? act_save + (int64_t)L * M * hp : nullptr;
 #pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            const int c = 32 * t + l32;
-            const float b = bL[c];
+        for (int j = 0; j < 2; ++j) {
+            if (!(j == 0 ? wc.has0 : wc.has1)) continue;
+            const float b = bL[(j == 0 ? wc.t0 : wc.t1) * 32 + l32];
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int r = acc_row(i, h);
-                const float v = fmaxf(acc[t][i] + b, 0.f);
-                my[r * SS + c] = v;
-                if (save && row0 + r < M) save[(row0 + r) * hp + c] = v;
-            }
+            for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) acc[rt][j][i] = fmaxf(acc[rt][j][i] + b, 0.f);
         }
+        __syncthreads();  // every wave has finished reading the layer's input rows
+        store_layer<NT>(acc, act, SS, masks ? masks + (size_t)L * n_rt * NT * 64 : nullptr, rt0);
         __syncthreads();
+        if (act_save) copy_rows<NT>(act, SS, act_save + (int64_t)L * M * hp, row0, M);
     }
 
-    // ---- output layer (N = d_out <= 2) on the VALU: lane = (row l32, output h)
-    const int64_t r = row0 + l32;
-    const int j = h;
+    // ---- output layer (N = d_out <= 2) on the VALU: thread = (row, output)
+    const int rloc = tid & (TM - 1);
+    const int j = tid >> 7;
+    const int64_t r = row0 + rloc;
     float y = 0.f;
     if (j < d_out) {
         const float* Wo = net.params + net.w_off[nh] + j * hp;
-        const float* ar = my + l32 * SS;
+        const float* ar = act + rloc * SS;
         float acc0 = 0.f, acc1 = 0.f;
+#pragma unroll 4
         for (int k = 0; k < hp; k += 8) {
             const float4 x0 = *reinterpret_cast<const float4*>(ar + k);
             const float4 x1 = *reinterpret_cast<const float4*>(ar + k + 4);
@@ -292,10 +356,31 @@ struct BwdArgs {
     MlpDev net;
     int64_t M;
     const float* dy;
-    const float* acts;
+    const uint16_t* masks;
     float* dz;
     float* dx;
 };
+
+template <int NT>
+NAV_DEV void mask_and_store(f32x16 (&acc)[4][2], const uint16_t* mask, float* act, int S_,
+                            int64_t rt0) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
+    const WaveCols<NT> wc(wv);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        if (!(j == 0 ? wc.has0 : wc.has1)) continue;
+        const int t = j == 0 ? wc.t0 : wc.t1;
+        float* col = act + t * 32 + l32 + 4 * h * S_;
+#pragma unroll
+        for (int rt = 0; rt < 4; ++rt) {
+            const uint32_t bits = mask[mask_idx(rt0 + rt, NT, t, lane)];
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                col[(rt * 32 + (i & 3) + 8 * (i >> 2)) * S_] =
+                    (bits >> i) & 1u ? acc[rt][j][i] : 0.f;
+        }
+    }
+}
 
 template <int NT>
 __global__ __launch_bounds__(kBlock, 1) void k_mlp_bwd(BwdArgs a) {
@@ -304,82 +389,75 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_bwd(BwdArgs a) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, l32 = lane & 31;
     const MlpDev& net = a.net;
     const int64_t M = a.M;
-    const int64_t row0 = (int64_t)blockIdx.x * TM + wv * 32;
-    float* wbuf = smem + TM * SS;
-    float* xin = wbuf + 16 * hp + wv * 128;
-    float* my = smem + wv * 32 * SS;
+    const int64_t row0 = (int64_t)blockIdx.x * TM;
+    const int64_t rt0 = (int64_t)blockIdx.x * 4;
+    const int64_t n_rt = ((M + TM - 1) / TM) * 4;
+    float* act = smem;
+    float* dys = smem + TM * SS;
     const int d_in = net.d_in, d_out = net.d_out, nh = net.n_hidden;
     const int64_t MH = M * hp;
+    const WaveCols<NT> wc(wv);
+    const size_t mstride = (size_t)n_rt * NT * 64;
 
-    if (lane < 32) {
-        const int64_t r = row0 + lane;
-        float x[4] = {0.f, 0.f, 0.f, 0.f};
+    if (tid < TM) {
+        const int64_t r = row0 + tid;
+        float x[2] = {0.f, 0.f};
         if (r < M)
             for (int j = 0; j < d_out; ++j) x[j] = a.dy[r * d_out + j];
-        *reinterpret_cast<float4*>(xin + lane * 4) = make_float4(x[0], x[1], x[2], x[3]);
+        *reinterpret_cast<float4*>(dys + tid * 4) = make_float4(x[0], x[1], 0.f, 0.f);
     }
     __syncthreads();
 
-    // top hidden layer: dz = (dy . Wo) * (act > 0)
+    // top hidden layer: dz = (dy . Wo) * relu'(.), in the C layout
     {
         const float* Wo = net.params + net.w_off[nh];
-        const float* act = a.acts + (int64_t)(nh - 1) * MH;
-        float* dzo = a.dz + (int64_t)(nh - 1) * MH;
-        for (int c = lane; c < hp; c += 64) {
-            const float w0 = Wo[c], w1 = d_out > 1 ? Wo[hp + c] : 0.f;
-            for (int r = 0; r < 32; ++r) {
-                const float4 g = *reinterpret_cast<const float4*>(xin + r * 4);
-                float v = g.x * w0;
-                if (d_out > 1) v = fmaf(g.y, w1, v);
-                const int64_t gr = row0 + r;
-                if (gr < M) {
-                    if (!(act[gr * hp + c] > 0.f)) v = 0.f;
-                    dzo[gr * hp + c] = v;
-                } else {
-                    v = 0.f;
+        const uint16_t* mk = a.masks + (size_t)(nh - 1) * mstride;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            if (!(j == 0 ? wc.has0 : wc.has1)) continue;
+            const int t = j == 0 ? wc.t0 : wc.t1;
+            const int c = t * 32 + l32;
+            const float w0 = Wo[c];
+            const float w1 = d_out > 1 ? Wo[hp + c] : 0.f;
+            float* col = act + c + 4 * h * SS;
+            const float* gr = dys + 4 * h * 4;
+#pragma unroll 1
+            for (int rt = 0; rt < 4; ++rt) {
+                const uint32_t bits = mk[mask_idx(rt0 + rt, NT, t, lane)];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int ro = rt * 32 + (i & 3) + 8 * (i >> 2);
+                    const float4 g = *reinterpret_cast<const float4*>(gr + ro * 4);
+                    const float v = fmaf(g.y, w1, g.x * w0);
+                    col[ro * SS] = (bits >> i) & 1u ? v : 0.f;
                 }
-                my[r * SS + c] = v;
             }
         }
     }
     __syncthreads();
+    copy_rows<NT>(act, SS, a.dz + (int64_t)(nh - 1) * MH, row0, M);
 
-    // hidden layers, top-down: dz_{L-1} = (dz_L . W_L) * (act_{L-1} > 0), B = packed Wb_L
+    // hidden layers, top-down: dz_{L-1} = (dz_L . W_L) * relu'(act_{L-1}), B = packed Wb_L
     for (int L = nh - 1; L >= 1; --L) {
-        f32x16 acc[NT];
-        gemm_rows<NT>(my, SS, net.packed + (int64_t)(L - 1) * 2 * hp * hp + (int64_t)hp * hp,
-                      wbuf, acc);
-        const float* act = a.acts + (int64_t)(L - 1) * MH;
-        float* dzo = a.dz + (int64_t)(L - 1) * MH;
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            const int c = 32 * t + l32;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int r = acc_row(i, h);
-                const int64_t gr = row0 + r;
-                float v = acc[t][i];
-                if (gr < M) {
-                    if (!(act[gr * hp + c] > 0.f)) v = 0.f;
-                    dzo[gr * hp + c] = v;
-                } else {
-                    v = 0.f;
-                }
-                my[r * SS + c] = v;
-            }
-        }
+        f32x16 acc[4][2];
+        gemm_cols<NT>(act, SS, net.packed + (int64_t)(L - 1) * 2 * hp * hp + (int64_t)hp * hp,
+                      acc);
         __syncthreads();
+        mask_and_store<NT>(acc, a.masks + (size_t)(L - 1) * mstride, act, SS, rt0);
+        __syncthreads();
+        copy_rows<NT>(act, SS, a.dz + (int64_t)(L - 1) * MH, row0, M);
     }
 
-    // dx = dz_0 . W0 : lane = (row l32, inputs h and h+2)
+    // dx = dz_0 . W0 : thread = (row, input pair)
     if (a.dx) {
         const float* W0 = net.params + net.w_off[0];
-        const int64_t r = row0 + l32;
-        const float* zr = my + l32 * SS;
-        for (int j = h; j < d_in; j += 2) {
+        const int rloc = tid & (TM - 1);
+        const int64_t r = row0 + rloc;
+        const float* zr = act + rloc * SS;
+        for (int jj = tid >> 7; jj < d_in; jj += 2) {
             float acc = 0.f;
-            for (int c = 0; c < hp; ++c) acc = fmaf(zr[c], W0[c * d_in + j], acc);
-            if (r < M) a.dx[r * d_in + j] = acc;
+            for (int c = 0; c < hp; ++c) acc = fmaf(zr[c], W0[c * d_in + jj], acc);
+            if (r < M) a.dx[r * d_in + jj] = acc;
         }
     }
 }
@@ -395,49 +473,97 @@ struct WgradArgs {
     const float* dy;
     float* slabs;
     int splits;
+    int T;        // 64-wide tiles across hp
+    int n_hid;    // jobs of kind A = (nh - 1) * T * T
 };
 
 constexpr int WG_MC = 32;   // rows per staged chunk
 constexpr int WG_LD = 68;   // LDS row stride of the staged 64-column panels
 
-// dW_L[n][k] = sum_m dz_L[m][n] * act_{L-1}[m][k] for hidden x hidden layers; grid = (tiles of
-// 64x64, splits, layer-1). Each wave owns one 32x32 MFMA tile of the 64x64 workgroup tile.
-__global__ __launch_bounds__(kBlock) void k_wgrad_hidden(WgradArgs a) {
+// One launch computes every parameter gradient of a network for one row split (grid.y):
+//  kind A (hidden x hidden layer L, 64x64 tile): dW_L = dz_L^T act_{L-1} on MFMA, plus
+//          db_L = column sums of dz_L on the VALU in the tk == 0 tiles;
+//  kind B (layer 0, 64 columns of dz_0): dW_0 = dz_0^T x and db_0 on the VALU (K = d_in);
+//  kind C (output layer, 64 columns of act_top): dW_o = dy^T act_top and db_o on the VALU.
+// All kinds stage 32-row chunks of 64-column panels through LDS (double-buffered).
+__global__ __launch_bounds__(kBlock) void k_wgrad(WgradArgs a) {
     __shared__ __attribute__((aligned(16))) float pa[2][WG_MC][WG_LD];
     __shared__ __attribute__((aligned(16))) float pb[2][WG_MC][WG_LD];
+    __shared__ __attribute__((aligned(16))) float sm[2][WG_MC][4];
+    __shared__ float red[4][64][6];
     const MlpDev& net = a.net;
-    const int hp = net.hp;
-    const int tiles = (hp + 63) / 64;
-    const int tn = blockIdx.x / tiles, tk = blockIdx.x % tiles;
-    const int L = blockIdx.z + 1;
+    const int hp = net.hp, T = a.T, nh = net.n_hidden;
+    const int job = blockIdx.x;
+    int kind, L = 0, tn = 0, tk = 0;
+    if (job < a.n_hid) {
+        kind = 0;
+        L = job / (T * T) + 1;
+        tn = (job % (T * T)) / T;
+        tk = job % T;
+    } else if (job < a.n_hid + T) {
+        kind = 1;
+        tn = job - a.n_hid;
+    } else {
+        kind = 2;
+        tk = job - a.n_hid - T;
+    }
     const int64_t MH = a.M * hp;
-    const float* P = a.dz + (int64_t)L * MH;         // dz of layer L (its pre-activation)
-    const float* Q = a.acts + (int64_t)(L - 1) * MH;  // input of layer L
+    // P panel source (columns n0..n0+63) and Q panel source (columns k0..k0+63)
+    const float* P = nullptr;
+    const float* Q = nullptr;
+    const int n0 = tn * 64, k0 = tk * 64;
+    if (kind == 0) {
+        P = a.dz + (int64_t)L * MH;
+        Q = a.acts + (int64_t)(L - 1) * MH;
+    } else if (kind == 1) {
+        P = a.dz;
+    } else {
+        Q = a.acts + (int64_t)(nh - 1) * MH;
+    }
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, l32 = lane & 31;
     const int nloc = 32 * (wv >> 1), kloc = 32 * (wv & 1);
-    const int n0 = tn * 64, k0 = tk * 64;
     const int64_t per = (a.M + a.splits - 1) / a.splits;
     const int64_t m_lo = (int64_t)blockIdx.y * per;
     const int64_t m_hi = m_lo + per < a.M ? m_lo + per : a.M;
+    const int d_in = net.d_in, d_out = net.d_out;
+    const bool do_mfma = kind == 0 && (n0 + nloc) < hp && (k0 + kloc) < hp;
+    const bool do_colsum = kind == 1 || (kind == 0 && tk == 0);
     f32x16 acc;
     for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-    // staging: 32 rows x 64 cols per panel = 512 float4 per panel; thread -> 2 per panel
-    auto load = [&](int64_t m0, float4 (&ra)[2], float4 (&rb)[2]) {
+    // VALU accumulators: thread = (column c = tid & 63, row group g = tid >> 6: rows g, g+4, ..)
+    const int vc = tid & 63, vg = tid >> 6;
+    float va[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+
+    auto load = [&](int64_t m0, float4 (&ra)[2], float4 (&rb)[2], float4& rs) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const int i = tid + kBlock * j;
             const int rr = i >> 4, cc = (i & 15) * 4;
             const int64_t m = m0 + rr;
-            float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
             ra[j] = z;
             rb[j] = z;
             if (m < m_hi) {
-                if (n0 + cc < hp) ra[j] = *reinterpret_cast<const float4*>(P + m * hp + n0 + cc);
-                if (k0 + cc < hp) rb[j] = *reinterpret_cast<const float4*>(Q + m * hp + k0 + cc);
+                if (P && n0 + cc < hp) ra[j] = *reinterpret_cast<const float4*>(P + m * hp + n0 + cc);
+                if (Q && k0 + cc < hp) rb[j] = *reinterpret_cast<const float4*>(Q + m * hp + k0 + cc);
+            }
+        }
+        rs = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (tid < WG_MC && m0 + tid < m_hi) {
+            const int64_t m = m0 + tid;
+            if (kind == 1) {
+                const float* x = a.in + m * a.ld_in + a.in_col;
+                rs.x = x[0];
+                if (d_in > 1) rs.y = x[1];
+                if (d_in > 2) rs.z = x[2];
+                if (d_in > 3) rs.w = x[3];
+            } else if (kind == 2) {
+                rs.x = a.dy[m * d_out];
+                if (d_out > 1) rs.y = a.dy[m * d_out + 1];
             }
         }
     };
-    auto store = [&](int buf, float4 (&ra)[2], float4 (&rb)[2]) {
+    auto store = [&](int buf, float4 (&ra)[2], float4 (&rb)[2], float4 rs) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const int i = tid + kBlock * j;
@@ -445,76 +571,87 @@ __global__ __launch_bounds__(kBlock) void k_wgrad_hidden(WgradArgs a) {
             *reinterpret_cast<float4*>(&pa[buf][rr][cc]) = ra[j];
             *reinterpret_cast<float4*>(&pb[buf][rr][cc]) = rb[j];
         }
+        if (tid < WG_MC) *reinterpret_cast<float4*>(&sm[buf][tid][0]) = rs;
     };
-    float4 ra[2], rb[2];
+    float4 ra[2], rb[2], rs;
     const int nch = (int)((m_hi - m_lo + WG_MC - 1) / WG_MC);
     if (nch > 0) {
-        load(m_lo, ra, rb);
-        store(0, ra, rb);
+        load(m_lo, ra, rb, rs);
+        store(0, ra, rb, rs);
     }
     __syncthreads();
     for (int c = 0; c < nch; ++c) {
-        if (c + 1 < nch) load(m_lo + (int64_t)(c + 1) * WG_MC, ra, rb);
+        if (c + 1 < nch) load(m_lo + (int64_t)(c + 1) * WG_MC, ra, rb, rs);
         const int buf = c & 1;
+        if (do_mfma) {
 #pragma unroll
-        for (int s = 0; s < WG_MC / 2; ++s) {
-            const float av = pa[buf][2 * s + h][nloc + l32];
-            const float bv = pb[buf][2 * s + h][kloc + l32];
-            acc = mfma(av, bv, acc);
+            for (int s = 0; s < WG_MC / 2; ++s)
+                acc = mfma(pa[buf][2 * s + h][nloc + l32], pb[buf][2 * s + h][kloc + l32], acc);
         }
-        if (c + 1 < nch) store(buf ^ 1, ra, rb);
+        if (kind == 1) {
+#pragma unroll
+            for (int rr = vg; rr < WG_MC; rr += 4) {
+                const float g = pa[buf][rr][vc];
+                const float4 x = *reinterpret_cast<const float4*>(&sm[buf][rr][0]);
+                va[0] = fmaf(g, x.x, va[0]);
+                va[1] = fmaf(g, x.y, va[1]);
+                va[2] = fmaf(g, x.z, va[2]);
+                va[3] = fmaf(g, x.w, va[3]);
+                va[4] += g;
+            }
+        } else if (kind == 2) {
+#pragma unroll
+            for (int rr = vg; rr < WG_MC; rr += 4) {
+                const float x = pb[buf][rr][vc];
+                const float4 g = *reinterpret_cast<const float4*>(&sm[buf][rr][0]);
+                va[0] = fmaf(g.x, x, va[0]);
+                va[1] = fmaf(g.y, x, va[1]);
+                va[2] += g.x;
+                va[3] += g.y;
+            }
+        } else if (do_colsum) {
+#pragma unroll
+            for (int rr = vg; rr < WG_MC; rr += 4) va[4] += pa[buf][rr][vc];
+        }
+        if (c + 1 < nch) store(buf ^ 1, ra, rb, rs);
         __syncthreads();
     }
-    const int nb = n0 + nloc, kb = k0 + kloc;
-    if (nb >= hp || kb >= hp) return;
-    float* out = a.slabs + (int64_t)blockIdx.y * net.count + net.w_off[L];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) out[(int64_t)(nb + acc_row(i, h)) * hp + kb + l32] = acc[i];
-}
-
-// Thin reductions: every bias, layer-0 weights (K = d_in) and output weights (N = d_out).
-// grid = (n_hidden + 1 jobs, splits); thread = column.
-__global__ __launch_bounds__(kBlock) void k_wgrad_small(WgradArgs a) {
-    const MlpDev& net = a.net;
-    const int hp = net.hp, nh = net.n_hidden, job = blockIdx.x, c = threadIdx.x;
-    const int64_t per = (a.M + a.splits - 1) / a.splits;
-    const int64_t m_lo = (int64_t)blockIdx.y * per;
-    const int64_t m_hi = m_lo + per < a.M ? m_lo + per : a.M;
-    const int64_t MH = a.M * hp;
     float* out = a.slabs + (int64_t)blockIdx.y * net.count;
-    if (job < nh) {
-        if (c >= hp) return;
-        const float* P = a.dz + (int64_t)job * MH;
-        float sb = 0.f, sw[4] = {0.f, 0.f, 0.f, 0.f};
-        const int d_in = net.d_in;
-        for (int64_t m = m_lo; m < m_hi; ++m) {
-            const float g = P[m * hp + c];
-            sb += g;
-            if (job == 0) {
-                const float* x = a.in + m * a.ld_in + a.in_col;
-                for (int k = 0; k < d_in; ++k) sw[k] = fmaf(g, x[k], sw[k]);
+    if (do_mfma) {
+        const int nb = n0 + nloc, kb = k0 + kloc;
+        float* o = out + net.w_off[L];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[(int64_t)(nb + acc_row(i, h)) * hp + kb + l32] = acc[i];
+    }
+    if (kind == 0 && !do_colsum) return;
+    // reduce the 4 row groups of the VALU accumulators
+#pragma unroll
+    for (int q = 0; q < 6; ++q) red[vg][vc][q] = va[q];
+    __syncthreads();
+    if (tid < 64) {
+        float s[6];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) s[q] = red[0][tid][q] + red[1][tid][q] + red[2][tid][q] +
+                                           red[3][tid][q];
+        if (kind == 0) {
+            const int n = n0 + tid;
+            if (n < hp) out[net.b_off[L] + n] = s[4];
+        } else if (kind == 1) {
+            const int n = n0 + tid;
+            if (n < hp) {
+                for (int k = 0; k < d_in; ++k) out[net.w_off[0] + n * d_in + k] = s[k];
+                out[net.b_off[0] + n] = s[4];
             }
-        }
-        out[net.b_off[job] + c] = sb;
-        if (job == 0)
-            for (int k = 0; k < d_in; ++k) out[net.w_off[0] + c * d_in + k] = sw[k];
-    } else {
-        const int d_out = net.d_out;
-        if (c < hp) {
-            const float* A = a.acts + (int64_t)(nh - 1) * MH;
-            float s0 = 0.f, s1 = 0.f;
-            for (int64_t m = m_lo; m < m_hi; ++m) {
-                const float x = A[m * hp + c];
-                s0 = fmaf(a.dy[m * d_out], x, s0);
-                if (d_out > 1) s1 = fmaf(a.dy[m * d_out + 1], x, s1);
+        } else {
+            const int k = k0 + tid;
+            if (k < hp) {
+                out[net.w_off[nh] + k] = s[0];
+                if (d_out > 1) out[net.w_off[nh] + hp + k] = s[1];
             }
-            out[net.w_off[nh] + c] = s0;
-            if (d_out > 1) out[net.w_off[nh] + hp + c] = s1;
-        }
-        if (c < d_out) {
-            float s = 0.f;
-            for (int64_t m = m_lo; m < m_hi; ++m) s += a.dy[m * d_out + c];
-            out[net.b_off[nh] + c] = s;
+            if (tk == 0 && tid == 0) {
+                out[net.b_off[nh]] = s[2];
+                if (d_out > 1) out[net.b_off[nh] + 1] = s[3];
+            }
         }
     }
 }
@@ -793,7 +930,7 @@ int nav_mlp_forward(const nav_mlp* nets, int32_t n_nets, int64_t M, const float*
                     int32_t ld_in, int32_t in_col, float* const* out, int32_t ld_out,
                     int32_t out_col, int32_t out_mode, const float* eps, float policy_noise,
                     float noise_clip, float max_action, uint32_t seed_lo, uint32_t seed_hi,
-                    uint32_t counter, float* const* acts, void* stream) {
+                    uint32_t counter, float* const* acts, uint16_t* const* masks, void* stream) {
     FwdArgs a{};
     if (!nets || n_nets < 1 || n_nets > 2 || M < 0 || !out) return NAV_EINVAL;
     for (int i = 0; i < n_nets; ++i) {
@@ -801,6 +938,7 @@ int nav_mlp_forward(const nav_mlp* nets, int32_t n_nets, int64_t M, const float*
         if (a.net[i].hp != a.net[0].hp || a.net[i].d_in != a.net[0].d_in) return NAV_EINVAL;
         a.out[i] = out[i];
         a.acts[i] = acts ? acts[i] : nullptr;
+        a.masks[i] = masks ? masks[i] : nullptr;
     }
     if (M == 0) return 0;
     if (!in || in_col < 0 || in_col + a.net[0].d_in > ld_in || out_col < 0 ||
@@ -827,15 +965,21 @@ int nav_mlp_forward(const nav_mlp* nets, int32_t n_nets, int64_t M, const float*
     return NAV_EINVAL;
 }
 
-int nav_mlp_backward(const nav_mlp* net, int64_t M, const float* dy, const float* acts,
+int64_t nav_mlp_mask_count(int32_t hidden_pad, int32_t n_hidden, int64_t M) {
+    if (hidden_pad < 32 || hidden_pad > 256 || (hidden_pad & 31) || n_hidden < 1 || M < 0)
+        return NAV_EINVAL;
+    return (int64_t)n_hidden * ((M + TM - 1) / TM) * 4 * (hidden_pad / 32) * 64;
+}
+
+int nav_mlp_backward(const nav_mlp* net, int64_t M, const float* dy, const uint16_t* masks,
                      float* dz, float* dx, void* stream) {
     BwdArgs a{};
     if (!make_dev(net, &a.net) || M < 0) return NAV_EINVAL;
     if (M == 0) return 0;
-    if (!dy || !acts || !dz) return NAV_EINVAL;
+    if (!dy || !masks || !dz) return NAV_EINVAL;
     a.M = M;
     a.dy = dy;
-    a.acts = acts;
+    a.masks = masks;
     a.dz = dz;
     a.dx = dx;
     return launch_bwd(a, S(stream));
@@ -857,15 +1001,9 @@ int nav_mlp_wgrad(const nav_mlp* net, int64_t M, const float* in, int32_t ld_in,
     a.dy = dy;
     a.slabs = slabs;
     a.splits = splits;
-    const int hp = a.net.hp;
-    if (a.net.n_hidden > 1) {
-        const int tiles = (hp + 63) / 64;
-        hipLaunchKernelGGL(k_wgrad_hidden, dim3(tiles * tiles, splits, a.net.n_hidden - 1),
-                           dim3(kBlock), 0, S(stream), a);
-        NAV_CHECK_LAUNCH();
-    }
-    hipLaunchKernelGGL(k_wgrad_small, dim3(a.net.n_hidden + 1, splits), dim3(kBlock), 0,
-                       S(stream), a);
+    a.T = (a.net.hp + 63) / 64;
+    a.n_hid = (a.net.n_hidden - 1) * a.T * a.T;
+    hipLaunchKernelGGL(k_wgrad, dim3(a.n_hid + 2 * a.T, splits), dim3(kBlock), 0, S(stream), a);
     NAV_CHECK_LAUNCH();
     return 0;
 }

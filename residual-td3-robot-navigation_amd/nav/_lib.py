@@ -75,7 +75,8 @@ SIGNATURES = [
     ("nav_mlp_forward", C.c_int, [_P(NavMlp), C.c_int32, C.c_int64, _vp, C.c_int32, C.c_int32,
                                   _P(_vp), C.c_int32, C.c_int32, C.c_int32, _vp, C.c_float,
                                   C.c_float, C.c_float, C.c_uint32, C.c_uint32, C.c_uint32,
-                                  _P(_vp), _vp]),
+                                  _P(_vp), _P(_vp), _vp]),
+    ("nav_mlp_mask_count", C.c_int64, [C.c_int32, C.c_int32, C.c_int64]),
     ("nav_mlp_backward", C.c_int, [_P(NavMlp), C.c_int64, _vp, _vp, _vp, _vp, _vp]),
     ("nav_mlp_wgrad", C.c_int, [_P(NavMlp), C.c_int64, _vp, C.c_int32, C.c_int32, _vp, _vp, _vp,
                                 _vp, C.c_int32, _vp]),
@@ -95,7 +96,7 @@ SIGNATURES = [
 ]
 
 # Entry points that return int64 counts (negative = error) rather than a status code.
-_COUNT_FNS = {"nav_mlp_param_count", "nav_mlp_packed_count"}
+_COUNT_FNS = {"nav_mlp_param_count", "nav_mlp_packed_count", "nav_mlp_mask_count"}
 
 
 class NavError(RuntimeError):

@@ -51,6 +51,11 @@ class DeviceMLP:
                    self.params.data_ptr(), self.packed.data_ptr())
         return d
 
+    def mask_buffer(self, M):
+        """ReLU-derivative bit image for M rows (nav_mlp_mask_count u16 words)."""
+        n = lib().nav_mlp_mask_count(self.hp, self.n_hidden, M)
+        return torch.zeros(n, dtype=torch.int16, device=self.device)
+
     def sizes(self):
         return [self.d_in] + [self.hidden] * self.n_hidden + [self.d_out]
 
@@ -115,7 +120,7 @@ class DeviceMLP:
 
 def forward(nets, inp, ld_in, in_col, outs, ld_out, out_col, M, out_mode=0, eps=None,
             policy_noise=0.2, noise_clip=0.5, max_action=5.0, seed=(0, 0), counter=0, acts=None,
-            stream=None):
+            masks=None, stream=None):
     """nav_mlp_forward for 1 or 2 networks sharing `inp`."""
     from ._lib import stream_handle
     n = len(nets)
@@ -124,9 +129,13 @@ def forward(nets, inp, ld_in, in_col, outs, ld_out, out_col, M, out_mode=0, eps=
     acts_arr = None
     if acts is not None:
         acts_arr = (C.c_void_p * n)(*[(a.data_ptr() if a is not None else None) for a in acts])
+    masks_arr = None
+    if masks is not None:
+        masks_arr = (C.c_void_p * n)(*[(m.data_ptr() if m is not None else None) for m in masks])
     net = nets[0]
     flops = n * prof.mlp_fwd_flops(net.d_in, net.d_out, net.hidden, net.n_hidden, M)
     with prof.region("mlp_fwd", flops):
         lib().nav_mlp_forward(descs, n, M, ptr(inp), ld_in, in_col, out_arr, ld_out, out_col,
                               out_mode, ptr(eps), policy_noise, noise_clip, max_action,
-                              seed[0], seed[1], counter, acts_arr, stream_handle(stream))
+                              seed[0], seed[1], counter, acts_arr, masks_arr,
+                              stream_handle(stream))

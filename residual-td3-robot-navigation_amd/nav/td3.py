@@ -81,6 +81,9 @@ class TD3:
         self.acts1, self.acts2 = f(nh, B, hp), f(nh, B, hp)
         self.dz1, self.dz2 = f(nh, B, hp), f(nh, B, hp)
         self.acts_a, self.dz_a = f(nh, B, hp), f(nh, B, hp)
+        self.mask1 = self.critic_network_1.mask_buffer(B)
+        self.mask2 = self.critic_network_1.mask_buffer(B)
+        self.mask_a = self.actor_network.mask_buffer(B)
         self.dx = f(B, 4)
         self.da = f(B, 2)
         self.loss_part = f((B + 255) // 256, 2)
@@ -102,11 +105,11 @@ class TD3:
         if self.grad_hook is not None:
             self.grad_hook(grad)
 
-    def _bwd(self, net, M, dy, acts, dz, dx, s):
+    def _bwd(self, net, M, dy, masks, dz, dx, s):
         with prof.region("mlp_bwd", prof.mlp_bwd_flops(net.d_in, net.d_out, net.hidden,
                                                          net.n_hidden, M, dx is not None)):
-            lib().nav_mlp_backward(C.byref(net.desc()), M, ptr(dy), ptr(acts), ptr(dz), ptr(dx),
-                                   s)
+            lib().nav_mlp_backward(C.byref(net.desc()), M, ptr(dy), ptr(masks), ptr(dz),
+                                   ptr(dx), s)
 
     def _sample(self, replay, B, out, idx=None, stream=None):
         """ReplayBuffer.sample (robot.py:98-115) into a [B][8] batch."""
@@ -134,16 +137,17 @@ class TD3:
                 [self.q1t, self.q2t], 1, 0, B, stream=stream)
         lib().nav_batch_sa(B, ptr(bt), ptr(self.sa), s)
         forward([self.critic_network_1, self.critic_network_2], self.sa, 4, 0,
-                [self.q1, self.q2], 1, 0, B, acts=[self.acts1, self.acts2], stream=stream)
+                [self.q1, self.q2], 1, 0, B, acts=[self.acts1, self.acts2],
+                masks=[self.mask1, self.mask2], stream=stream)
         lib().nav_td3_critic_loss(B, ptr(bt), ptr(self.q1t), ptr(self.q2t), ptr(self.q1),
                                   ptr(self.q2), c.gamma, ptr(self.dq1), ptr(self.dq2),
                                   ptr(self.y), ptr(self.loss_part), s)
-        for net, opt, acts, dz, dq, grad in (
-                (self.critic_network_1, self.critic_optimizer_1, self.acts1, self.dz1, self.dq1,
-                 self.grad_c1),
-                (self.critic_network_2, self.critic_optimizer_2, self.acts2, self.dz2, self.dq2,
-                 self.grad_c2)):
-            self._bwd(net, B, dq, acts, dz, None, s)
+        for net, opt, acts, mask, dz, dq, grad in (
+                (self.critic_network_1, self.critic_optimizer_1, self.acts1, self.mask1, self.dz1,
+                 self.dq1, self.grad_c1),
+                (self.critic_network_2, self.critic_optimizer_2, self.acts2, self.mask2, self.dz2,
+                 self.dq2, self.grad_c2)):
+            self._bwd(net, B, dq, mask, dz, None, s)
             self._grads(net, B, self.sa, 4, 0, acts, dz, dq, grad, s)
             opt.step(grad, stream)
 
@@ -162,15 +166,15 @@ class TD3:
         bt = self.batch2
         lib().nav_strided_copy(ptr(bt), 8, 0, ptr(self.sa), 4, 0, B, 2, s)
         forward([self.actor_network], bt, 8, 0, [self.sa], 4, 2, B, acts=[self.acts_a],
-                stream=stream)
-        forward([self.critic_network_1], self.sa, 4, 0, [self.q1], 1, 0, B, acts=[self.acts1],
+                masks=[self.mask_a], stream=stream)
+        forward([self.critic_network_1], self.sa, 4, 0, [self.q1], 1, 0, B, masks=[self.mask1],
                 stream=stream)
         # d(-mean Q)/dQ = -1/B; backprop through critic 1 to its action input
         lib().nav_fill(ptr(self.dq1), B, -1.0 / B, s)
-        self._bwd(self.critic_network_1, B, self.dq1, self.acts1, self.dz1, self.dx, s)
+        self._bwd(self.critic_network_1, B, self.dq1, self.mask1, self.dz1, self.dx, s)
         lib().nav_strided_copy(ptr(self.dx), 4, 2, ptr(self.da), 2, 0, B, 2, s)
         net = self.actor_network
-        self._bwd(net, B, self.da, self.acts_a, self.dz_a, None, s)
+        self._bwd(net, B, self.da, self.mask_a, self.dz_a, None, s)
         self._grads(net, B, bt, 8, 0, self.acts_a, self.dz_a, self.da, self.grad_a, s)
         self.actor_optimizer.step(self.grad_a, stream)
 

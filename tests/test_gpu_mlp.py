@@ -128,13 +128,14 @@ def test_backward_and_weight_grads_vs_autograd(nav, d_in, d_out, hidden, nh, M):
     dy = torch.randn(M, d_out) / M
     out = torch.zeros(M, d_out, device=DEV)
     acts = torch.zeros(nh, M, net.hp, device=DEV)
+    masks = net.mask_buffer(M)
     xd = x.to(DEV)
-    forward([net], xd, d_in, 0, [out], d_out, 0, M, acts=[acts])
+    forward([net], xd, d_in, 0, [out], d_out, 0, M, acts=[acts], masks=[masks])
     dz = torch.zeros(nh, M, net.hp, device=DEV)
     dx = torch.zeros(M, d_in, device=DEV)
     s = stream_handle()
     dyd = dy.to(DEV)
-    lib().nav_mlp_backward(C.byref(net.desc()), M, ptr(dyd), ptr(acts), ptr(dz), ptr(dx), s)
+    lib().nav_mlp_backward(C.byref(net.desc()), M, ptr(dyd), ptr(masks), ptr(dz), ptr(dx), s)
     splits = 7
     slabs = torch.zeros(splits, net.count, device=DEV)
     grad = torch.zeros(net.count, device=DEV)

@@ -20,7 +20,12 @@ for step in "$@"; do
     smoke) run smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 900 python bench.py ;;
     benchq) run bench 600 python bench.py --steps 10 --warmup 3 --cpu-budget 8 ;;
-    prof) run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-sweep ;;
+    micro) run micro 600 python tools/microbench.py ;;
+    prof) run prof 900 rocprofv3 --kernel-trace --stats -T -f csv -d gpurun_out/prof -o run -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-sweep ;;
+    pmc) run pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE -T -f csv -d gpurun_out/pmc_fetch -o run -- python bench.py --steps 4 --warmup 2 --no-cpu-baseline --no-sweep &&
+         run pmc_write 900 rocprofv3 --pmc WRITE_SIZE -T -f csv -d gpurun_out/pmc_write -o run -- python bench.py --steps 4 --warmup 2 --no-cpu-baseline --no-sweep &&
+         run pmc_step_fetch 600 rocprofv3 --pmc FETCH_SIZE -T -f csv -d gpurun_out/pmc_step_fetch -o run -- python bench.py --sweep-only 16777216 &&
+         run pmc_step_write 600 rocprofv3 --pmc WRITE_SIZE -T -f csv -d gpurun_out/pmc_step_write -o run -- python bench.py --sweep-only 16777216 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
