@@ -140,6 +140,16 @@ int nav_dynamics(const float* field, const double* state, const double* action, 
 int nav_agent_step(const nav_params* p, const nav_env_soa* env, const float* field,
                    const double* action, const nav_replay* replay,
                    int64_t replay_base, const nav_step_out* out, void* stream);
+/* Robot.process_transition (robot.py:645-675) without the environment step, for callers that
+ * step the Environment themselves (the N = 1 drop-in): reward w/o demo term, check_if_stuck,
+ * done, replay push; meta/hist updated, plan_index/path_length read (not advanced). */
+int nav_transition(const nav_params* p, const nav_env_soa* env, const double* state,
+                   const double* action, const double* next_state, const nav_replay* replay,
+                   int64_t replay_base, const nav_step_out* out, void* stream);
+/* Robot.check_if_stuck (robot.py:509-538) alone: updates the history ring (hist, meta bits
+ * 8-14) with `state` [n][2] and writes stuck [n] (0/1). */
+int nav_check_if_stuck(const nav_params* p, const nav_env_soa* env, const double* state,
+                       uint8_t* stuck, void* stream);
 /* robot.py:741-762 demo-proximity term for envs flagged by nav_agent_step:
  * r = (goal_term + demo_factor * -min_j ||s' - d_j||) - stuck_penalty*stuck, written to the
  * replay row. demo_xy [m][2] f64 per group: group g = env / envs_per_group uses
@@ -149,11 +159,26 @@ int nav_demo_reward(const nav_params* p, int64_t n, const double* next_state,
                     const int64_t* demo_off, int64_t m, int32_t envs_per_group,
                     const nav_replay* replay, int64_t replay_base, double* reward_out,
                     void* stream);
+/* robot.py:753 min_j ||p_i - d_j|| (scipy cdist euclidean, f64) for n points [n][2]. */
+int nav_demo_min(const double* points, int64_t n, const double* demo_xy, int64_t m,
+                 double* out, void* stream);
 /* Pure robot.py:727-762 compute_reward for n next-states, f64 out; goal_hit (nullable) [n]
  * receives the goal_reached side effect (robot.py:745). */
 int nav_compute_reward(const nav_params* p, int64_t n, const double* next_state,
                        const double* goal, const double* demo_xy, int64_t m, int32_t demo_flag,
                        double* reward, uint8_t* goal_hit, void* stream);
+
+/* Batched open-loop rollouts of Environment.dynamics (the CEM demonstrator's inner loop,
+ * environment.py:230-244): P paths x T steps; start [P][2], actions [P][T][2] f64 ->
+ * paths [P][T+1][2] f64; reward (nullable) [P] = -||f32(s_T) - goal|| (environment.py:261-262). */
+int nav_rollout(const float* field, int64_t P, int32_t T, const double* start,
+                const double* actions, double* paths, const double* goal, double* reward,
+                void* stream);
+/* ReplayBuffer.push (robot.py:79-96) of n transitions (f64 in, float32 rows), slots
+ * (base + i) % capacity. */
+int nav_replay_push(const nav_replay* replay, int64_t base, int64_t n, const double* state,
+                    const double* action, const double* reward, const double* next_state,
+                    const uint8_t* done, void* stream);
 
 /* ---- Actor / critic MLPs on MFMA (robot.py:128-206) ---- */
 /* Action selection, fused: residual = actor(f32(state - goal)) (robot.py:598-624) and the

@@ -99,6 +99,126 @@ __global__ __launch_bounds__(kBlock) void k_dynamics(int64_t n, const float2* __
     out[e] = dynamics(field, s[e], a[e]);
 }
 
+// Robot.process_transition (robot.py:645-675) for env e given (s, a, s'): reward without the
+// demo term (robot.py:727-762; the term is added by nav_demo_reward for flagged envs),
+// check_if_stuck on the pre-step state (robot.py:509-538, ring of 5 in hist [5][n]), done, and
+// ReplayBuffer.push (robot.py:79-96) as one 32-B row. Returns the updated meta word.
+struct TransOut {
+    double r, gt;
+    bool goal_hit, demo_term, stuck, done;
+    uint32_t meta;
+};
+
+NAV_DEV TransOut transition(const nav_params& p, const nav_env_soa& env, int64_t e, double2 s,
+                            double2 a, double2 ns, uint32_t meta, int32_t plan, int32_t path,
+                            float4* __restrict__ rows, int64_t slot) {
+    double2* hist = reinterpret_cast<double2*>(env.hist);
+    const double2 g = reinterpret_cast<const double2*>(env.goal)[e];
+    TransOut t;
+    bool goal_reached = (meta & M_GOAL) != 0;
+    t.gt = -norm2(ns.x - g.x, ns.y - g.y);
+    t.goal_hit = t.gt >= -p.goal_threshold;
+    t.demo_term = false;
+    if (t.goal_hit) {
+        goal_reached = true;
+        t.r = p.goal_reward;
+    } else {
+        t.r = t.gt;
+        t.demo_term = (meta & M_DEMO) != 0;
+    }
+    int cnt = (int)((meta >> 8) & 7u), head = (int)((meta >> 12) & 7u);
+    t.stuck = false;
+    if (cnt >= NAV_HIST) {
+        bool all = true;
+#pragma unroll
+        for (int k = 0; k < NAV_HIST; ++k) {
+            const double2 h = hist[(int64_t)k * env.n + e];
+            const double d = norm2(s.x - h.x, s.y - h.y);
+            all = all && (d < p.stuck_threshold);
+        }
+        if (all) {
+            t.stuck = true;
+            cnt = 0;
+        } else {
+            head = head == NAV_HIST - 1 ? 0 : head + 1;
+            cnt -= 1;
+        }
+    }
+    {
+        int sl = head + cnt;
+        if (sl >= NAV_HIST) sl -= NAV_HIST;
+        hist[(int64_t)sl * env.n + e] = s;
+        cnt += 1;
+    }
+    bool stuck_flag = (meta & M_STUCK) != 0;
+    if (t.stuck) {
+        stuck_flag = true;
+        if (!t.demo_term) t.r -= p.stuck_penalty;
+    }
+    t.done = plan == path - 1;  // robot.py:672
+    rows[2 * slot] = make_float4((float)s.x, (float)s.y, (float)a.x, (float)a.y);
+    rows[2 * slot + 1] = make_float4((float)t.r, (float)ns.x, (float)ns.y, t.done ? 1.f : 0.f);
+    t.meta = (goal_reached ? M_GOAL : 0u) | (stuck_flag ? M_STUCK : 0u) | (meta & M_DEMO) |
+             ((uint32_t)cnt << 8) | ((uint32_t)head << 12);
+    return t;
+}
+
+NAV_DEV uint8_t flag_byte(const TransOut& t, bool ended) {
+    return (uint8_t)((t.done ? F_DONE : 0) | (t.goal_hit ? F_GOAL : 0) | (t.stuck ? F_STUCK : 0) |
+                     (ended ? F_ENDED : 0) | (t.demo_term ? F_DEMO : 0));
+}
+
+// Robot.check_if_stuck alone (robot.py:509-538): history ring update + stuck verdict.
+__global__ __launch_bounds__(kBlock) void k_check_if_stuck(nav_params p, nav_env_soa env,
+                                                           const double2* __restrict__ st,
+                                                           uint8_t* __restrict__ stuck_out) {
+    const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (e >= env.n) return;
+    double2* hist = reinterpret_cast<double2*>(env.hist);
+    const double2 s = st[e];
+    const uint32_t meta = env.meta[e];
+    int cnt = (int)((meta >> 8) & 7u), head = (int)((meta >> 12) & 7u);
+    bool stuck = false;
+    if (cnt >= NAV_HIST) {
+        bool all = true;
+        for (int k = 0; k < NAV_HIST; ++k) {
+            const double2 h = hist[(int64_t)k * env.n + e];
+            all = all && (norm2(s.x - h.x, s.y - h.y) < p.stuck_threshold);
+        }
+        if (all) {
+            stuck = true;
+            cnt = 0;
+        } else {
+            head = head == NAV_HIST - 1 ? 0 : head + 1;
+            cnt -= 1;
+        }
+    }
+    int sl = head + cnt;
+    if (sl >= NAV_HIST) sl -= NAV_HIST;
+    hist[(int64_t)sl * env.n + e] = s;
+    cnt += 1;
+    env.meta[e] = (meta & 0xffu) | ((uint32_t)cnt << 8) | ((uint32_t)head << 12);
+    stuck_out[e] = stuck ? 1 : 0;
+}
+
+// Robot.process_transition alone (the N = 1 drop-in's path): s, a, s' given by the caller.
+__global__ __launch_bounds__(kBlock) void k_transition(nav_params p, nav_env_soa env,
+                                                       const double2* __restrict__ st,
+                                                       const double2* __restrict__ act,
+                                                       const double2* __restrict__ nst,
+                                                       float4* __restrict__ rows, int64_t cap,
+                                                       int64_t base, nav_step_out out) {
+    const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (e >= env.n) return;
+    const uint32_t meta = env.meta[e];
+    const TransOut t = transition(p, env, e, st[e], act[e], nst[e], meta, env.plan_index[e],
+                                  env.path_length[e], rows, (base + e) % cap);
+    env.meta[e] = t.meta;
+    if (out.next_state) reinterpret_cast<double2*>(out.next_state)[e] = nst[e];
+    if (out.goal_term) out.goal_term[e] = t.gt;
+    if (out.flags) out.flags[e] = flag_byte(t, false);
+}
+
 // One training tick per env (see navenv.h nav_agent_step).
 __global__ __launch_bounds__(kBlock) void k_agent_step(nav_params p, nav_env_soa env,
                                                        const float2* __restrict__ field,
@@ -109,79 +229,26 @@ __global__ __launch_bounds__(kBlock) void k_agent_step(nav_params p, nav_env_soa
     float st_r = 0.f, st_done = 0.f, st_goal = 0.f, st_stuck = 0.f, st_end = 0.f;
     if (e < env.n) {
         double2* state = reinterpret_cast<double2*>(env.state);
-        double2* hist = reinterpret_cast<double2*>(env.hist);
         const double2 s = state[e];
         const double2 a = action[e];
-        const double2 g = reinterpret_cast<const double2*>(env.goal)[e];
-        uint32_t meta = env.meta[e];
+        const uint32_t meta = env.meta[e];
         int32_t plan = env.plan_index[e];
         const int32_t path = env.path_length[e];
 
         // environment.py:201-206
         double2 ns = dynamics(field, s, a);
         if (!in_world(ns)) ns = s;
-
-        // robot.py:727-762 (demo term added by nav_demo_reward when flagged)
-        bool goal_reached = (meta & M_GOAL) != 0;
-        const double gt = -norm2(ns.x - g.x, ns.y - g.y);
-        double r;
-        bool demo_term = false;
-        if (gt >= -p.goal_threshold) {
-            goal_reached = true;
-            r = p.goal_reward;
-        } else {
-            r = gt;
-            demo_term = (meta & M_DEMO) != 0;
-        }
-
-        // robot.py:509-538 check_if_stuck on the pre-step state; ring of 5 in hist [5][n]
-        int cnt = (int)((meta >> 8) & 7u), head = (int)((meta >> 12) & 7u);
-        bool stuck = false;
-        if (cnt >= NAV_HIST) {
-            bool all = true;
-#pragma unroll
-            for (int k = 0; k < NAV_HIST; ++k) {
-                const double2 h = hist[(int64_t)k * env.n + e];
-                const double d = norm2(s.x - h.x, s.y - h.y);
-                all = all && (d < p.stuck_threshold);
-            }
-            if (all) {
-                stuck = true;
-                cnt = 0;
-            } else {
-                head = head == NAV_HIST - 1 ? 0 : head + 1;
-                cnt -= 1;
-            }
-        }
-        {
-            int slot = head + cnt;
-            if (slot >= NAV_HIST) slot -= NAV_HIST;
-            hist[(int64_t)slot * env.n + e] = s;
-            cnt += 1;
-        }
-        bool stuck_flag = (meta & M_STUCK) != 0;
-        if (stuck) {
-            stuck_flag = true;
-            if (!demo_term) r -= p.stuck_penalty;
-        }
-        const bool done = plan == path - 1;  // robot.py:672
-
-        // ReplayBuffer.push (robot.py:79-96) as one 32-B row
-        const int64_t slot = (base + e) % cap;
-        rows[2 * slot] = make_float4((float)s.x, (float)s.y, (float)a.x, (float)a.y);
-        rows[2 * slot + 1] = make_float4((float)r, (float)ns.x, (float)ns.y, done ? 1.f : 0.f);
+        TransOut t = transition(p, env, e, s, a, ns, meta, plan, path, rows, (base + e) % cap);
 
         // next tick: robot.py:479-487 end check -> Robot.reset (492-506) + Environment.reset
-        const bool ended = done || goal_reached || stuck_flag;
-        const uint32_t dflag = meta & M_DEMO;
+        const bool ended = t.done || (t.meta & (M_GOAL | M_STUCK));
         if (ended) {
             const int32_t ep = env.episodes[e] + 1;
             env.episodes[e] = ep;
             env.path_length[e] = path + p.path_increase;
             env.noise_scale[e] = env.noise_scale[e] * p.noise_decay;
             plan = 1;  // Robot.reset sets 0, the next tick's increment makes it 1
-            goal_reached = false;
-            stuck_flag = false;
+            t.meta &= ~(M_GOAL | M_STUCK);
             const uint4 w = philox(0u, (uint32_t)e, NAV_TAG_RESET, (uint32_t)ep, p.seed_lo,
                                    p.seed_hi);
             const double4 rg = reinterpret_cast<const double4*>(env.region)[e];
@@ -192,18 +259,14 @@ __global__ __launch_bounds__(kBlock) void k_agent_step(nav_params p, nav_env_soa
             state[e] = ns;
         }
         env.plan_index[e] = plan;
-        env.meta[e] = (goal_reached ? M_GOAL : 0u) | (stuck_flag ? M_STUCK : 0u) | dflag |
-                      ((uint32_t)cnt << 8) | ((uint32_t)head << 12);
+        env.meta[e] = t.meta;
         if (out.next_state) reinterpret_cast<double2*>(out.next_state)[e] = ns;
-        if (out.goal_term) out.goal_term[e] = gt;
-        if (out.flags)
-            out.flags[e] = (uint8_t)((done ? F_DONE : 0) | (gt >= -p.goal_threshold ? F_GOAL : 0) |
-                                     (stuck ? F_STUCK : 0) | (ended ? F_ENDED : 0) |
-                                     (demo_term ? F_DEMO : 0));
-        st_r = (float)r;
-        st_done = done ? 1.f : 0.f;
-        st_goal = gt >= -p.goal_threshold ? 1.f : 0.f;
-        st_stuck = stuck ? 1.f : 0.f;
+        if (out.goal_term) out.goal_term[e] = t.gt;
+        if (out.flags) out.flags[e] = flag_byte(t, ended);
+        st_r = (float)t.r;
+        st_done = t.done ? 1.f : 0.f;
+        st_goal = t.goal_hit ? 1.f : 0.f;
+        st_stuck = t.stuck ? 1.f : 0.f;
         st_end = ended ? 1.f : 0.f;
     }
     if (out.block_stats) {
@@ -226,9 +289,16 @@ __global__ __launch_bounds__(kBlock) void k_agent_step(nav_params p, nav_env_soa
     }
 }
 
-// robot.py:753 demo-proximity min distance; points staged through LDS in chunks and read by
-// broadcast (every lane of the block reads the same point). f64 math as scipy's cdist.
-constexpr int kDemoChunk = 2048;
+// robot.py:753 demo-proximity min distance, f64 exactly as scipy's cdist (dx*dx + dy*dy, no
+// fma; sqrt is monotone and correctly rounded, so sqrt(min) == min(sqrt)). One wave = 64 envs of
+// one group; every lane tests the same point at the same time, so the points are read with
+// wave-uniform (scalar-unit) loads straight into SGPRs — no LDS staging, no bank traffic — and
+// four independent min chains keep the f64 pipe busy. A workgroup = kDemoSplit waves over the
+// SAME 64 envs, each scanning 1/kDemoSplit of the points (4 waves per SIMD hide the scalar-cache
+// latency), combined through LDS.
+constexpr int kDemoEnvs = 64;
+constexpr int kDemoSplit = 8;
+constexpr int kDemoBlock = kDemoEnvs * kDemoSplit;
 
 NAV_DEV double demo_min_global(const double2* __restrict__ d, int64_t m, double x, double y) {
     double best = __builtin_inf();
@@ -241,66 +311,72 @@ NAV_DEV double demo_min_global(const double2* __restrict__ d, int64_t m, double 
     return best;
 }
 
-__global__ __launch_bounds__(kBlock) void k_demo_reward(nav_params p, int64_t n,
-                                                        const double2* __restrict__ ns,
-                                                        const double* __restrict__ gterm,
-                                                        const uint8_t* __restrict__ flags,
-                                                        const double2* __restrict__ demo,
-                                                        const int64_t* __restrict__ off,
-                                                        int64_t m_shared, int32_t epg,
-                                                        float* __restrict__ rows, int64_t cap,
-                                                        int64_t base, double* reward_out) {
-    __shared__ double2 pts[kDemoChunk];
-    const int64_t e0 = (int64_t)blockIdx.x * kBlock;
-    const int64_t e = e0 + threadIdx.x;
+NAV_DEV double sqd(double x, double y, double px, double py) {
+    const double dx = x - px, dy = y - py;
+    return dx * dx + dy * dy;
+}
+
+NAV_DEV double demo_min_uniform(const double* __restrict__ d, int m, double x, double y) {
+    double b0 = __builtin_inf(), b1 = b0, b2 = b0, b3 = b0;
+    int j = 0;
+    for (; j + 4 <= m; j += 4) {
+        const double* q = d + 2 * j;
+        const double v0 = sqd(x, y, q[0], q[1]), v1 = sqd(x, y, q[2], q[3]);
+        const double v2 = sqd(x, y, q[4], q[5]), v3 = sqd(x, y, q[6], q[7]);
+        // fmin == (v < b ? v : b) here: no NaN among the distances
+        b0 = fmin(v0, b0);
+        b1 = fmin(v1, b1);
+        b2 = fmin(v2, b2);
+        b3 = fmin(v3, b3);
+    }
+    for (; j < m; ++j) b0 = fmin(sqd(x, y, d[2 * j], d[2 * j + 1]), b0);
+    return fmin(fmin(b0, b1), fmin(b2, b3));
+}
+
+__global__ __launch_bounds__(kDemoBlock) void k_demo_reward(nav_params p, int64_t n,
+                                                            const double2* __restrict__ ns,
+                                                            const double* __restrict__ gterm,
+                                                            const uint8_t* __restrict__ flags,
+                                                            const double* __restrict__ demo,
+                                                            const int64_t* __restrict__ off,
+                                                            int64_t m_shared, int32_t epg,
+                                                            float* __restrict__ rows,
+                                                            int64_t cap, int64_t base,
+                                                            double* __restrict__ reward_out) {
+    __shared__ double part[kDemoSplit][kDemoEnvs];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t e0 = (int64_t)blockIdx.x * kDemoEnvs;
+    const int64_t e = e0 + lane;
     const bool live = e < n;
     const uint8_t f = live ? flags[e] : 0;
     const bool want = live && (f & F_DEMO);
+    if (!__syncthreads_or(want ? 1 : 0)) return;
     double x = 0.0, y = 0.0;
     if (live) {
         const double2 s = ns[e];
-        x = s.x; y = s.y;
+        x = s.x;
+        y = s.y;
     }
-    // group range of this env, and whether the whole block shares it
-    const int64_t last = (e0 + kBlock - 1 < n ? e0 + kBlock - 1 : n - 1);
+    const int64_t last = e0 + kDemoEnvs - 1 < n ? e0 + kDemoEnvs - 1 : n - 1;
     const int64_t g0 = off ? e0 / epg : 0, g1 = off ? last / epg : 0;
-    double best = __builtin_inf();
-    if (g0 == g1) {
+    double best;
+    if (g0 == g1) {  // the 64 envs share one group: wave-uniform scalar loads
         const int64_t lo = off ? off[g0] : 0, hi = off ? off[g0 + 1] : m_shared;
-        const int any = __syncthreads_or(want ? 1 : 0);
-        if (any) {
-            for (int64_t c = lo; c < hi; c += kDemoChunk) {
-                const int cn = (int)(hi - c < kDemoChunk ? hi - c : kDemoChunk);
-                __syncthreads();
-                for (int i = threadIdx.x; i < cn; i += kBlock) pts[i] = demo[c + i];
-                __syncthreads();
-                if (want) {
-                    int j = 0;
-                    double b0 = best, b1 = __builtin_inf();
-                    for (; j + 1 < cn; j += 2) {
-                        const double2 q0 = pts[j], q1 = pts[j + 1];
-                        const double dx0 = x - q0.x, dy0 = y - q0.y;
-                        const double dx1 = x - q1.x, dy1 = y - q1.y;
-                        const double v0 = dx0 * dx0 + dy0 * dy0;
-                        const double v1 = dx1 * dx1 + dy1 * dy1;
-                        b0 = v0 < b0 ? v0 : b0;
-                        b1 = v1 < b1 ? v1 : b1;
-                    }
-                    if (j < cn) {
-                        const double2 q0 = pts[j];
-                        const double dx0 = x - q0.x, dy0 = y - q0.y;
-                        const double v0 = dx0 * dx0 + dy0 * dy0;
-                        b0 = v0 < b0 ? v0 : b0;
-                    }
-                    best = b0 < b1 ? b0 : b1;
-                }
-            }
-        }
-    } else if (want) {
-        const int64_t g = e / epg;
-        best = demo_min_global(demo + off[g], off[g + 1] - off[g], x, y);
+        const int64_t m = hi - lo, per = (m + kDemoSplit - 1) / kDemoSplit;
+        const int64_t a = lo + wv * per, b = a + per < hi ? a + per : hi;
+        best = a < b ? demo_min_uniform(demo + 2 * a, (int)(b - a), x, y) : __builtin_inf();
+    } else if (wv == 0) {
+        const int64_t g = live ? e / epg : g0;
+        best = demo_min_global(reinterpret_cast<const double2*>(demo) + off[g],
+                               off[g + 1] - off[g], x, y);
+    } else {
+        best = __builtin_inf();
     }
-    if (!want) return;
+    part[wv][lane] = best;
+    __syncthreads();
+    if (wv != 0 || !want) return;
+#pragma unroll
+    for (int k = 1; k < kDemoSplit; ++k) best = fmin(best, part[k][lane]);
     // robot.py:756-760 then the stuck penalty of robot.py:667-669
     const double mn = sqrt(best);
     double r = gterm[e] + p.demo_factor * (-mn);
@@ -308,6 +384,56 @@ __global__ __launch_bounds__(kBlock) void k_demo_reward(nav_params p, int64_t n,
     const int64_t slot = (base + e) % cap;
     rows[slot * NAV_ROW + 4] = (float)r;
     if (reward_out) reward_out[e] = r;
+}
+
+// Batched open-loop rollouts through Environment.dynamics (the CEM demonstrator's inner loop,
+// environment.py:230-244): lane = path, T sequential steps, state carried in f64; paths [P][T+1][2]
+// f64; reward (nullable) = -||f32(s_T) - goal|| as compute_reward on the float32 planning_paths
+// row (environment.py:243, 261-262).
+__global__ __launch_bounds__(kBlock) void k_rollout(const float2* __restrict__ field, int64_t P,
+                                                    int32_t T, const double2* __restrict__ start,
+                                                    const double2* __restrict__ actions,
+                                                    double2* __restrict__ paths,
+                                                    const double* __restrict__ goal,
+                                                    double* __restrict__ reward) {
+    const int64_t pth = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (pth >= P) return;
+    double2 s = start[pth];
+    paths[pth * (T + 1)] = s;
+    for (int t = 0; t < T; ++t) {
+        s = dynamics(field, s, actions[pth * T + t]);
+        paths[pth * (T + 1) + t + 1] = s;
+    }
+    if (reward) {
+        const double fx = (double)(float)s.x, fy = (double)(float)s.y;
+        reward[pth] = -norm2(fx - goal[0], fy - goal[1]);
+    }
+}
+
+// ReplayBuffer.push (robot.py:79-96) of n transitions given as f64 arrays.
+__global__ __launch_bounds__(kBlock) void k_replay_push(int64_t n, const double2* __restrict__ s,
+                                                        const double2* __restrict__ a,
+                                                        const double* __restrict__ r,
+                                                        const double2* __restrict__ s2,
+                                                        const uint8_t* __restrict__ d,
+                                                        float4* __restrict__ rows, int64_t cap,
+                                                        int64_t base) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const int64_t slot = (base + i) % cap;
+    const double2 x = s[i], y = a[i], z = s2[i];
+    rows[2 * slot] = make_float4((float)x.x, (float)x.y, (float)y.x, (float)y.y);
+    rows[2 * slot + 1] = make_float4((float)r[i], (float)z.x, (float)z.y, d[i] ? 1.f : 0.f);
+}
+
+// robot.py:753 min_j ||p_i - d_j|| for arbitrary points (scipy cdist semantics).
+__global__ __launch_bounds__(kBlock) void k_demo_min(const double2* __restrict__ pts, int64_t n,
+                                                     const double2* __restrict__ demo, int64_t m,
+                                                     double* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const double2 s = pts[i];
+    out[i] = sqrt(demo_min_global(demo, m, s.x, s.y));
 }
 
 __global__ __launch_bounds__(kBlock) void k_compute_reward(nav_params p, int64_t n,
@@ -430,6 +556,69 @@ int nav_agent_step(const nav_params* p, const nav_env_soa* env, const float* fie
     return 0;
 }
 
+int nav_transition(const nav_params* p, const nav_env_soa* env, const double* state,
+                   const double* action, const double* next_state, const nav_replay* replay,
+                   int64_t replay_base, const nav_step_out* out, void* stream) {
+    if (!p || !env || env->n < 0 || !replay || !replay->rows || replay->capacity <= 0 ||
+        replay_base < 0 || !out)
+        return NAV_EINVAL;
+    if (env->n == 0) return 0;
+    if (!env->goal || !env->hist || !env->meta || !env->plan_index || !env->path_length ||
+        !state || !action || !next_state)
+        return NAV_EINVAL;
+    hipLaunchKernelGGL(k_transition, dim3(blocks_for(env->n)), dim3(kBlock), 0, S(stream), *p,
+                       *env, reinterpret_cast<const double2*>(state),
+                       reinterpret_cast<const double2*>(action),
+                       reinterpret_cast<const double2*>(next_state),
+                       reinterpret_cast<float4*>(replay->rows), replay->capacity,
+                       replay_base % replay->capacity, *out);
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_check_if_stuck(const nav_params* p, const nav_env_soa* env, const double* state,
+                       uint8_t* stuck, void* stream) {
+    if (!p || !env || env->n < 0 || (env->n && (!env->hist || !env->meta || !state || !stuck)))
+        return NAV_EINVAL;
+    if (env->n == 0) return 0;
+    hipLaunchKernelGGL(k_check_if_stuck, dim3(blocks_for(env->n)), dim3(kBlock), 0, S(stream),
+                       *p, *env, reinterpret_cast<const double2*>(state), stuck);
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_rollout(const float* field, int64_t P, int32_t T, const double* start,
+                const double* actions, double* paths, const double* goal, double* reward,
+                void* stream) {
+    if (P < 0 || T < 0 || (P && (!field || !start || !actions || !paths)) || (reward && !goal))
+        return NAV_EINVAL;
+    if (P == 0) return 0;
+    hipLaunchKernelGGL(k_rollout, dim3(blocks_for(P)), dim3(kBlock), 0, S(stream),
+                       reinterpret_cast<const float2*>(field), P, T,
+                       reinterpret_cast<const double2*>(start),
+                       reinterpret_cast<const double2*>(actions),
+                       reinterpret_cast<double2*>(paths), goal, reward);
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_replay_push(const nav_replay* replay, int64_t base, int64_t n, const double* state,
+                    const double* action, const double* reward, const double* next_state,
+                    const uint8_t* done, void* stream) {
+    if (!replay || !replay->rows || replay->capacity <= 0 || base < 0 || n < 0 ||
+        (n && (!state || !action || !reward || !next_state || !done)))
+        return NAV_EINVAL;
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_replay_push, dim3(blocks_for(n)), dim3(kBlock), 0, S(stream), n,
+                       reinterpret_cast<const double2*>(state),
+                       reinterpret_cast<const double2*>(action), reward,
+                       reinterpret_cast<const double2*>(next_state), done,
+                       reinterpret_cast<float4*>(replay->rows), replay->capacity,
+                       base % replay->capacity);
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
 int nav_demo_reward(const nav_params* p, int64_t n, const double* next_state,
                     const double* goal_term, const uint8_t* flags, const double* demo_xy,
                     const int64_t* demo_off, int64_t m, int32_t epg, const nav_replay* replay,
@@ -440,11 +629,23 @@ int nav_demo_reward(const nav_params* p, int64_t n, const double* next_state,
     if (demo_off && epg <= 0) return NAV_EINVAL;
     if (!demo_off && m > 0 && !demo_xy) return NAV_EINVAL;
     if (n == 0 || (!demo_off && m == 0)) return 0;
-    hipLaunchKernelGGL(k_demo_reward, dim3(blocks_for(n)), dim3(kBlock), 0, S(stream), *p, n,
-                       reinterpret_cast<const double2*>(next_state), goal_term, flags,
-                       reinterpret_cast<const double2*>(demo_xy), demo_off, m, epg > 0 ? epg : 1,
+    hipLaunchKernelGGL(k_demo_reward, dim3((unsigned)((n + kDemoEnvs - 1) / kDemoEnvs)),
+                       dim3(kDemoBlock), 0, S(stream), *p, n,
+                       reinterpret_cast<const double2*>(next_state), goal_term, flags, demo_xy,
+                       demo_off, m, epg > 0 ? epg : 1,
                        replay->rows, replay->capacity, replay_base % replay->capacity,
                        reward_out);
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_demo_min(const double* points, int64_t n, const double* demo_xy, int64_t m,
+                 double* out, void* stream) {
+    if (n < 0 || m < 1 || (n && (!points || !demo_xy || !out))) return NAV_EINVAL;
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_demo_min, dim3(blocks_for(n)), dim3(kBlock), 0, S(stream),
+                       reinterpret_cast<const double2*>(points), n,
+                       reinterpret_cast<const double2*>(demo_xy), m, out);
     NAV_CHECK_LAUNCH();
     return 0;
 }

@@ -68,6 +68,13 @@ SIGNATURES = [
                                  C.c_int64, _P(NavStepOut), _vp]),
     ("nav_demo_reward", C.c_int, [_P(NavParams), C.c_int64, _vp, _vp, _vp, _vp, _vp, C.c_int64,
                                   C.c_int32, _P(NavReplay), C.c_int64, _vp, _vp]),
+    ("nav_transition", C.c_int, [_P(NavParams), _P(NavEnvSoa), _vp, _vp, _vp, _P(NavReplay),
+                                 C.c_int64, _P(NavStepOut), _vp]),
+    ("nav_check_if_stuck", C.c_int, [_P(NavParams), _P(NavEnvSoa), _vp, _vp, _vp]),
+    ("nav_rollout", C.c_int, [_vp, C.c_int64, C.c_int32, _vp, _vp, _vp, _vp, _vp, _vp]),
+    ("nav_replay_push", C.c_int, [_P(NavReplay), C.c_int64, C.c_int64, _vp, _vp, _vp, _vp, _vp,
+                                  _vp]),
+    ("nav_demo_min", C.c_int, [_vp, C.c_int64, _vp, C.c_int64, _vp, _vp]),
     ("nav_compute_reward", C.c_int, [_P(NavParams), C.c_int64, _vp, _vp, _vp, C.c_int64,
                                      C.c_int32, _vp, _vp, _vp]),
     ("nav_act", C.c_int, [_P(NavParams), _P(NavMlp), C.c_int64, _vp, _vp, _vp, _vp, C.c_uint32,

@@ -1,0 +1,148 @@
+"""The N = 1 drop-ins (nav.Environment, nav.Robot) against the reference's own outputs: same numpy
+seed -> same goal, region, start states, demonstrations, rewards and Robot counters."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def navmods():
+    from nav import _lib
+    _lib.require_gpu()
+    from nav import environment, robot
+    return environment, robot
+
+
+def test_environment_seeding_bit_exact(navmods):
+    environment, _ = navmods
+    g = golden("rng_init.npz")
+    d = golden("dynamics.npz")
+    for k, seed in enumerate(g["seeds"]):
+        np.random.seed(int(seed))
+        env = environment.Environment(d["speed"], d["angle"])
+        assert np.array_equal(np.asarray(env.robot_init_region, np.float64), g["region"][k])
+        assert np.array_equal(np.asarray(env.goal_state, np.float64), g["goal"][k])
+        for j in range(3):
+            assert np.array_equal(env.reset(), g["resets"][k][j])
+        assert np.array_equal(np.random.random_sample(4), g["tail"][k])
+
+
+def test_environment_dynamics_and_step_api(navmods):
+    environment, _ = navmods
+    d = golden("dynamics.npz")
+    np.random.seed(0)
+    env = environment.Environment(d["speed"], d["angle"])
+    for i in range(0, 300, 7):
+        out = env.dynamics(list(d["state"][i]), list(d["action"][i]))  # graphics.py:224 form
+        ref = d["dynamics"][i]
+        if np.isnan(ref).any():
+            assert np.isnan(out).any()
+        else:
+            assert np.max(np.abs(out - ref)) < 1e-11
+        env.robot_state = d["state"][i].copy()
+        before = env.robot_state
+        after = env.step(d["action"][i])
+        assert (after is before) == (not d["committed"][i])
+        assert np.max(np.abs(after - d["step"][i])) < 1e-11
+
+
+def _trace_setup(environment, robot):
+    t = golden("trace.npz")
+    torch.manual_seed(0)
+    np.random.seed(1707366464)
+    env = environment.Environment(t["speed"], t["angle"])
+    state = env.reset()
+    rb = robot.Robot(env.goal_state)
+    rb.td3_agent.td3_update = lambda memory: None  # as the trace generator did
+    return t, env, state, rb
+
+
+def test_demonstration_matches_reference(navmods):
+    environment, robot = navmods
+    t, env, state, rb = _trace_setup(environment, robot)
+    assert np.array_equal(np.asarray(env.goal_state, np.float64), t["goal"])
+    ds, da = env.get_demonstration()
+    assert ds.dtype == np.float32 and ds.shape == (200, 2) and da.shape == (200, 2)
+    assert np.array_equal(da, t["demo_actions"][0])
+    assert np.max(np.abs(ds - t["demo_states"][0])) < 1e-4
+
+
+def test_robot_replays_reference_trace(navmods):
+    """robot-learning.py's loop with nav.Environment + nav.Robot, teacher-forced with the
+    reference's actions (the actor weights differ): every numpy draw, reset, demonstration,
+    reward, done flag and Robot counter must follow the reference's trace."""
+    environment, robot = navmods
+    t, env, state, rb = _trace_setup(environment, robot)
+    types = t["tick_type"]
+    pushes = []
+    orig = rb.memory.advance
+
+    def advance(n):
+        pushes.append((rb.memory.position, n))
+        return orig(n)
+
+    rb.memory.advance = advance
+    c = t["counters"]
+    for i in range(len(types)):
+        at = rb.get_next_action_type(state, 100.0)
+        assert {"step": 0, "demo": 1, "reset": 2}[at] == types[i], i
+        if at == "reset":
+            state = env.reset()
+            assert np.array_equal(state, t["tick_next"][i]), i
+        elif at == "demo":
+            ds, da = env.get_demonstration()
+            rb.process_demonstration(ds, da, 100.0)
+        else:
+            rb.get_next_action_training(state, 100.0)  # consumes the same noise draws
+            a = t["tick_action"][i]
+            ns = env.step(a)
+            assert np.max(np.abs(ns - t["tick_next"][i])) < 1e-9, i
+            rb.process_transition(state, a, ns, 100.0)
+            state = ns
+            lo = t["push_idx"][i][0]
+            slot, n = pushes[-1]
+            row = rb.memory.rows[slot].cpu().numpy()
+            ref_r = t["push_r"][lo]
+            assert abs(row[4] - ref_r) <= 1e-4 * max(1.0, abs(ref_r)), i
+            assert row[7] == float(t["push_d"][lo])
+        cc = c[i]
+        assert (rb.plan_index, rb.path_length, rb.num_episodes) == (cc[0], cc[1], cc[2]), i
+        assert (int(rb.goal_reached), int(rb.stuck_flag), int(rb.demo_flag)) == \
+            (cc[3], cc[4], cc[5]), i
+        assert rb.current_noise_scale == cc[6]
+    assert len(rb.demonstration_states) == len(t["demo_set"])
+    got = np.asarray([np.asarray(x, np.float64) for x in rb.demonstration_states])
+    assert np.max(np.abs(got - t["demo_set"])) < 1e-4
+    assert len(rb.memory) == len(t["push_r"])
+
+
+def test_td3_update_dropin_runs(navmods):
+    """robot.py's TD3.td3_update(memory) end to end: 100 epochs, batch 100, numpy-drawn
+    permutations, finite weights afterwards."""
+    environment, robot = navmods
+    rb = robot.Robot(np.array([60.0, 40.0]))
+    rng = np.random.default_rng(0)
+    for _ in range(300):
+        s = rng.uniform(0, 100, 2)
+        rb.memory.push(s, rng.uniform(-5, 5, 2), rng.uniform(-100, 0), s + 1, False)
+    np.random.seed(3)
+    rb.td3_agent.td3_update(rb.memory)
+    torch.cuda.synchronize()
+    for net in rb.td3_agent.networks().values():
+        assert torch.isfinite(net.params).all()
+    assert rb.td3_agent.actor_optimizer.step_count == 50
+    assert rb.td3_agent.critic_optimizer_1.step_count == 100
+    st = rb.memory.sample(100)
+    assert st[0].shape == (100, 2) and st[4].dtype == bool
+
+
+def test_headless_driver_short_run(navmods):
+    from nav import driver
+    d = golden("dynamics.npz")
+    r = driver.run(seed=5, max_ticks=40, budget=False, verbose=False,
+                   env_kwargs={"speed": d["speed"], "angle": d["angle"]})
+    assert r["demos"] == 3 and r["steps"] > 0 and r["ticks"] == 40

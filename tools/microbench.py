@@ -88,6 +88,27 @@ def main():
     res["demo_reward"] = {"us": sm["demo_reward"]["avg_us"],
                           "f64_TFs": prof.demo_flops(args.envs, m_per) /
                           sm["demo_reward"]["avg_us"] / 1e6}
+    # host cost of issuing one full training step vs its GPU time
+    import time
+    tr2 = VecTrainer(n_envs=args.envs, hidden=H, n_hidden=L, batch=B, updates_per_step=2,
+                     device=dev)
+    for _ in range(3):
+        tr2.step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(10):
+        tr2.step()
+    t1 = time.perf_counter()
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    res["train_step"] = {"host_issue_us": (t1 - t0) * 1e5, "wall_us": (t2 - t0) * 1e5}
+    for splits in (16, 32, 64):
+        sl = torch.zeros(splits, crit[0].count, device=dev)
+        us_w = timeit(lambda: lib().nav_mlp_wgrad(C.byref(d), B, ptr(x), 4, 0, ptr(acts),
+                                                  ptr(dz), ptr(dy), ptr(sl), splits, s))
+        us_r = timeit(lambda: lib().nav_grad_reduce(ptr(sl), splits, crit[0].count, ptr(grad),
+                                                    s))
+        res[f"wgrad_splits{splits}"] = {"wgrad_us": us_w, "reduce_us": us_r}
     print(json.dumps({k: {kk: round(vv, 3) if isinstance(vv, float) else vv
                           for kk, vv in v.items()} for k, v in res.items()}), flush=True)
 
