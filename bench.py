@@ -138,18 +138,16 @@ def main():
         print(json.dumps(step_kernel_sweep(make_field(*make_fields(args.seed), dev),
                                            [args.sweep_only])), flush=True)
         return
-    hook = None
-    if args.shared_policy and ws > 1:
-        def hook(g):  # RCCL all-reduce (sum) over xGMI, then mean
-            torch.distributed.all_reduce(g)
-            g.div_(ws)
+    from nav.dist import broadcast_params, make_grad_hook, max_over_ranks, shard_seed
+    hook = make_grad_hook(ws) if args.shared_policy else None  # RCCL all-reduce over xGMI
     tr = VecTrainer(n_envs=args.envs, hidden=args.hidden, n_hidden=args.layers, batch=args.batch,
-                    updates_per_step=args.updates, seed=args.seed + rank,
+                    updates_per_step=args.updates, seed=shard_seed(args.seed, rank),
                     envs_per_group=args.envs_per_group, device=dev, grad_hook=hook)
-    if args.shared_policy and ws > 1:
-        for net in tr.td3.networks().values():  # same initial policy on every rank
-            torch.distributed.broadcast(net.params, 0)
-            net.pack()
+    if args.shared_policy and ws > 1:  # same initial policy on every rank
+        nets = list(tr.td3.networks().values())
+        broadcast_params([n.params for n in nets])
+        for n in nets:
+            n.pack()
     # warmup: first step fills the replay ring past one batch; then breakdown pass
     for _ in range(max(args.warmup, 1)):
         tr.step()
@@ -173,9 +171,7 @@ def main():
     barrier(ws)
     dt = time.perf_counter() - t0
     if ws > 1:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        dt = t.item()
+        dt = max_over_ranks(dt, dev)
     ksum = timer.summary()
     env_steps = args.envs * args.steps * ws
     value = env_steps / dt

@@ -506,7 +506,10 @@ int nav_env_init(const nav_params* p, const nav_env_soa* env, int32_t epg, int32
 
 int nav_env_reset(const nav_params* p, const nav_env_soa* env, const uint8_t* mask,
                   const double* uniforms, void* stream) {
-    if (!p || !env_ok(env)) return NAV_EINVAL;
+    // needs state + region; the Philox draw also reads episodes
+    if (!p || !env || env->n < 0 ||
+        (env->n && (!env->state || !env->region || (!uniforms && !env->episodes))))
+        return NAV_EINVAL;
     if (env->n == 0) return 0;
     hipLaunchKernelGGL(k_env_reset, dim3(blocks_for(env->n)), dim3(kBlock), 0, S(stream), *p,
                        *env, mask, reinterpret_cast<const double2*>(uniforms));

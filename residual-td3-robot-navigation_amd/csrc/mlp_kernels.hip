@@ -9,6 +9,8 @@
 // input layer (K = 2 or 4) and output layer (N = 1 or 2) run on the VALU; ReLU derivatives travel
 // from forward to backward as C-layout bit masks. Weight gradients: one launch per network over
 // row splits writing deterministic partial slabs, reduced in a fixed order.
+#include <stdlib.h>
+
 #include "nav_device.h"
 
 using namespace nav;
@@ -18,7 +20,7 @@ namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kMaxLayers = 9;
-constexpr int TM = 128;  // rows per workgroup
+constexpr int TM = 128;  // max rows per workgroup (row tiles of 32: RT = 1, 2 or 4)
 
 struct MlpDev {
     const float* params;
@@ -77,15 +79,15 @@ struct WaveCols {
 // once per workgroup, prefetched two K-steps ahead in registers. No barrier inside the K loop:
 // the LDS rows are read-only during the product. K order inside an 8-deep step is permuted the
 // same way for A and B (lane half h covers k = 8q + 4h + s at MFMA s).
-template <int NT>
+template <int NT, int RT>
 NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const float* __restrict__ Bp,
-                       f32x16 (&acc)[4][2]) {
+                       f32x16 (&acc)[RT][2]) {
     constexpr int hp = NT * 32;
     constexpr int nq = hp / 8;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
     const WaveCols<NT> wc(wv);
 #pragma unroll
-    for (int rt = 0; rt < 4; ++rt)
+    for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -106,12 +108,12 @@ NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const float* __restr
             p1 = B0[(q + 2) * STEP];
             if (wc.has1) r1 = B1[(q + 2) * STEP];
         }
-        float4 a[4];
+        float4 a[RT];
 #pragma unroll
-        for (int rt = 0; rt < 4; ++rt)
+        for (int rt = 0; rt < RT; ++rt)
             a[rt] = *reinterpret_cast<const float4*>(arow + rt * 32 * S_ + 8 * q);
 #define NAV_MF(S, C)                                                                     \
-    _Pragma("unroll") for (int rt = 0; rt < 4; ++rt) {                                  \
+    _Pragma("unroll") for (int rt = 0; rt < RT; ++rt) {                                 \
         acc[rt][0] = mfma(a[rt].S, c0.S, acc[rt][0]);                                   \
         if (NT >= 8 || wc.has1) acc[rt][1] = mfma(a[rt].S, c1.S, acc[rt][1]);           \
     }
@@ -154,12 +156,16 @@ struct FwdArgs {
     double* action_out;
 };
 
-inline size_t lds_bytes(int hp) { return ((size_t)TM * (hp + 4) + TM * 4) * 4; }
+inline size_t lds_bytes(int hp, int tm) { return ((size_t)tm * (hp + 4) + tm * 4) * 4; }
+
+// Mask image row-tile count: independent of the workgroup height, so any RT reads what any RT
+// wrote (row tile = global row / 32; layers strided by ceil(M/128)*4 tiles).
+__host__ __device__ inline int64_t mask_rowtiles(int64_t M) { return ((M + 127) / 128) * 4; }
 
 // Store a layer's C-layout result into the LDS rows (the next layer's A operand) and its ReLU
 // mask bits. Global copies of the rows are written afterwards by copy_rows (coalesced).
-template <int NT>
-NAV_DEV void store_layer(f32x16 (&acc)[4][2], float* act, int S_, uint16_t* mask, int64_t rt0) {
+template <int NT, int RT>
+NAV_DEV void store_layer(f32x16 (&acc)[RT][2], float* act, int S_, uint16_t* mask, int64_t rt0) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
     const WaveCols<NT> wc(wv);
 #pragma unroll
@@ -168,7 +174,7 @@ NAV_DEV void store_layer(f32x16 (&acc)[4][2], float* act, int S_, uint16_t* mask
         const int t = j == 0 ? wc.t0 : wc.t1;
         float* col = act + t * 32 + l32 + 4 * h * S_;
 #pragma unroll
-        for (int rt = 0; rt < 4; ++rt) {
+        for (int rt = 0; rt < RT; ++rt) {
             uint32_t bits = 0;
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
@@ -182,10 +188,10 @@ NAV_DEV void store_layer(f32x16 (&acc)[4][2], float* act, int S_, uint16_t* mask
 }
 
 // 128 LDS rows -> global [M][hp] rows row0.., float4 per lane (1 KiB per wave instruction).
-template <int NT>
+template <int NT, int RT>
 NAV_DEV void copy_rows(const float* act, int S_, float* g, int64_t row0, int64_t M) {
     constexpr int hp = NT * 32, Q4 = hp / 4;
-    for (int idx = threadIdx.x; idx < TM * Q4; idx += kBlock) {
+    for (int idx = threadIdx.x; idx < RT * 32 * Q4; idx += kBlock) {
         const int r = idx / Q4, c4 = idx - r * Q4;
         if (row0 + r < M)
             *reinterpret_cast<float4*>(g + (row0 + r) * hp + 4 * c4) =
@@ -193,20 +199,20 @@ NAV_DEV void copy_rows(const float* act, int S_, float* g, int64_t row0, int64_t
     }
 }
 
-template <int NT, int IN_MODE, int OUT_MODE>
+template <int NT, int RT, int IN_MODE, int OUT_MODE>
 __global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    constexpr int hp = NT * 32, SS = hp + 4;
+    constexpr int hp = NT * 32, SS = hp + 4, TM = RT * 32;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, l32 = lane & 31;
     const MlpDev& net = a.net[blockIdx.y];
     float* act_save = a.acts[blockIdx.y];
     uint16_t* masks = a.masks[blockIdx.y];
     const int64_t M = a.M;
     const int64_t row0 = (int64_t)blockIdx.x * TM;
-    const int64_t rt0 = (int64_t)blockIdx.x * 4;
-    const int64_t n_rt = ((M + TM - 1) / TM) * 4;
+    const int64_t rt0 = (int64_t)blockIdx.x * RT;
+    const int64_t n_rt = mask_rowtiles(M);
     float* act = smem;
-    float* xin = smem + TM * SS;  // [128][4]
+    float* xin = smem + TM * SS;  // [TM][4]
     const int d_in = net.d_in, d_out = net.d_out, nh = net.n_hidden;
     const WaveCols<NT> wc(wv);
 
@@ -249,7 +255,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
             float* col = act + c + 4 * h * SS;
             const float* xr = xin + 4 * h * 4;
 #pragma unroll 1
-            for (int rt = 0; rt < 4; ++rt) {
+            for (int rt = 0; rt < RT; ++rt) {
                 uint32_t bits = 0;
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
@@ -269,31 +275,32 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
         }
     }
     __syncthreads();
-    if (act_save) copy_rows<NT>(act, SS, act_save, row0, M);
+    if (act_save) copy_rows<NT, RT>(act, SS, act_save, row0, M);
 
     // ---- hidden x hidden layers on MFMA
     for (int L = 1; L < nh; ++L) {
-        f32x16 acc[4][2];
-        gemm_cols<NT>(act, SS, net.packed + (int64_t)(L - 1) * 2 * hp * hp, acc);
+        f32x16 acc[RT][2];
+        gemm_cols<NT, RT>(act, SS, net.packed + (int64_t)(L - 1) * 2 * hp * hp, acc);
         const float* bL = net.params + net.b_off[L];
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             if (!(j == 0 ? wc.has0 : wc.has1)) continue;
             const float b = bL[(j == 0 ? wc.t0 : wc.t1) * 32 + l32];
 #pragma unroll
-            for (int rt = 0; rt < 4; ++rt)
+            for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
                 for (int i = 0; i < 16; ++i) acc[rt][j][i] = fmaxf(acc[rt][j][i] + b, 0.f);
         }
         __syncthreads();  // every wave has finished reading the layer's input rows
-        store_layer<NT>(acc, act, SS, masks ? masks + (size_t)L * n_rt * NT * 64 : nullptr, rt0);
+        store_layer<NT, RT>(acc, act, SS, masks ? masks + (size_t)L * n_rt * NT * 64 : nullptr,
+                            rt0);
         __syncthreads();
-        if (act_save) copy_rows<NT>(act, SS, act_save + (int64_t)L * M * hp, row0, M);
+        if (act_save) copy_rows<NT, RT>(act, SS, act_save + (int64_t)L * M * hp, row0, M);
     }
 
     // ---- output layer (N = d_out <= 2) on the VALU: thread = (row, output)
-    const int rloc = tid & (TM - 1);
-    const int j = tid >> 7;
+    const int rloc = tid % TM;
+    const int j = tid / TM;
     const int64_t r = row0 + rloc;
     float y = 0.f;
     if (j < d_out) {
@@ -361,8 +368,8 @@ struct BwdArgs {
     float* dx;
 };
 
-template <int NT>
-NAV_DEV void mask_and_store(f32x16 (&acc)[4][2], const uint16_t* mask, float* act, int S_,
+template <int NT, int RT>
+NAV_DEV void mask_and_store(f32x16 (&acc)[RT][2], const uint16_t* mask, float* act, int S_,
                             int64_t rt0) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
     const WaveCols<NT> wc(wv);
@@ -372,7 +379,7 @@ NAV_DEV void mask_and_store(f32x16 (&acc)[4][2], const uint16_t* mask, float* ac
         const int t = j == 0 ? wc.t0 : wc.t1;
         float* col = act + t * 32 + l32 + 4 * h * S_;
 #pragma unroll
-        for (int rt = 0; rt < 4; ++rt) {
+        for (int rt = 0; rt < RT; ++rt) {
             const uint32_t bits = mask[mask_idx(rt0 + rt, NT, t, lane)];
 #pragma unroll
             for (int i = 0; i < 16; ++i)
@@ -382,16 +389,16 @@ NAV_DEV void mask_and_store(f32x16 (&acc)[4][2], const uint16_t* mask, float* ac
     }
 }
 
-template <int NT>
+template <int NT, int RT>
 __global__ __launch_bounds__(kBlock, 1) void k_mlp_bwd(BwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    constexpr int hp = NT * 32, SS = hp + 4;
+    constexpr int hp = NT * 32, SS = hp + 4, TM = RT * 32;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, l32 = lane & 31;
     const MlpDev& net = a.net;
     const int64_t M = a.M;
     const int64_t row0 = (int64_t)blockIdx.x * TM;
-    const int64_t rt0 = (int64_t)blockIdx.x * 4;
-    const int64_t n_rt = ((M + TM - 1) / TM) * 4;
+    const int64_t rt0 = (int64_t)blockIdx.x * RT;
+    const int64_t n_rt = mask_rowtiles(M);
     float* act = smem;
     float* dys = smem + TM * SS;
     const int d_in = net.d_in, d_out = net.d_out, nh = net.n_hidden;
@@ -422,7 +429,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_bwd(BwdArgs a) {
             float* col = act + c + 4 * h * SS;
             const float* gr = dys + 4 * h * 4;
 #pragma unroll 1
-            for (int rt = 0; rt < 4; ++rt) {
+            for (int rt = 0; rt < RT; ++rt) {
                 const uint32_t bits = mk[mask_idx(rt0 + rt, NT, t, lane)];
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
@@ -435,26 +442,26 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_bwd(BwdArgs a) {
         }
     }
     __syncthreads();
-    copy_rows<NT>(act, SS, a.dz + (int64_t)(nh - 1) * MH, row0, M);
+    copy_rows<NT, RT>(act, SS, a.dz + (int64_t)(nh - 1) * MH, row0, M);
 
     // hidden layers, top-down: dz_{L-1} = (dz_L . W_L) * relu'(act_{L-1}), B = packed Wb_L
     for (int L = nh - 1; L >= 1; --L) {
-        f32x16 acc[4][2];
-        gemm_cols<NT>(act, SS, net.packed + (int64_t)(L - 1) * 2 * hp * hp + (int64_t)hp * hp,
-                      acc);
+        f32x16 acc[RT][2];
+        gemm_cols<NT, RT>(act, SS,
+                          net.packed + (int64_t)(L - 1) * 2 * hp * hp + (int64_t)hp * hp, acc);
         __syncthreads();
-        mask_and_store<NT>(acc, a.masks + (size_t)(L - 1) * mstride, act, SS, rt0);
+        mask_and_store<NT, RT>(acc, a.masks + (size_t)(L - 1) * mstride, act, SS, rt0);
         __syncthreads();
-        copy_rows<NT>(act, SS, a.dz + (int64_t)(L - 1) * MH, row0, M);
+        copy_rows<NT, RT>(act, SS, a.dz + (int64_t)(L - 1) * MH, row0, M);
     }
 
     // dx = dz_0 . W0 : thread = (row, input pair)
     if (a.dx) {
         const float* W0 = net.params + net.w_off[0];
-        const int rloc = tid & (TM - 1);
+        const int rloc = tid % TM;
         const int64_t r = row0 + rloc;
         const float* zr = act + rloc * SS;
-        for (int jj = tid >> 7; jj < d_in; jj += 2) {
+        for (int jj = tid / TM; jj < d_in; jj += kBlock / TM) {
             float acc = 0.f;
             for (int c = 0; c < hp; ++c) acc = fmaf(zr[c], W0[c * d_in + jj], acc);
             if (r < M) a.dx[r * d_in + jj] = acc;
@@ -831,21 +838,37 @@ PackInfo pack_info(const MlpDev& d, float* packed) {
     return pk;
 }
 
-// ---- launch helpers (template dispatch on NT = hp / 32) ----
+// ---- launch helpers (template dispatch on NT = hp / 32 and RT = rows / 32) ----
+// Workgroup height: RT = 4 (128 rows, one workgroup per CU) or RT = 2 (64 rows, two per CU so one
+// workgroup's epilogue overlaps the other's MFMA loop). NAV_MLP_RT overrides (tuning only).
+int row_tiles() {
+    static const int rt = [] {
+        const char* e = getenv("NAV_MLP_RT");
+        const int v = e ? atoi(e) : 2;
+        return (v == 4) ? 4 : 2;
+    }();
+    return rt;
+}
+
+template <int NT, int RT, int IN_MODE, int OUT_MODE>
+void launch_fwd_k(const FwdArgs& a, int n_nets, hipStream_t st) {
+    const size_t lds = lds_bytes(NT * 32, RT * 32);
+    auto k = k_mlp_fwd<NT, RT, IN_MODE, OUT_MODE>;
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    const dim3 grid((unsigned)((a.M + RT * 32 - 1) / (RT * 32)), (unsigned)n_nets);
+    hipLaunchKernelGGL(k, grid, dim3(kBlock), lds, st, a);
+}
+
 template <int IN_MODE, int OUT_MODE>
 int launch_fwd(const FwdArgs& a, int n_nets, hipStream_t st) {
-    const int hp = a.net[0].hp;
-    const size_t lds = lds_bytes(hp);
-    const dim3 grid((unsigned)((a.M + TM - 1) / TM), (unsigned)n_nets);
-#define NAV_FWD_CASE(NT_)                                                                        \
-    case NT_: {                                                                                  \
-        auto k = k_mlp_fwd<NT_, IN_MODE, OUT_MODE>;                                              \
-        hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,          \
-                            (int)lds);                                                           \
-        hipLaunchKernelGGL(k, grid, dim3(kBlock), lds, st, a);                                   \
-        break;                                                                                   \
-    }
-    switch (hp / 32) {
+    const int rt = row_tiles();
+#define NAV_FWD_CASE(NT_)                                                                    \
+    case NT_:                                                                                \
+        if (rt == 4) launch_fwd_k<NT_, 4, IN_MODE, OUT_MODE>(a, n_nets, st);                 \
+        else launch_fwd_k<NT_, 2, IN_MODE, OUT_MODE>(a, n_nets, st);                         \
+        break;
+    switch (a.net[0].hp / 32) {
         NAV_FWD_CASE(1) NAV_FWD_CASE(2) NAV_FWD_CASE(3) NAV_FWD_CASE(4)
         NAV_FWD_CASE(5) NAV_FWD_CASE(6) NAV_FWD_CASE(7) NAV_FWD_CASE(8)
         default: return NAV_EINVAL;
@@ -855,19 +878,24 @@ int launch_fwd(const FwdArgs& a, int n_nets, hipStream_t st) {
     return 0;
 }
 
+template <int NT, int RT>
+void launch_bwd_k(const BwdArgs& a, hipStream_t st) {
+    const size_t lds = lds_bytes(NT * 32, RT * 32);
+    auto k = k_mlp_bwd<NT, RT>;
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    const dim3 grid((unsigned)((a.M + RT * 32 - 1) / (RT * 32)));
+    hipLaunchKernelGGL(k, grid, dim3(kBlock), lds, st, a);
+}
+
 int launch_bwd(const BwdArgs& a, hipStream_t st) {
-    const int hp = a.net.hp;
-    const size_t lds = lds_bytes(hp);
-    const dim3 grid((unsigned)((a.M + TM - 1) / TM));
-#define NAV_BWD_CASE(NT_)                                                                        \
-    case NT_: {                                                                                  \
-        auto k = k_mlp_bwd<NT_>;                                                                 \
-        hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,          \
-                            (int)lds);                                                           \
-        hipLaunchKernelGGL(k, grid, dim3(kBlock), lds, st, a);                                   \
-        break;                                                                                   \
-    }
-    switch (hp / 32) {
+    const int rt = row_tiles();
+#define NAV_BWD_CASE(NT_)                                                                    \
+    case NT_:                                                                                \
+        if (rt == 4) launch_bwd_k<NT_, 4>(a, st);                                            \
+        else launch_bwd_k<NT_, 2>(a, st);                                                    \
+        break;
+    switch (a.net.hp / 32) {
         NAV_BWD_CASE(1) NAV_BWD_CASE(2) NAV_BWD_CASE(3) NAV_BWD_CASE(4)
         NAV_BWD_CASE(5) NAV_BWD_CASE(6) NAV_BWD_CASE(7) NAV_BWD_CASE(8)
         default: return NAV_EINVAL;
@@ -968,7 +996,7 @@ int nav_mlp_forward(const nav_mlp* nets, int32_t n_nets, int64_t M, const float*
 int64_t nav_mlp_mask_count(int32_t hidden_pad, int32_t n_hidden, int64_t M) {
     if (hidden_pad < 32 || hidden_pad > 256 || (hidden_pad & 31) || n_hidden < 1 || M < 0)
         return NAV_EINVAL;
-    return (int64_t)n_hidden * ((M + TM - 1) / TM) * 4 * (hidden_pad / 32) * 64;
+    return (int64_t)n_hidden * mask_rowtiles(M) * (hidden_pad / 32) * 64;
 }
 
 int nav_mlp_backward(const nav_mlp* net, int64_t M, const float* dy, const uint16_t* masks,
