@@ -159,6 +159,25 @@ int nav_demo_reward(const nav_params* p, int64_t n, const double* next_state,
                     const int64_t* demo_off, int64_t m, int32_t envs_per_group,
                     const nav_replay* replay, int64_t replay_base, double* reward_out,
                     void* stream);
+/* Exact bucketed nearest-demo index over the 100 x 100 dynamics cells (robot.py:753 made
+ * sublinear, result bit-identical to the brute force): for each (group, cell) the bound
+ * U^2 = min_q maxdist^2(q, cell) and the candidate count (plan), an exclusive scan into
+ * cell_start [n_groups*10000 + 1] (scan), then ascending group-relative point indices (fill).
+ * cell_bound f64 / cell_count i32: [n_groups][10000]; cand: cell_start[last] int32 entries. */
+int nav_demo_index_plan(const double* demo_xy, const int64_t* demo_off, int32_t n_groups,
+                        int64_t m, double* cell_bound, int32_t* cell_count, void* stream);
+int nav_demo_index_scan(const int32_t* cell_count, int32_t n_groups, int64_t* cell_start,
+                        void* stream);
+int nav_demo_index_fill(const double* demo_xy, const int64_t* demo_off, int32_t n_groups,
+                        int64_t m, const double* cell_bound, const int64_t* cell_start,
+                        int32_t* cand, void* stream);
+/* nav_demo_reward through the index (same result, ~11 instead of 11 355 points per env). */
+int nav_demo_reward_indexed(const nav_params* p, int64_t n, const double* next_state,
+                            const double* goal_term, const uint8_t* flags, const double* demo_xy,
+                            const int64_t* demo_off, int32_t envs_per_group,
+                            const int64_t* cell_start, const int32_t* cand,
+                            const nav_replay* replay, int64_t replay_base, double* reward_out,
+                            void* stream);
 /* robot.py:753 min_j ||p_i - d_j|| (scipy cdist euclidean, f64) for n points [n][2]. */
 int nav_demo_min(const double* points, int64_t n, const double* demo_xy, int64_t m,
                  double* out, void* stream);

@@ -436,6 +436,188 @@ __global__ __launch_bounds__(kBlock) void k_demo_min(const double2* __restrict__
     out[i] = sqrt(demo_min_global(demo, m, s.x, s.y));
 }
 
+// ---------------- exact bucketed nearest-demo index (1 x 1 cells = the dynamics cells) --------
+// For cell C = [i, i+1) x [j, j+1): U(C)^2 = min_q maxdist^2(q, C) bounds the nearest-demo
+// distance of every query inside C, so the nearest point p* satisfies mindist(p*, C) <= U(C).
+// The candidate list of C = { p : mindist^2(p, C) <= U^2 (1 + 1e-12) + 1e-12 } contains p* for
+// every query in C; the kernel then takes the same f64 minimum over it as over all points, so the
+// result is bit-identical to the brute force (tests/test_gpu_env.py checks it).
+constexpr int kCells = NAV_WORLD_CELLS * NAV_WORLD_CELLS;
+
+NAV_DEV double cell_maxd2(double px, double py, double lx, double ly) {
+    const double fx = fmax(fabs(px - lx), fabs(px - (lx + 1.0)));
+    const double fy = fmax(fabs(py - ly), fabs(py - (ly + 1.0)));
+    return fx * fx + fy * fy;
+}
+
+NAV_DEV double cell_mind2(double px, double py, double lx, double ly) {
+    const double nx = fmax(0.0, fmax(lx - px, px - (lx + 1.0)));
+    const double ny = fmax(0.0, fmax(ly - py, py - (ly + 1.0)));
+    return nx * nx + ny * ny;
+}
+
+NAV_DEV double block_min(double v, double* red) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) red[wv] = v;
+    __syncthreads();
+    v = red[0];
+    for (int w = 1; w < kBlock / 64; ++w) v = fmin(v, red[w]);
+    return v;
+}
+
+// grid = (cells, groups): bound U^2 and candidate count of one cell of one group
+__global__ __launch_bounds__(kBlock) void k_demo_index_plan(const double2* __restrict__ demo,
+                                                            const int64_t* __restrict__ off,
+                                                            int64_t m_shared,
+                                                            double* __restrict__ bound,
+                                                            int32_t* __restrict__ count) {
+    __shared__ double red[kBlock / 64];
+    __shared__ int cnt[kBlock / 64];
+    const int cell = blockIdx.x, g = blockIdx.y;
+    const int64_t lo = off ? off[g] : 0, hi = off ? off[g + 1] : m_shared;
+    const double lx = (double)(cell / NAV_WORLD_CELLS), ly = (double)(cell % NAV_WORLD_CELLS);
+    double u = __builtin_inf();
+    for (int64_t j = lo + threadIdx.x; j < hi; j += kBlock) {
+        const double2 q = demo[j];
+        u = fmin(u, cell_maxd2(q.x, q.y, lx, ly));
+    }
+    u = block_min(u, red);
+    const double lim = u * (1.0 + 1e-12) + 1e-12;
+    int c = 0;
+    for (int64_t j = lo + threadIdx.x; j < hi; j += kBlock) {
+        const double2 q = demo[j];
+        c += cell_mind2(q.x, q.y, lx, ly) <= lim ? 1 : 0;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if ((threadIdx.x & 63) == 0) cnt[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int t = 0;
+        for (int w = 0; w < kBlock / 64; ++w) t += cnt[w];
+        const int64_t k = (int64_t)g * kCells + cell;
+        bound[k] = lim;
+        count[k] = t;
+    }
+}
+
+// exclusive scan of counts [n] into start [n + 1] (one workgroup; set-up time only)
+__global__ __launch_bounds__(kBlock) void k_scan_counts(const int32_t* __restrict__ count,
+                                                        int64_t n, int64_t* __restrict__ start) {
+    __shared__ int64_t part[kBlock];
+    const int64_t per = (n + kBlock - 1) / kBlock;
+    const int64_t a = threadIdx.x * per, b = a + per < n ? a + per : n;
+    int64_t s = 0;
+    for (int64_t i = a; i < b; ++i) s += count[i];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t run = 0;
+        for (int t = 0; t < kBlock; ++t) {
+            const int64_t v = part[t];
+            part[t] = run;
+            run += v;
+        }
+        start[n] = run;
+    }
+    __syncthreads();
+    int64_t run = part[threadIdx.x];
+    for (int64_t i = a; i < b; ++i) {
+        start[i] = run;
+        run += count[i];
+    }
+}
+
+// grid = (cells, groups): write the cell's candidate indices (group-relative, ascending)
+__global__ __launch_bounds__(kBlock) void k_demo_index_fill(const double2* __restrict__ demo,
+                                                            const int64_t* __restrict__ off,
+                                                            int64_t m_shared,
+                                                            const double* __restrict__ bound,
+                                                            const int64_t* __restrict__ start,
+                                                            int32_t* __restrict__ cand) {
+    __shared__ int wcnt[kBlock / 64];
+    __shared__ int64_t base;
+    const int cell = blockIdx.x, g = blockIdx.y;
+    const int64_t lo = off ? off[g] : 0, hi = off ? off[g + 1] : m_shared;
+    const double lx = (double)(cell / NAV_WORLD_CELLS), ly = (double)(cell % NAV_WORLD_CELLS);
+    const int64_t k = (int64_t)g * kCells + cell;
+    const double lim = bound[k];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (threadIdx.x == 0) base = start[k];
+    __syncthreads();
+    for (int64_t j0 = lo; j0 < hi; j0 += kBlock) {
+        const int64_t j = j0 + threadIdx.x;
+        bool take = false;
+        if (j < hi) {
+            const double2 q = demo[j];
+            take = cell_mind2(q.x, q.y, lx, ly) <= lim;
+        }
+        const unsigned long long bal = __ballot(take);
+        const int before = __popcll(bal & ((1ull << lane) - 1ull));
+        if (lane == 0) wcnt[wv] = __popcll(bal);
+        __syncthreads();
+        int wbase = 0, tot = 0;
+        for (int w = 0; w < kBlock / 64; ++w) {
+            if (w < wv) wbase += wcnt[w];
+            tot += wcnt[w];
+        }
+        if (take) cand[base + wbase + before] = (int32_t)(j - lo);
+        __syncthreads();
+        if (threadIdx.x == 0) base += tot;
+        __syncthreads();
+    }
+}
+
+// The demo-proximity term through the index: lane = env, its cell = the dynamics cell of s'.
+__global__ __launch_bounds__(kBlock) void k_demo_reward_idx(nav_params p, int64_t n,
+                                                            const double2* __restrict__ ns,
+                                                            const double* __restrict__ gterm,
+                                                            const uint8_t* __restrict__ flags,
+                                                            const double2* __restrict__ demo,
+                                                            const int64_t* __restrict__ off,
+                                                            int32_t epg,
+                                                            const int64_t* __restrict__ start,
+                                                            const int32_t* __restrict__ cand,
+                                                            float* __restrict__ rows,
+                                                            int64_t cap, int64_t base,
+                                                            double* __restrict__ reward_out) {
+    const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (e >= n) return;
+    const uint8_t f = flags[e];
+    if (!(f & F_DEMO)) return;
+    const double2 s = ns[e];
+    const int64_t g = off ? e / epg : 0;
+    const double2* pts = demo + (off ? off[g] : 0);
+    double best = __builtin_inf();
+    if (s.x >= 0.0 && s.x < 100.0 && s.y >= 0.0 && s.y < 100.0) {
+        const int64_t k = g * kCells + (int64_t)((int)s.x * NAV_WORLD_CELLS + (int)s.y);
+        const int64_t a = start[k], b = start[k + 1];
+        int64_t j = a;
+        double b1 = __builtin_inf();
+        for (; j + 1 < b; j += 2) {
+            const double2 q0 = pts[cand[j]], q1 = pts[cand[j + 1]];
+            best = fmin(best, sqd(s.x, s.y, q0.x, q0.y));
+            b1 = fmin(b1, sqd(s.x, s.y, q1.x, q1.y));
+        }
+        if (j < b) {
+            const double2 q0 = pts[cand[j]];
+            best = fmin(best, sqd(s.x, s.y, q0.x, q0.y));
+        }
+        best = fmin(best, b1);
+    } else {  // outside the indexed cells: brute force
+        best = demo_min_global(pts, (off ? off[g + 1] - off[g] : 0), s.x, s.y);
+    }
+    const double mn = sqrt(best);
+    double r = gterm[e] + p.demo_factor * (-mn);
+    if (f & F_STUCK) r -= p.stuck_penalty;
+    const int64_t slot = (base + e) % cap;
+    rows[slot * NAV_ROW + 4] = (float)r;
+    if (reward_out) reward_out[e] = r;
+}
+
 __global__ __launch_bounds__(kBlock) void k_compute_reward(nav_params p, int64_t n,
                                                            const double2* __restrict__ ns,
                                                            const double2* __restrict__ goal,
@@ -649,6 +831,61 @@ int nav_demo_min(const double* points, int64_t n, const double* demo_xy, int64_t
     hipLaunchKernelGGL(k_demo_min, dim3(blocks_for(n)), dim3(kBlock), 0, S(stream),
                        reinterpret_cast<const double2*>(points), n,
                        reinterpret_cast<const double2*>(demo_xy), m, out);
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_demo_index_plan(const double* demo_xy, const int64_t* demo_off, int32_t n_groups,
+                        int64_t m, double* cell_bound, int32_t* cell_count, void* stream) {
+    if (!demo_xy || n_groups < 1 || (!demo_off && (n_groups != 1 || m < 1)) || !cell_bound ||
+        !cell_count)
+        return NAV_EINVAL;
+    hipLaunchKernelGGL(k_demo_index_plan, dim3(kCells, n_groups), dim3(kBlock), 0, S(stream),
+                       reinterpret_cast<const double2*>(demo_xy), demo_off, m, cell_bound,
+                       cell_count);
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_demo_index_scan(const int32_t* cell_count, int32_t n_groups, int64_t* cell_start,
+                        void* stream) {
+    if (!cell_count || !cell_start || n_groups < 1) return NAV_EINVAL;
+    hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(kBlock), 0, S(stream), cell_count,
+                       (int64_t)n_groups * kCells, cell_start);
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_demo_index_fill(const double* demo_xy, const int64_t* demo_off, int32_t n_groups,
+                        int64_t m, const double* cell_bound, const int64_t* cell_start,
+                        int32_t* cand, void* stream) {
+    if (!demo_xy || n_groups < 1 || (!demo_off && n_groups != 1) || !cell_bound ||
+        !cell_start || !cand)
+        return NAV_EINVAL;
+    hipLaunchKernelGGL(k_demo_index_fill, dim3(kCells, n_groups), dim3(kBlock), 0, S(stream),
+                       reinterpret_cast<const double2*>(demo_xy), demo_off, m, cell_bound,
+                       cell_start, cand);
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_demo_reward_indexed(const nav_params* p, int64_t n, const double* next_state,
+                            const double* goal_term, const uint8_t* flags, const double* demo_xy,
+                            const int64_t* demo_off, int32_t envs_per_group,
+                            const int64_t* cell_start, const int32_t* cand,
+                            const nav_replay* replay, int64_t replay_base, double* reward_out,
+                            void* stream) {
+    if (!p || n < 0 || !replay || !replay->rows || replay->capacity <= 0 || replay_base < 0 ||
+        (demo_off && envs_per_group <= 0))
+        return NAV_EINVAL;
+    if (n == 0) return 0;
+    if (!next_state || !goal_term || !flags || !demo_xy || !cell_start || !cand)
+        return NAV_EINVAL;
+    hipLaunchKernelGGL(k_demo_reward_idx, dim3(blocks_for(n)), dim3(kBlock), 0, S(stream), *p,
+                       n, reinterpret_cast<const double2*>(next_state), goal_term, flags,
+                       reinterpret_cast<const double2*>(demo_xy), demo_off,
+                       envs_per_group > 0 ? envs_per_group : 1, cell_start, cand, replay->rows,
+                       replay->capacity, replay_base % replay->capacity, reward_out);
     NAV_CHECK_LAUNCH();
     return 0;
 }

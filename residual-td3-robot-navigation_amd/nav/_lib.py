@@ -74,6 +74,12 @@ SIGNATURES = [
     ("nav_rollout", C.c_int, [_vp, C.c_int64, C.c_int32, _vp, _vp, _vp, _vp, _vp, _vp]),
     ("nav_replay_push", C.c_int, [_P(NavReplay), C.c_int64, C.c_int64, _vp, _vp, _vp, _vp, _vp,
                                   _vp]),
+    ("nav_demo_index_plan", C.c_int, [_vp, _vp, C.c_int32, C.c_int64, _vp, _vp, _vp]),
+    ("nav_demo_index_scan", C.c_int, [_vp, C.c_int32, _vp, _vp]),
+    ("nav_demo_index_fill", C.c_int, [_vp, _vp, C.c_int32, C.c_int64, _vp, _vp, _vp, _vp]),
+    ("nav_demo_reward_indexed", C.c_int, [_P(NavParams), C.c_int64, _vp, _vp, _vp, _vp, _vp,
+                                          C.c_int32, _vp, _vp, _P(NavReplay), C.c_int64, _vp,
+                                          _vp]),
     ("nav_demo_min", C.c_int, [_vp, C.c_int64, _vp, C.c_int64, _vp, _vp]),
     ("nav_compute_reward", C.c_int, [_P(NavParams), C.c_int64, _vp, _vp, _vp, C.c_int64,
                                      C.c_int32, _vp, _vp, _vp]),

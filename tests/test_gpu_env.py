@@ -235,6 +235,38 @@ def test_agent_step_replays_reference_trace(nav):
     assert n_checked > 300
 
 
+def test_demo_index_bit_exact_vs_brute_force(nav, orc):
+    """The bucketed demo index returns the brute-force minimum bit for bit (same f64 values)."""
+    from nav.vec_env import DemoIndex, ReplayRing, VecEnv
+    t = golden("trace.npz")
+    demo = t["demo_set"]
+    n, epg = 4096, 1024
+    G = n // epg
+    pts = np.concatenate([demo + 3.0 * k for k in range(G)])
+    off = np.arange(G + 1, dtype=np.int64) * len(demo)
+    rng = np.random.default_rng(9)
+    rewards = []
+    for use_index in (True, False):
+        env = VecEnv(n, field_of(t["speed"], t["angle"]), seed=5, envs_per_group=epg)
+        env.set_demo(pts, off, index=use_index)
+        s = rng.uniform(0, 99, (n, 2))
+        s[:512] = np.floor(s[:512])  # exactly on cell corners
+        s[512:1024] = demo[rng.integers(0, len(demo), 512)].clip(0, 98.99)  # on demo points
+        rng = np.random.default_rng(9)  # same states for both passes
+        env.state.copy_(torch.tensor(s))
+        rep = ReplayRing(n, DEV)
+        r = torch.zeros(n, dtype=torch.float64, device=DEV)
+        env.agent_step(torch.zeros(n, 2, dtype=torch.float64, device=DEV), rep, reward_out=r)
+        rewards.append((r.cpu().numpy(), env.flags.cpu().numpy()))
+        if use_index:
+            assert env.demo_index.mean_candidates < 200
+    (ri, fi), (rb, fb) = rewards
+    assert np.array_equal(fi, fb)
+    m = (fi & 16) != 0
+    assert m.sum() > n // 2
+    assert np.array_equal(ri[m], rb[m])
+
+
 def test_compute_reward_kernel_vs_oracle(nav, orc):
     from nav._lib import lib, params_struct, ptr, stream_handle
     t = golden("trace.npz")
