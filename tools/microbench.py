@@ -85,9 +85,22 @@ def main():
     m_per = tr.env.demo_xy.shape[0] / (tr.env.demo_off.shape[0] - 1)
     res["agent_step"] = {"us": sm["agent_step"]["avg_us"],
                          "GBs": prof.AGENT_STEP_BYTES * args.envs / sm["agent_step"]["avg_us"] / 1e3}
-    res["demo_reward"] = {"us": sm["demo_reward"]["avg_us"],
-                          "f64_TFs": prof.demo_flops(args.envs, m_per) /
-                          sm["demo_reward"]["avg_us"] / 1e6}
+    ix = tr.env.demo_index
+    res["demo_reward_indexed"] = {"us": sm["demo_reward"]["avg_us"],
+                                  "mean_candidates": ix.mean_candidates if ix else None}
+    ix_saved, tr.env.demo_index = tr.env.demo_index, None
+    t = prof.KernelTimer()
+    with prof.timing(t):
+        for _ in range(10):
+            tr.collect()
+    sm = t.summary()
+    res["demo_reward_brute"] = {"us": sm["demo_reward"]["avg_us"],
+                                "f64_TFs": prof.demo_flops(args.envs, m_per) /
+                                sm["demo_reward"]["avg_us"] / 1e6}
+    from nav.vec_env import DemoIndex
+    us = timeit(lambda: DemoIndex(tr.env.demo_xy, tr.env.demo_off))
+    res["demo_index_build"] = {"us": us}
+    tr.env.demo_index = ix_saved
     # host cost of issuing one full training step vs its GPU time
     import time
     tr2 = VecTrainer(n_envs=args.envs, hidden=H, n_hidden=L, batch=B, updates_per_step=2,
