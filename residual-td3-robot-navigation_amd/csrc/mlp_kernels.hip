@@ -20,7 +20,7 @@ namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kMaxLayers = 9;
-constexpr int TM = 128;  // max rows per workgroup (row tiles of 32: RT = 1, 2 or 4)
+// workgroups hold RT row tiles of 32 rows (RT = 2 or 4; NAV_MLP_RT)
 
 struct MlpDev {
     const float* params;
@@ -67,11 +67,15 @@ NAV_DEV int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
 
 // Column tiles of a wave: wave w owns 32-column tiles t = w and w + 4 (when < NT) of every
 // 128-row block, for all 4 row tiles: acc[rt][j] is the 32x32 tile (rows rt*32.., cols t_j*32..).
+// Wave index as a scalar: the compiler then treats per-wave tile ownership as uniform control
+// flow (s_cbranch) instead of exec-masked vector branches with pointer selects.
+NAV_DEV int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
 template <int NT>
 struct WaveCols {
     int t0, t1;
     bool has0, has1;
-    NAV_DEV WaveCols(int wv) : t0(wv), t1(wv + 4), has0(wv < NT), has1(wv + 4 < NT) {}
+    NAV_DEV WaveCols(int wv) : t0(wv), t1(wv + 4), has0(NT >= 4 || wv < NT), has1(NT >= 8 || wv + 4 < NT) {}
 };
 
 // acc[rt][j] = A[128 rows][hp] (LDS, row stride S_) x B[hp][tile t_j], B from a packed image in
@@ -84,7 +88,7 @@ NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const float* __restr
                        f32x16 (&acc)[RT][2]) {
     constexpr int hp = NT * 32;
     constexpr int nq = hp / 8;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
+    const int lane = threadIdx.x & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
     const WaveCols<NT> wc(wv);
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt)
@@ -92,26 +96,37 @@ NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const float* __restr
         for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int i = 0; i < 16; ++i) acc[rt][j][i] = 0.f;
-    if (!wc.has0) return;
+    if (!wc.has0) return;  // wave-uniform (scalar) branch
+    // A wave without a second tile re-reads its first tile's B (same cache lines) so every load
+    // is unconditional; its second-tile MFMAs are skipped by a scalar branch.
+    const int t1 = wc.has1 ? wc.t1 : wc.t0;
     const float4* B0 = reinterpret_cast<const float4*>(Bp) + (size_t)h * hp + wc.t0 * 32 + l32;
-    const float4* B1 = reinterpret_cast<const float4*>(Bp) + (size_t)h * hp + wc.t1 * 32 + l32;
+    const float4* B1 = reinterpret_cast<const float4*>(Bp) + (size_t)h * hp + t1 * 32 + l32;
     constexpr size_t STEP = 2 * (size_t)hp;  // float4 per 8-deep K step
-    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    float4 p0 = B0[0], p1 = nq > 1 ? B0[STEP] : z4;
-    float4 r0 = wc.has1 ? B1[0] : z4, r1 = (wc.has1 && nq > 1) ? B1[STEP] : z4;
+    constexpr size_t S1 = nq > 1 ? STEP : 0;
+    float4 p0 = B0[0], p1 = B0[S1];
+    float4 r0 = B1[0], r1 = B1[S1];
     const float* arow = A + l32 * S_ + 4 * h;
+    float4 a[RT], an[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) a[rt] = *reinterpret_cast<const float4*>(arow + rt * 32 * S_);
+#pragma unroll
     for (int q = 0; q < nq; ++q) {
         const float4 c0 = p0, c1 = r0;
         p0 = p1;
         r0 = r1;
+        // issue step q+2's B (L2) and step q+1's A (LDS) before step q's MFMAs; the scheduling
+        // fences keep the compiler from sinking the loads next to their uses
         if (q + 2 < nq) {
             p1 = B0[(q + 2) * STEP];
-            if (wc.has1) r1 = B1[(q + 2) * STEP];
+            r1 = B1[(q + 2) * STEP];
         }
-        float4 a[RT];
+        if (q + 1 < nq) {
 #pragma unroll
-        for (int rt = 0; rt < RT; ++rt)
-            a[rt] = *reinterpret_cast<const float4*>(arow + rt * 32 * S_ + 8 * q);
+            for (int rt = 0; rt < RT; ++rt)
+                an[rt] = *reinterpret_cast<const float4*>(arow + rt * 32 * S_ + 8 * (q + 1));
+        }
+        __builtin_amdgcn_sched_barrier(0);
 #define NAV_MF(S, C)                                                                     \
     _Pragma("unroll") for (int rt = 0; rt < RT; ++rt) {                                 \
         acc[rt][0] = mfma(a[rt].S, c0.S, acc[rt][0]);                                   \
@@ -119,6 +134,9 @@ NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const float* __restr
     }
         NAV_MF(x, 0) NAV_MF(y, 1) NAV_MF(z, 2) NAV_MF(w, 3)
 #undef NAV_MF
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) a[rt] = an[rt];
     }
 }
 
@@ -156,7 +174,10 @@ struct FwdArgs {
     double* action_out;
 };
 
-inline size_t lds_bytes(int hp, int tm) { return ((size_t)tm * (hp + 4) + tm * 4) * 4; }
+// rows [tm][hp+4] + input/dy staging [tm][4] + output-layer partial sums [2][kBlock]
+inline size_t lds_bytes(int hp, int tm) {
+    return ((size_t)tm * (hp + 4) + tm * 4 + 2 * kBlock) * 4;
+}
 
 // Mask image row-tile count: independent of the workgroup height, so any RT reads what any RT
 // wrote (row tile = global row / 32; layers strided by ceil(M/128)*4 tiles).
@@ -166,7 +187,7 @@ __host__ __device__ inline int64_t mask_rowtiles(int64_t M) { return ((M + 127) 
 // mask bits. Global copies of the rows are written afterwards by copy_rows (coalesced).
 template <int NT, int RT>
 NAV_DEV void store_layer(f32x16 (&acc)[RT][2], float* act, int S_, uint16_t* mask, int64_t rt0) {
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
+    const int lane = threadIdx.x & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
     const WaveCols<NT> wc(wv);
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -203,7 +224,7 @@ template <int NT, int RT, int IN_MODE, int OUT_MODE>
 __global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     constexpr int hp = NT * 32, SS = hp + 4, TM = RT * 32;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, l32 = lane & 31;
+    const int tid = threadIdx.x, lane = tid & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
     const MlpDev& net = a.net[blockIdx.y];
     float* act_save = a.acts[blockIdx.y];
     uint16_t* masks = a.masks[blockIdx.y];
@@ -257,10 +278,16 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
 #pragma unroll 1
             for (int rt = 0; rt < RT; ++rt) {
                 uint32_t bits = 0;
+                // all 16 input rows first: the LDS stores below may alias them for the compiler,
+                // which would otherwise wait on every read
+                float4 xs[16];
+#pragma unroll
+                for (int i = 0; i < 16; ++i)
+                    xs[i] = *reinterpret_cast<const float4*>(xr + (rt * 32 + (i & 3) + 8 * (i >> 2)) * 4);
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
                     const int ro = rt * 32 + (i & 3) + 8 * (i >> 2);
-                    const float4 x = *reinterpret_cast<const float4*>(xr + ro * 4);
+                    const float4 x = xs[i];
                     float v = b;
                     v = fmaf(x.x, w[0], v);
                     v = fmaf(x.y, w[1], v);
@@ -298,29 +325,43 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
         if (act_save) copy_rows<NT, RT>(act, SS, act_save + (int64_t)L * M * hp, row0, M);
     }
 
-    // ---- output layer (N = d_out <= 2) on the VALU: thread = (row, output)
+    // ---- output layer (N = d_out <= 2) on the VALU: every thread takes one row and one K slice
+    // of hp / PARTS; the slices' partial sums meet in LDS and add up in a fixed order
+    {
+        constexpr int PARTS = kBlock / TM, KP = hp / PARTS;
+        const int rl = tid % TM, part = tid / TM;
+        const float* ar = act + rl * SS + part * KP;
+        const float* Wo = net.params + net.w_off[nh] + part * KP;
+        float s0 = 0.f, s1 = 0.f;
+#pragma unroll 4
+        for (int k = 0; k < KP; k += 4) {
+            const float4 x = *reinterpret_cast<const float4*>(ar + k);
+            const float4 w0 = *reinterpret_cast<const float4*>(Wo + k);
+            s0 = fmaf(x.x, w0.x, s0); s0 = fmaf(x.y, w0.y, s0);
+            s0 = fmaf(x.z, w0.z, s0); s0 = fmaf(x.w, w0.w, s0);
+            if (d_out > 1) {
+                const float4 w1 = *reinterpret_cast<const float4*>(Wo + hp + k);
+                s1 = fmaf(x.x, w1.x, s1); s1 = fmaf(x.y, w1.y, s1);
+                s1 = fmaf(x.z, w1.z, s1); s1 = fmaf(x.w, w1.w, s1);
+            }
+        }
+        float* red = xin + TM * 4;  // [2][PARTS][TM]
+        red[part * TM + rl] = s0;
+        red[(PARTS + part) * TM + rl] = s1;
+    }
+    __syncthreads();
     const int rloc = tid % TM;
     const int j = tid / TM;
     const int64_t r = row0 + rloc;
-    float y = 0.f;
-    if (j < d_out) {
-        const float* Wo = net.params + net.w_off[nh] + j * hp;
-        const float* ar = act + rloc * SS;
-        float acc0 = 0.f, acc1 = 0.f;
-#pragma unroll 4
-        for (int k = 0; k < hp; k += 8) {
-            const float4 x0 = *reinterpret_cast<const float4*>(ar + k);
-            const float4 x1 = *reinterpret_cast<const float4*>(ar + k + 4);
-            const float4 w0 = *reinterpret_cast<const float4*>(Wo + k);
-            const float4 w1 = *reinterpret_cast<const float4*>(Wo + k + 4);
-            acc0 = fmaf(x0.x, w0.x, acc0); acc0 = fmaf(x0.y, w0.y, acc0);
-            acc0 = fmaf(x0.z, w0.z, acc0); acc0 = fmaf(x0.w, w0.w, acc0);
-            acc1 = fmaf(x1.x, w1.x, acc1); acc1 = fmaf(x1.y, w1.y, acc1);
-            acc1 = fmaf(x1.z, w1.z, acc1); acc1 = fmaf(x1.w, w1.w, acc1);
-        }
-        y = (acc0 + acc1) + net.params[net.b_off[nh] + j];
-    }
     if (r >= M || j >= d_out) return;
+    float y = 0.f;
+    {
+        constexpr int PARTS = kBlock / TM;
+        const float* red = xin + TM * 4 + j * PARTS * TM + rloc;
+#pragma unroll
+        for (int p = 0; p < PARTS; ++p) y += red[p * TM];
+        y += net.params[net.b_off[nh] + j];
+    }
     if (OUT_MODE == OUT_F32) {
         a.out[blockIdx.y][r * a.ld_out + a.out_col + j] = y;
     } else if (OUT_MODE == OUT_TARGET) {
@@ -371,7 +412,7 @@ struct BwdArgs {
 template <int NT, int RT>
 NAV_DEV void mask_and_store(f32x16 (&acc)[RT][2], const uint16_t* mask, float* act, int S_,
                             int64_t rt0) {
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
+    const int lane = threadIdx.x & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
     const WaveCols<NT> wc(wv);
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -393,7 +434,7 @@ template <int NT, int RT>
 __global__ __launch_bounds__(kBlock, 1) void k_mlp_bwd(BwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     constexpr int hp = NT * 32, SS = hp + 4, TM = RT * 32;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, l32 = lane & 31;
+    const int tid = threadIdx.x, lane = tid & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
     const MlpDev& net = a.net;
     const int64_t M = a.M;
     const int64_t row0 = (int64_t)blockIdx.x * TM;
@@ -431,10 +472,14 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_bwd(BwdArgs a) {
 #pragma unroll 1
             for (int rt = 0; rt < RT; ++rt) {
                 const uint32_t bits = mk[mask_idx(rt0 + rt, NT, t, lane)];
+                float4 gs[16];
+#pragma unroll
+                for (int i = 0; i < 16; ++i)
+                    gs[i] = *reinterpret_cast<const float4*>(gr + (rt * 32 + (i & 3) + 8 * (i >> 2)) * 4);
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
                     const int ro = rt * 32 + (i & 3) + 8 * (i >> 2);
-                    const float4 g = *reinterpret_cast<const float4*>(gr + ro * 4);
+                    const float4 g = gs[i];
                     const float v = fmaf(g.y, w1, g.x * w0);
                     col[ro * SS] = (bits >> i) & 1u ? v : 0.f;
                 }
@@ -527,7 +572,7 @@ __global__ __launch_bounds__(kBlock) void k_wgrad(WgradArgs a) {
     } else {
         Q = a.acts + (int64_t)(nh - 1) * MH;
     }
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, l32 = lane & 31;
+    const int tid = threadIdx.x, lane = tid & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
     const int nloc = 32 * (wv >> 1), kloc = 32 * (wv & 1);
     const int64_t per = (a.M + a.splits - 1) / a.splits;
     const int64_t m_lo = (int64_t)blockIdx.y * per;
