@@ -525,80 +525,197 @@ struct WgradArgs {
     const float* dy;
     float* slabs;
     int splits;
-    int T;        // 64-wide tiles across hp
-    int n_hid;    // jobs of kind A = (nh - 1) * T * T
+    int T;        // 64-wide column panels across hp (edge kinds)
+    int TA;       // 128-wide tiles across hp (hidden kind)
+    int n_hid;    // hidden-kind jobs = (nh - 1) * TA * TA
 };
 
-constexpr int WG_MC = 32;   // rows per staged chunk
-constexpr int WG_LD = 68;   // LDS row stride of the staged 64-column panels
+constexpr int WG_MC = 32;    // rows per staged chunk
+constexpr int WG_LD = 68;    // LDS row stride of the staged 64-column panels (edge kinds)
+constexpr int WA_W = 128;    // hidden-kind tile width
+constexpr int WA_LD = 132;   // LDS row stride of its 128-column panels
 
-// One launch computes every parameter gradient of a network for one row split (grid.y):
-//  kind A (hidden x hidden layer L, 64x64 tile): dW_L = dz_L^T act_{L-1} on MFMA, plus
-//          db_L = column sums of dz_L on the VALU in the tk == 0 tiles;
-//  kind B (layer 0, 64 columns of dz_0): dW_0 = dz_0^T x and db_0 on the VALU (K = d_in);
-//  kind C (output layer, 64 columns of act_top): dW_o = dy^T act_top and db_o on the VALU.
-// All kinds stage 32-row chunks of 64-column panels through LDS (double-buffered).
-__global__ __launch_bounds__(kBlock) void k_wgrad(WgradArgs a) {
-    __shared__ __attribute__((aligned(16))) float pa[2][WG_MC][WG_LD];
-    __shared__ __attribute__((aligned(16))) float pb[2][WG_MC][WG_LD];
-    __shared__ __attribute__((aligned(16))) float sm[2][WG_MC][4];
-    __shared__ float red[4][64][6];
+inline size_t wgrad_lds_bytes() {
+    const size_t hid = (2 * 2 * WG_MC * WA_LD + 2 * WA_W) * 4;
+    const size_t edge = (2 * 2 * WG_MC * WG_LD + 2 * WG_MC * 4 + 4 * 64 * 6) * 4;
+    return hid > edge ? hid : edge;
+}
+
+// v if c else 0, per component (a float4-wide select would be lowered through the stack)
+NAV_DEV float4 sel4(bool c, float4 v) {
+    return make_float4(c ? v.x : 0.f, c ? v.y : 0.f, c ? v.z : 0.f, c ? v.w : 0.f);
+}
+
+// Hidden x hidden layer L, one 128x128 tile (tn, tk) of dW_L = dz_L^T act_{L-1} over the rows of
+// one split: the 4 waves own 64x64 quadrants (2x2 v_mfma_f32_32x32x2_f32 tiles each; the MFMA K
+// dimension is the row index). 32-row chunks of the two 128-column panels are double-buffered in
+// LDS with the next chunk's global loads in flight during the current chunk's MFMAs. Tiles with
+// tk == 0 also produce db_L = column sums of dz_L.
+template <bool FULL>
+NAV_DEV void wgrad_hidden(const WgradArgs& a, int job, int split, float* smem) {
+    const MlpDev& net = a.net;
+    const int hp = net.hp, TA = a.TA;
+    const int L = job / (TA * TA) + 1;
+    const int tn = (job % (TA * TA)) / TA, tk = job % TA;
+    const int n0 = tn * WA_W, k0 = tk * WA_W;
+    const int64_t MH = a.M * hp;
+    const float* P = a.dz + (int64_t)L * MH;
+    const float* Q = a.acts + (int64_t)(L - 1) * MH;
+    float* Ps = smem;                          // [2][32][WA_LD]
+    float* Qs = smem + 2 * WG_MC * WA_LD;      // [2][32][WA_LD]
+    float* red = smem + 4 * WG_MC * WA_LD;     // [2][128]
+    const int tid = threadIdx.x, lane = tid & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
+    const int wn = 64 * (wv >> 1), wk = 64 * (wv & 1);
+    // 32x32 sub-tiles inside hp (wave-uniform)
+    const bool n0k = n0 + wn < hp, n1k = n0 + wn + 32 < hp;
+    const bool k0k = k0 + wk < hp, k1k = k0 + wk + 32 < hp;
+    const int64_t per = (a.M + a.splits - 1) / a.splits;
+    const int64_t m_lo = (int64_t)split * per;
+    const int64_t m_hi = m_lo + per < a.M ? m_lo + per : a.M;
+    const bool colsum = tk == 0;
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+    float cs = 0.f;  // column sum: thread = (column tid & 127, row parity tid >> 7)
+    // staging: thread loads float4 (row rr, columns 4*c4..) for rr = (tid >> 5) + 8 f
+    const int c4 = tid & 31, rr0 = tid >> 5;
+    // loads are unconditional from clamped (valid) addresses; out-of-range values are zeroed
+    // in registers, so no load sits behind a branch or a pointer select
+    const bool pc_ok = n0 + 4 * c4 < hp, qc_ok = k0 + 4 * c4 < hp;
+    const float* Pc = P + (pc_ok ? n0 + 4 * c4 : 0);
+    const float* Qc = Q + (qc_ok ? k0 + 4 * c4 : 0);
+    // (zeroing happens at store time, so nothing consumes the loads before the chunk's MFMAs)
+    auto load = [&](int64_t m0, float4 (&rp)[4], float4 (&rq)[4]) {
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+            const int64_t m = m0 + rr0 + 8 * f;
+            const int64_t mc = m < m_hi ? m : m_lo;
+            rp[f] = *reinterpret_cast<const float4*>(Pc + mc * hp);
+            rq[f] = *reinterpret_cast<const float4*>(Qc + mc * hp);
+        }
+    };
+    auto store = [&](int buf, int64_t m0, const float4 (&rp)[4], const float4 (&rq)[4]) {
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+            const int r = rr0 + 8 * f;
+            const bool ok = m0 + r < m_hi;
+            *reinterpret_cast<float4*>(Ps + (buf * WG_MC + r) * WA_LD + 4 * c4) =
+                sel4(ok && pc_ok, rp[f]);
+            *reinterpret_cast<float4*>(Qs + (buf * WG_MC + r) * WA_LD + 4 * c4) =
+                sel4(ok && qc_ok, rq[f]);
+        }
+    };
+    float4 rp[4], rq[4];
+    const int nch = (int)((m_hi - m_lo + WG_MC - 1) / WG_MC);
+    if (nch > 0) {
+        load(m_lo, rp, rq);
+        store(0, m_lo, rp, rq);
+    }
+    __syncthreads();
+    for (int c = 0; c < nch; ++c) {
+        if (c + 1 < nch) load(m_lo + (int64_t)(c + 1) * WG_MC, rp, rq);
+        const int buf = c & 1;
+        const float* pb = Ps + buf * WG_MC * WA_LD;
+        const float* qb = Qs + buf * WG_MC * WA_LD;
+        __builtin_amdgcn_sched_barrier(0);
+        if (FULL) {
+            // branch-free: step s+1's operands are read before step s's 4 MFMAs (fenced so
+            // the scheduler cannot sink the reads onto their uses)
+            const float* pw = pb + h * WA_LD + wn + l32;
+            const float* qw = qb + h * WA_LD + wk + l32;
+            float a0 = pw[0], a1 = pw[32], b0 = qw[0], b1 = qw[32];
+#pragma unroll
+            for (int s = 0; s < WG_MC / 2; ++s) {
+                float a0n = 0.f, a1n = 0.f, b0n = 0.f, b1n = 0.f;
+                if (s + 1 < WG_MC / 2) {
+                    const int o = 2 * (s + 1) * WA_LD;
+                    a0n = pw[o];
+                    a1n = pw[o + 32];
+                    b0n = qw[o];
+                    b1n = qw[o + 32];
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                acc[0][0] = mfma(a0, b0, acc[0][0]);
+                acc[0][1] = mfma(a0, b1, acc[0][1]);
+                acc[1][0] = mfma(a1, b0, acc[1][0]);
+                acc[1][1] = mfma(a1, b1, acc[1][1]);
+                __builtin_amdgcn_sched_barrier(0);
+                a0 = a0n; a1 = a1n; b0 = b0n; b1 = b1n;
+            }
+        } else {
+#pragma unroll
+            for (int s = 0; s < WG_MC / 2; ++s) {
+                const int row = 2 * s + h;
+                const float a0 = pb[row * WA_LD + wn + l32], a1 = pb[row * WA_LD + wn + 32 + l32];
+                const float b0 = qb[row * WA_LD + wk + l32], b1 = qb[row * WA_LD + wk + 32 + l32];
+                if (n0k && k0k) acc[0][0] = mfma(a0, b0, acc[0][0]);
+                if (n0k && k1k) acc[0][1] = mfma(a0, b1, acc[0][1]);
+                if (n1k && k0k) acc[1][0] = mfma(a1, b0, acc[1][0]);
+                if (n1k && k1k) acc[1][1] = mfma(a1, b1, acc[1][1]);
+            }
+        }
+        if (colsum) {
+#pragma unroll
+            for (int r = 0; r < WG_MC / 2; ++r) cs += pb[(2 * r + (tid >> 7)) * WA_LD + (tid & 127)];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (c + 1 < nch) store(buf ^ 1, m_lo + (int64_t)(c + 1) * WG_MC, rp, rq);
+        __syncthreads();
+    }
+    float* out = a.slabs + (int64_t)split * net.count;
+    float* o = out + net.w_off[L];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            if (!((i ? n1k : n0k) && (j ? k1k : k0k))) continue;
+            const int nb = n0 + wn + 32 * i, kb = k0 + wk + 32 * j;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) o[(int64_t)(nb + acc_row(e, h)) * hp + kb + l32] = acc[i][j][e];
+        }
+    if (!colsum) return;
+    red[tid] = cs;
+    __syncthreads();
+    if (tid < WA_W && n0 + tid < hp) out[net.b_off[L] + n0 + tid] = red[tid] + red[WA_W + tid];
+}
+
+// Edge layers, one 64-column panel per job (VALU, K = d_in or d_out):
+//  kind B (layer 0): dW_0 = dz_0^T x and db_0 = column sums of dz_0;
+//  kind C (output layer): dW_o = dy^T act_top and db_o = sums of dy.
+NAV_DEV void wgrad_edge(const WgradArgs& a, int job, int split, float* smem) {
+    typedef float Panel[WG_MC][WG_LD];
+    Panel* pa = reinterpret_cast<Panel*>(smem);                       // [2]
+    float (*sm)[WG_MC][4] = reinterpret_cast<float (*)[WG_MC][4]>(smem + 2 * WG_MC * WG_LD);
+    float (*red)[64][6] = reinterpret_cast<float (*)[64][6]>(smem + 2 * WG_MC * WG_LD +
+                                                              2 * WG_MC * 4);
     const MlpDev& net = a.net;
     const int hp = net.hp, T = a.T, nh = net.n_hidden;
-    const int job = blockIdx.x;
-    int kind, L = 0, tn = 0, tk = 0;
-    if (job < a.n_hid) {
-        kind = 0;
-        L = job / (T * T) + 1;
-        tn = (job % (T * T)) / T;
-        tk = job % T;
-    } else if (job < a.n_hid + T) {
-        kind = 1;
-        tn = job - a.n_hid;
-    } else {
-        kind = 2;
-        tk = job - a.n_hid - T;
-    }
+    const int kind = job < T ? 1 : 2;
+    const int tcol = kind == 1 ? job : job - T;
+    const int c0 = tcol * 64;
     const int64_t MH = a.M * hp;
-    // P panel source (columns n0..n0+63) and Q panel source (columns k0..k0+63)
-    const float* P = nullptr;
-    const float* Q = nullptr;
-    const int n0 = tn * 64, k0 = tk * 64;
-    if (kind == 0) {
-        P = a.dz + (int64_t)L * MH;
-        Q = a.acts + (int64_t)(L - 1) * MH;
-    } else if (kind == 1) {
-        P = a.dz;
-    } else {
-        Q = a.acts + (int64_t)(nh - 1) * MH;
-    }
-    const int tid = threadIdx.x, lane = tid & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
-    const int nloc = 32 * (wv >> 1), kloc = 32 * (wv & 1);
+    const float* src = kind == 1 ? a.dz : a.acts + (int64_t)(nh - 1) * MH;
+    const int tid = threadIdx.x;
     const int64_t per = (a.M + a.splits - 1) / a.splits;
-    const int64_t m_lo = (int64_t)blockIdx.y * per;
+    const int64_t m_lo = (int64_t)split * per;
     const int64_t m_hi = m_lo + per < a.M ? m_lo + per : a.M;
     const int d_in = net.d_in, d_out = net.d_out;
-    const bool do_mfma = kind == 0 && (n0 + nloc) < hp && (k0 + kloc) < hp;
-    const bool do_colsum = kind == 1 || (kind == 0 && tk == 0);
-    f32x16 acc;
-    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-    // VALU accumulators: thread = (column c = tid & 63, row group g = tid >> 6: rows g, g+4, ..)
+    // thread = (column c = tid & 63, row group g = tid >> 6: rows g, g+4, ..)
     const int vc = tid & 63, vg = tid >> 6;
     float va[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-
-    auto load = [&](int64_t m0, float4 (&ra)[2], float4 (&rb)[2], float4& rs) {
+    auto load = [&](int64_t m0, float4 (&ra)[2], float4& rs) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const int i = tid + kBlock * j;
             const int rr = i >> 4, cc = (i & 15) * 4;
             const int64_t m = m0 + rr;
-            const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-            ra[j] = z;
-            rb[j] = z;
-            if (m < m_hi) {
-                if (P && n0 + cc < hp) ra[j] = *reinterpret_cast<const float4*>(P + m * hp + n0 + cc);
-                if (Q && k0 + cc < hp) rb[j] = *reinterpret_cast<const float4*>(Q + m * hp + k0 + cc);
-            }
+            ra[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (m < m_hi && c0 + cc < hp)
+                ra[j] = *reinterpret_cast<const float4*>(src + m * hp + c0 + cc);
         }
         rs = make_float4(0.f, 0.f, 0.f, 0.f);
         if (tid < WG_MC && m0 + tid < m_hi) {
@@ -609,37 +726,31 @@ __global__ __launch_bounds__(kBlock) void k_wgrad(WgradArgs a) {
                 if (d_in > 1) rs.y = x[1];
                 if (d_in > 2) rs.z = x[2];
                 if (d_in > 3) rs.w = x[3];
-            } else if (kind == 2) {
+            } else {
                 rs.x = a.dy[m * d_out];
                 if (d_out > 1) rs.y = a.dy[m * d_out + 1];
             }
         }
     };
-    auto store = [&](int buf, float4 (&ra)[2], float4 (&rb)[2], float4 rs) {
+    auto store = [&](int buf, float4 (&ra)[2], float4 rs) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const int i = tid + kBlock * j;
             const int rr = i >> 4, cc = (i & 15) * 4;
             *reinterpret_cast<float4*>(&pa[buf][rr][cc]) = ra[j];
-            *reinterpret_cast<float4*>(&pb[buf][rr][cc]) = rb[j];
         }
         if (tid < WG_MC) *reinterpret_cast<float4*>(&sm[buf][tid][0]) = rs;
     };
-    float4 ra[2], rb[2], rs;
+    float4 ra[2], rs;
     const int nch = (int)((m_hi - m_lo + WG_MC - 1) / WG_MC);
     if (nch > 0) {
-        load(m_lo, ra, rb, rs);
-        store(0, ra, rb, rs);
+        load(m_lo, ra, rs);
+        store(0, ra, rs);
     }
     __syncthreads();
     for (int c = 0; c < nch; ++c) {
-        if (c + 1 < nch) load(m_lo + (int64_t)(c + 1) * WG_MC, ra, rb, rs);
+        if (c + 1 < nch) load(m_lo + (int64_t)(c + 1) * WG_MC, ra, rs);
         const int buf = c & 1;
-        if (do_mfma) {
-#pragma unroll
-            for (int s = 0; s < WG_MC / 2; ++s)
-                acc = mfma(pa[buf][2 * s + h][nloc + l32], pb[buf][2 * s + h][kloc + l32], acc);
-        }
         if (kind == 1) {
 #pragma unroll
             for (int rr = vg; rr < WG_MC; rr += 4) {
@@ -651,75 +762,95 @@ __global__ __launch_bounds__(kBlock) void k_wgrad(WgradArgs a) {
                 va[3] = fmaf(g, x.w, va[3]);
                 va[4] += g;
             }
-        } else if (kind == 2) {
+        } else {
 #pragma unroll
             for (int rr = vg; rr < WG_MC; rr += 4) {
-                const float x = pb[buf][rr][vc];
+                const float x = pa[buf][rr][vc];
                 const float4 g = *reinterpret_cast<const float4*>(&sm[buf][rr][0]);
                 va[0] = fmaf(g.x, x, va[0]);
                 va[1] = fmaf(g.y, x, va[1]);
                 va[2] += g.x;
                 va[3] += g.y;
             }
-        } else if (do_colsum) {
-#pragma unroll
-            for (int rr = vg; rr < WG_MC; rr += 4) va[4] += pa[buf][rr][vc];
         }
-        if (c + 1 < nch) store(buf ^ 1, ra, rb, rs);
+        if (c + 1 < nch) store(buf ^ 1, ra, rs);
         __syncthreads();
     }
-    float* out = a.slabs + (int64_t)blockIdx.y * net.count;
-    if (do_mfma) {
-        const int nb = n0 + nloc, kb = k0 + kloc;
-        float* o = out + net.w_off[L];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) o[(int64_t)(nb + acc_row(i, h)) * hp + kb + l32] = acc[i];
-    }
-    if (kind == 0 && !do_colsum) return;
+    float* out = a.slabs + (int64_t)split * net.count;
     // reduce the 4 row groups of the VALU accumulators
 #pragma unroll
     for (int q = 0; q < 6; ++q) red[vg][vc][q] = va[q];
     __syncthreads();
-    if (tid < 64) {
-        float s[6];
+    if (tid >= 64) return;
+    float s[6];
 #pragma unroll
-        for (int q = 0; q < 6; ++q) s[q] = red[0][tid][q] + red[1][tid][q] + red[2][tid][q] +
-                                           red[3][tid][q];
-        if (kind == 0) {
-            const int n = n0 + tid;
-            if (n < hp) out[net.b_off[L] + n] = s[4];
-        } else if (kind == 1) {
-            const int n = n0 + tid;
-            if (n < hp) {
-                for (int k = 0; k < d_in; ++k) out[net.w_off[0] + n * d_in + k] = s[k];
-                out[net.b_off[0] + n] = s[4];
-            }
-        } else {
-            const int k = k0 + tid;
-            if (k < hp) {
-                out[net.w_off[nh] + k] = s[0];
-                if (d_out > 1) out[net.w_off[nh] + hp + k] = s[1];
-            }
-            if (tk == 0 && tid == 0) {
-                out[net.b_off[nh]] = s[2];
-                if (d_out > 1) out[net.b_off[nh] + 1] = s[3];
-            }
+    for (int q = 0; q < 6; ++q) s[q] = red[0][tid][q] + red[1][tid][q] + red[2][tid][q] + red[3][tid][q];
+    const int n = c0 + tid;
+    if (kind == 1) {
+        if (n < hp) {
+            for (int k = 0; k < d_in; ++k) out[net.w_off[0] + n * d_in + k] = s[k];
+            out[net.b_off[0] + n] = s[4];
+        }
+    } else {
+        if (n < hp) {
+            out[net.w_off[nh] + n] = s[0];
+            if (d_out > 1) out[net.w_off[nh] + hp + n] = s[1];
+        }
+        if (tcol == 0 && tid == 0) {
+            out[net.b_off[nh]] = s[2];
+            if (d_out > 1) out[net.b_off[nh] + 1] = s[3];
         }
     }
 }
 
+// One launch computes every parameter gradient of a network. The 1-D grid lists the hidden-layer
+// 128x128 MFMA tiles of every row split first, then the edge panels (T layer-0 + T output) of
+// every split: the dispatcher hands out the MFMA-bound blocks one per CU before the VALU/memory
+// bound edge blocks fill the second slots, so the two kinds share CUs instead of stacking up.
+__global__ __launch_bounds__(kBlock) void k_wgrad(WgradArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int b = blockIdx.x;
+    const int n_hid_blocks = a.n_hid * a.splits;
+    if (b < n_hid_blocks) {
+        const int job = b % a.n_hid, split = b / a.n_hid;
+        // tiles entirely inside hp take the branch-free MFMA body
+        const int TA = a.TA, t = job % (TA * TA);
+        const bool full = (t / TA + 1) * WA_W <= a.net.hp && (t % TA + 1) * WA_W <= a.net.hp;
+        if (full)
+            wgrad_hidden<true>(a, job, split, smem);
+        else
+            wgrad_hidden<false>(a, job, split, smem);
+    } else {
+        const int e = b - n_hid_blocks, ne = 2 * a.T;
+        wgrad_edge(a, e % ne, e / ne, smem);
+    }
+}
+
+// grad = sum of the split slabs, in a fixed order: block = 64 float4 columns x 4 split groups
+// (group g sums splits g, g+4, ..), the 4 group sums added in order through LDS.
 __global__ __launch_bounds__(kBlock) void k_grad_reduce(const float4* __restrict__ slabs,
                                                         int splits, int64_t n4,
                                                         float4* __restrict__ grad) {
-    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n4;
-         i += (int64_t)gridDim.x * kBlock) {
-        float4 s = slabs[i];
-        for (int k = 1; k < splits; ++k) {
+    __shared__ float4 part[4][64];
+    const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
+    const int64_t i = (int64_t)blockIdx.x * 64 + c;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (i < n4) {
+#pragma unroll 4
+        for (int k = g; k < splits; k += 4) {
             const float4 v = slabs[(int64_t)k * n4 + i];
             s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
         }
-        grad[i] = s;
     }
+    part[g][c] = s;
+    __syncthreads();
+    if (g != 0 || i >= n4) return;
+    float4 r = part[0][c];
+#pragma unroll
+    for (int q = 1; q < 4; ++q) {
+        r.x += part[q][c].x; r.y += part[q][c].y; r.z += part[q][c].z; r.w += part[q][c].w;
+    }
+    grad[i] = r;
 }
 
 // ---------------- optimizer / target update, refreshing the packed images ----------------
@@ -1075,8 +1206,13 @@ int nav_mlp_wgrad(const nav_mlp* net, int64_t M, const float* in, int32_t ld_in,
     a.slabs = slabs;
     a.splits = splits;
     a.T = (a.net.hp + 63) / 64;
-    a.n_hid = (a.net.n_hidden - 1) * a.T * a.T;
-    hipLaunchKernelGGL(k_wgrad, dim3(a.n_hid + 2 * a.T, splits), dim3(kBlock), 0, S(stream), a);
+    a.TA = (a.net.hp + WA_W - 1) / WA_W;
+    a.n_hid = (a.net.n_hidden - 1) * a.TA * a.TA;
+    const size_t lds = wgrad_lds_bytes();
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wgrad),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k_wgrad, dim3((unsigned)((a.n_hid + 2 * a.T) * splits)), dim3(kBlock), lds,
+                       S(stream), a);
     NAV_CHECK_LAUNCH();
     return 0;
 }
@@ -1086,7 +1222,7 @@ int nav_grad_reduce(const float* slabs, int32_t splits, int64_t count, float* gr
     if (!slabs || !grad || splits < 1 || count < 0 || (count & 3)) return NAV_EINVAL;
     if (count == 0) return 0;
     const int64_t n4 = count / 4;
-    hipLaunchKernelGGL(k_grad_reduce, dim3(grid_stride_blocks(n4)), dim3(kBlock), 0, S(stream),
+    hipLaunchKernelGGL(k_grad_reduce, dim3((unsigned)((n4 + 63) / 64)), dim3(kBlock), 0, S(stream),
                        reinterpret_cast<const float4*>(slabs), splits, n4,
                        reinterpret_cast<float4*>(grad));
     NAV_CHECK_LAUNCH();

@@ -87,7 +87,7 @@ class TD3:
         self.dx = f(B, 4)
         self.da = f(B, 2)
         self.loss_part = f((B + 255) // 256, 2)
-        self.splits = max(1, min(32, B // 1024))
+        self.splits = max(1, min(64, B // 512))
         cmax = max(self.actor_network.count, self.critic_network_1.count)
         self.slabs = f(self.splits, cmax)
         self.grad_a = f(self.actor_network.count)

@@ -27,6 +27,7 @@ for step in "$@"; do
          run pmc_write 900 rocprofv3 --pmc WRITE_SIZE -T -f csv -d gpurun_out/pmc_write -o run -- python bench.py --steps 4 --warmup 2 --no-cpu-baseline --no-sweep &&
          run pmc_step_fetch 600 rocprofv3 --pmc FETCH_SIZE -T -f csv -d gpurun_out/pmc_step_fetch -o run -- python bench.py --sweep-only 16777216 &&
          run pmc_step_write 600 rocprofv3 --pmc WRITE_SIZE -T -f csv -d gpurun_out/pmc_step_write -o run -- python bench.py --sweep-only 16777216 ;;
+    pmcmicro) run pmc_micro_a 900 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE -T -f csv -d gpurun_out/pmc_micro_a -o run -- python tools/microbench.py --quick ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

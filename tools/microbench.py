@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--layers", type=int, default=2)
     ap.add_argument("--batch", type=int, default=32768)
     ap.add_argument("--envs", type=int, default=65536)
+    ap.add_argument("--quick", action="store_true", help="MLP kernels only (for counter runs)")
     args = ap.parse_args()
     from nav import prof
     from nav._lib import lib, ptr, stream_handle
@@ -72,6 +73,15 @@ def main():
     grad = torch.zeros(crit[0].count, device=dev)
     us = timeit(lambda: lib().nav_grad_reduce(ptr(slabs), splits, crit[0].count, ptr(grad), s))
     res["grad_reduce"] = {"us": us, "GBs": 4 * (splits + 1) * crit[0].count / us / 1e3}
+    # edge layers alone: a one-hidden-layer net has no hidden x hidden gradient tile
+    e1 = DeviceMLP(4, 1, H, 1, dev).init_kaiming(g)
+    d1 = e1.desc()
+    us = timeit(lambda: lib().nav_mlp_wgrad(C.byref(d1), B, ptr(x), 4, 0, ptr(acts), ptr(dz),
+                                            ptr(dy), ptr(slabs), splits, s))
+    res["wgrad_edges_only"] = {"us": us}
+    if args.quick:
+        print(json.dumps(res), flush=True)
+        return
     # act + env tick + demo at the env count
     tr = VecTrainer(n_envs=args.envs, hidden=H, n_hidden=L, batch=B, updates_per_step=0,
                     device=dev)
@@ -115,7 +125,7 @@ def main():
     torch.cuda.synchronize()
     t2 = time.perf_counter()
     res["train_step"] = {"host_issue_us": (t1 - t0) * 1e5, "wall_us": (t2 - t0) * 1e5}
-    for splits in (16, 32, 64):
+    for splits in (32, 64, 128):
         sl = torch.zeros(splits, crit[0].count, device=dev)
         us_w = timeit(lambda: lib().nav_mlp_wgrad(C.byref(d), B, ptr(x), 4, 0, ptr(acts),
                                                   ptr(dz), ptr(dy), ptr(sl), splits, s))
