@@ -129,8 +129,10 @@ def test_td3_oracle_vs_reference():
         return x
 
     closs, aloss = ora.td3_update(sample, nz, int(g["epochs"]))
-    np.testing.assert_allclose(np.array(closs), g["critic_loss"], rtol=1e-5)
-    np.testing.assert_allclose(np.array(aloss), g["actor_loss"], rtol=1e-5)
+    # fp32 losses are means over the batch: torch-CPU's reduction order follows the host's vector
+    # ISA, and the fixture was written on another host (1.9e-5 relative seen on the actor loss)
+    np.testing.assert_allclose(np.array(closs), g["critic_loss"], rtol=1e-4)
+    np.testing.assert_allclose(np.array(aloss), g["actor_loss"], rtol=1e-4)
     for name, net in ora.networks().items():
         dig = param_digest(net)
         for k, (s, q, ix, v) in enumerate(dig):
