@@ -29,7 +29,7 @@ extern "C" {
 #define NAV_EINVAL (-100000)
 
 #define NAV_WORLD_CELLS 100 /* field = float32 [100][100][2] (speed, angle), x-major: cell cx*100+cy
-                              (environment.py:99-100 dynamics_speed / dynamics_angle interleaved) */
+                              (environment.py:20-21 dynamics_speed / dynamics_angle interleaved) */
 #define NAV_HIST 5          /* STUCK_STEPS, robot.py:40 */
 #define NAV_ROW 8           /* replay row: s0 s1 a0 a1 r s'0 s'1 done (float32) */
 
@@ -54,13 +54,13 @@ typedef struct nav_params {
     int32_t path_length0;    /* robot.py:28 PATH_LENGTH = 50 */
     int32_t path_increase;   /* robot.py:29 PATH_INCREASE = 20 */
     uint32_t seed_lo, seed_hi; /* configuration.py:26 RANDOM_SEED by default */
-    int32_t max_goal_draws;  /* cap on environment.py:131's rejection loop (default 65536) */
+    int32_t max_goal_draws;  /* cap on environment.py:52's rejection loop (default 65536) */
 } nav_params;
 
 /* Per-env state, structure-of-arrays, n envs (device). */
 typedef struct nav_env_soa {
     int64_t n;
-    double* state;        /* [n][2]  Environment.robot_state (environment.py:96)           */
+    double* state;        /* [n][2]  Environment.robot_state (environment.py:17)           */
     double* goal;         /* [n][2]  Environment.goal_state / Robot.goal_state              */
     double* region;       /* [n][4]  Environment.robot_init_region (left,right,bottom,top)  */
     double* hist;         /* [5][n][2] Robot.previous_states ring (robot.py:425, 509-538)   */
@@ -112,31 +112,31 @@ int64_t nav_mlp_packed_count(int32_t hidden_pad, int32_t n_hidden);
 int nav_mlp_layer_offsets(const nav_mlp* net, int32_t layer, int64_t* w_off, int64_t* b_off);
 
 /* ---- Environment (environment.py) ---- */
-/* environment.py:107-135 set_init_and_goal per env, Philox stream_id = env / envs_per_group (so a
+/* environment.py:28-56 set_init_and_goal per env, Philox stream_id = env / envs_per_group (so a
  * group shares region and goal); also initialises the Robot fields to their values at the first
  * training step after the demonstration phase (robot.py:443-489 trace: plan_index 5, path 50,
- * episodes 5, noise 1, demo_flag as given) and draws the first reset (environment.py:209-216).
+ * episodes 5, noise 1, demo_flag as given) and draws the first reset (environment.py:130-137).
  * draws_out (nullable) [n]: goal draws used, 0 = rejection cap hit. */
 int nav_env_init(const nav_params* p, const nav_env_soa* env, int32_t envs_per_group,
                  int32_t demo_flag, int32_t* draws_out, void* stream);
-/* environment.py:209-216 Environment.reset: state = low + (high-low)*u for envs with mask != 0
+/* environment.py:130-137 Environment.reset: state = low + (high-low)*u for envs with mask != 0
  * (mask NULL = all). u from `uniforms` [n][2] if given (e.g. the numpy stream of robot-learning.py:19,
  * for reference-stream parity) else Philox (NAV_TAG_RESET, episode = episodes[e]). */
 int nav_env_reset(const nav_params* p, const nav_env_soa* env, const uint8_t* mask,
                   const double* uniforms, void* stream);
-/* environment.py:201-206 Environment.step for n envs: state <- dynamics(state, action) when the
+/* environment.py:122-127 Environment.step for n envs: state <- dynamics(state, action) when the
  * result is inside the world. action [n][2] f64. next_state (nullable) receives the result. */
 int nav_env_step(const nav_params* p, const nav_env_soa* env, const float* field,
                  const double* action, double* next_state, void* stream);
-/* environment.py:177-198 Environment.dynamics, pure: out = f(state, action), n pairs. */
+/* environment.py:98-119 Environment.dynamics, pure: out = f(state, action), n pairs. */
 int nav_dynamics(const float* field, const double* state, const double* action, double* out,
                  int64_t n, void* stream);
 
 /* ---- Robot per-step (robot.py) ---- */
-/* One training tick for every env, fused: Environment.step (environment.py:201-206) ->
+/* One training tick for every env, fused: Environment.step (environment.py:122-127) ->
  * Robot.process_transition (robot.py:645-675: reward w/o demo term, check_if_stuck, done, push
  * to the replay row (replay_base + e) % capacity) -> next tick's end-of-episode check and
- * Robot.reset + Environment.reset (robot.py:479-506, environment.py:209-216). */
+ * Robot.reset + Environment.reset (robot.py:479-506, environment.py:130-137). */
 int nav_agent_step(const nav_params* p, const nav_env_soa* env, const float* field,
                    const double* action, const nav_replay* replay,
                    int64_t replay_base, const nav_step_out* out, void* stream);
@@ -188,8 +188,8 @@ int nav_compute_reward(const nav_params* p, int64_t n, const double* next_state,
                        double* reward, uint8_t* goal_hit, void* stream);
 
 /* Batched open-loop rollouts of Environment.dynamics (the CEM demonstrator's inner loop,
- * environment.py:230-244): P paths x T steps; start [P][2], actions [P][T][2] f64 ->
- * paths [P][T+1][2] f64; reward (nullable) [P] = -||f32(s_T) - goal|| (environment.py:261-262). */
+ * environment.py:151-165): P paths x T steps; start [P][2], actions [P][T][2] f64 ->
+ * paths [P][T+1][2] f64; reward (nullable) [P] = -||f32(s_T) - goal|| (environment.py:182-183). */
 int nav_rollout(const float* field, int64_t P, int32_t T, const double* start,
                 const double* actions, double* paths, const double* goal, double* reward,
                 void* stream);

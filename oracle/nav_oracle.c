@@ -16,7 +16,7 @@
 
 /* ======================= numpy legacy RandomState ======================= */
 /* numpy/random/src/mt19937 + legacy distributions (numpy 2.2.6): the RNG under every draw the
- * reference makes (environment.py:108-132, 215, 236-238; robot.py:111, 640, 802-815). */
+ * reference makes (environment.py:29-53, 136, 157-159; robot.py:111, 640, 802-815). */
 #define MT_N 624
 #define MT_M 397
 
@@ -144,7 +144,7 @@ static int cell_of(double v) {
 
 void orc_dynamics(const float* speed, const float* angle, const double* s, const double* a_in,
                   double* out) {
-    /* environment.py:177-198 */
+    /* environment.py:98-119 */
     double a0 = clipd(a_in[0], -5.0, 5.0), a1 = clipd(a_in[1], -5.0, 5.0);
     double mag = orc_norm2(a0, a1);
     double ang = atan2(a1, a0);
@@ -161,7 +161,7 @@ void orc_dynamics(const float* speed, const float* angle, const double* s, const
 }
 
 int orc_step(const float* speed, const float* angle, double* s, const double* a) {
-    /* environment.py:201-206: commit only inside the world (fails only for NaN after the clip) */
+    /* environment.py:122-127: commit only inside the world (fails only for NaN after the clip) */
     double n[2];
     orc_dynamics(speed, angle, s, a, n);
     if (0.0 <= n[0] && n[0] < 100.0 && 0.0 <= n[1] && n[1] < 100.0) {
@@ -173,7 +173,7 @@ int orc_step(const float* speed, const float* angle, double* s, const double* a)
 }
 
 void orc_reset_u(const double* region, double u0, double u1, double* out) {
-    /* environment.py:214-216: uniform([l, b], [r, t]) = low + (high - low) * u */
+    /* environment.py:135-137: uniform([l, b], [r, t]) = low + (high - low) * u */
     out[0] = region[0] + (region[1] - region[0]) * u0;
     out[1] = region[2] + (region[3] - region[2]) * u1;
 }
@@ -185,7 +185,7 @@ void orc_reset_mt(orc_mt_t* rs, const double* region, double* out) {
 }
 
 static void region_of(int r, double u, double* region) {
-    /* environment.py:108-128; region = (left, right, bottom, top) */
+    /* environment.py:29-49; region = (left, right, bottom, top) */
     const double W = 100.0, S = 25.0;
     double l, rr, b, t;
     double v = 0.0 + (W - S - 0.0) * u;
@@ -197,7 +197,7 @@ static void region_of(int r, double u, double* region) {
 }
 
 int orc_init_and_goal_mt(orc_mt_t* rs, double* region, double* goal, int* side) {
-    /* environment.py:107-135 */
+    /* environment.py:28-56 */
     int r = (int)orc_mt_randint(rs, 0, 4);
     double u = orc_mt_double(rs);
     region_of(r, u, region);
@@ -348,7 +348,7 @@ int orc_vec_agent_tick(const orc_params_t* p, const float* speed, const float* a
     int cnt = (int)((mt >> 8) & 7u), head = (int)((mt >> 12) & 7u);
 
     double s[2] = {state[0], state[1]}, ns[2] = {state[0], state[1]};
-    orc_step(speed, angle, ns, action); /* environment.py:201-206 */
+    orc_step(speed, angle, ns, action); /* environment.py:122-127 */
 
     /* robot.py:645-675 process_transition */
     double r = orc_compute_reward(ns, goal, demo, m, demo_flag, &goal_reached, p->goal_threshold,
@@ -369,7 +369,7 @@ int orc_vec_agent_tick(const orc_params_t* p, const float* speed, const float* a
     if (reward_out) *reward_out = r;
 
     /* the next tick's get_next_action_type (robot.py:479-487) + Robot.reset (robot.py:492-506)
-     * + Environment.reset (environment.py:209-211), fused: the reset tick takes no env step. */
+     * + Environment.reset (environment.py:130-132), fused: the reset tick takes no env step. */
     int ended = done || goal_reached || stuck_flag;
     int flags = (done ? 1 : 0) | (goal_reached ? 2 : 0) | (stuck ? 4 : 0) | (ended ? 8 : 0);
     if (ended) {

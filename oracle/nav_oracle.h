@@ -43,16 +43,16 @@ void   orc_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4])
 double orc_u01(uint32_t hi, uint32_t lo);         /* 53-bit double from two words, numpy formula */
 
 /* ---------------- Environment (environment.py) ---------------- */
-/* environment.py:177-198. fields are [100][100] float32, x-major (index cx*100+cy). */
+/* environment.py:98-119. fields are [100][100] float32, x-major (index cx*100+cy). */
 void orc_dynamics(const float* speed, const float* angle, const double* s, const double* a,
                   double* out);
-/* environment.py:201-206. returns 1 if the move was committed. */
+/* environment.py:122-127. returns 1 if the move was committed. */
 int  orc_step(const float* speed, const float* angle, double* s, const double* a);
-/* environment.py:214-216 with the two random_sample() draws given. */
+/* environment.py:135-137 with the two random_sample() draws given. */
 void orc_reset_u(const double* region, double u0, double u1, double* out);
-/* environment.py:107-135 drawn from a numpy legacy stream; returns the goal-draw count. */
+/* environment.py:28-56 drawn from a numpy legacy stream; returns the goal-draw count. */
 int  orc_init_and_goal_mt(orc_mt_t* rs, double* region, double* goal, int* side);
-/* environment.py:214-216 drawn from a numpy legacy stream. */
+/* environment.py:135-137 drawn from a numpy legacy stream. */
 void orc_reset_mt(orc_mt_t* rs, const double* region, double* out);
 /* np.linalg.norm of a 2-vector as numpy 2.2.6 + OpenBLAS ddot computes it (fma tail). */
 double orc_norm2(double a0, double a1);
@@ -78,17 +78,17 @@ typedef struct {
 
 void orc_default_params(orc_params_t* p);
 
-/* per-env Philox init: region/goal (environment.py:107-135 semantics). returns goal draws used
+/* per-env Philox init: region/goal (environment.py:28-56 semantics). returns goal draws used
  * (0 = rejection cap hit, goal left at the last draw). */
 int  orc_vec_init_one(const orc_params_t* p, uint32_t stream_id, double* region, double* goal);
-/* per-env Philox reset draw for episode `ep` (environment.py:214-216 semantics). */
+/* per-env Philox reset draw for episode `ep` (environment.py:135-137 semantics). */
 void orc_vec_reset_one(const orc_params_t* p, uint32_t env, uint32_t ep, const double* region,
                        double* out);
 /* per-env Box-Muller pair for the exploration noise at vector step `step`. */
 void orc_vec_noise_one(const orc_params_t* p, uint32_t env, uint32_t step, double* z);
 
 /* One training tick of env e, fused the way nav_agent_step fuses it (robot.py:443-506, 509-538,
- * 645-675, 727-762; environment.py:130-137, 177-206). All per-env arrays are this env's slots.
+ * 645-675, 727-762; environment.py:130-137, 98-127). All per-env arrays are this env's slots.
  * meta: bit0 goal_reached, bit1 stuck, bit2 demo_flag, bits 8-10 hist count, bits 12-14 hist head.
  * Writes the replay row [8] float32 = s0 s1 a0 a1 r s'0 s'1 done; returns flags bit0 done,
  * bit1 goal, bit2 stuck, bit3 episode ended. */

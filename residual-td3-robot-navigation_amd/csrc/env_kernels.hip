@@ -12,7 +12,7 @@ constexpr uint32_t M_GOAL = 1u, M_STUCK = 2u, M_DEMO = 4u;
 constexpr uint8_t F_DONE = 1, F_GOAL = 2, F_STUCK = 4, F_ENDED = 8, F_DEMO = 16;
 
 NAV_DEV void region_of(int r, double u, double* reg) {
-    // environment.py:108-128 (left, right, bottom, top)
+    // environment.py:29-49 (left, right, bottom, top)
     const double W = 100.0, S = 25.0;
     const double v = 0.0 + (W - S - 0.0) * u;
     double l, rr, b, t;
@@ -28,7 +28,7 @@ __global__ __launch_bounds__(kBlock) void k_env_init(nav_params p, nav_env_soa e
     const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (e >= env.n) return;
     const uint32_t sid = (uint32_t)(e / epg);
-    // environment.py:107-135 on the Philox stream (NAV_TAG_INIT, stream id)
+    // environment.py:28-56 on the Philox stream (NAV_TAG_INIT, stream id)
     uint4 w = philox(0u, sid, NAV_TAG_INIT, 0u, p.seed_lo, p.seed_hi);
     double reg[4];
     region_of((int)(w.x & 3u), u01(w.z, w.w), reg);
@@ -51,7 +51,7 @@ __global__ __launch_bounds__(kBlock) void k_env_init(nav_params p, nav_env_soa e
     env.episodes[e] = ep0;
     env.noise_scale[e] = 1.0;  // robot.py:32 INITIAL_NOISE
     env.meta[e] = demo_flag ? M_DEMO : 0u;
-    // environment.py:209-216 first reset on the reset stream of this env
+    // environment.py:130-137 first reset on the reset stream of this env
     w = philox(0u, (uint32_t)e, NAV_TAG_RESET, (uint32_t)ep0, p.seed_lo, p.seed_hi);
     reinterpret_cast<double2*>(env.state)[e] = region_sample(reg, u01(w.x, w.y), u01(w.z, w.w));
     if (draws_out) draws_out[e] = used;
@@ -80,7 +80,7 @@ __global__ __launch_bounds__(kBlock) void k_env_step(int64_t n, double2* __restr
                                                      const float2* __restrict__ field,
                                                      const double2* __restrict__ action,
                                                      double2* __restrict__ next_out) {
-    // environment.py:201-206: 16 B state in, 16 B action in, 16 B state out per env
+    // environment.py:122-127: 16 B state in, 16 B action in, 16 B state out per env
     const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (e >= n) return;
     const double2 s = state[e];
@@ -235,7 +235,7 @@ __global__ __launch_bounds__(kBlock) void k_agent_step(nav_params p, nav_env_soa
         int32_t plan = env.plan_index[e];
         const int32_t path = env.path_length[e];
 
-        // environment.py:201-206
+        // environment.py:122-127
         double2 ns = dynamics(field, s, a);
         if (!in_world(ns)) ns = s;
         TransOut t = transition(p, env, e, s, a, ns, meta, plan, path, rows, (base + e) % cap);
@@ -387,9 +387,9 @@ __global__ __launch_bounds__(kDemoBlock) void k_demo_reward(nav_params p, int64_
 }
 
 // Batched open-loop rollouts through Environment.dynamics (the CEM demonstrator's inner loop,
-// environment.py:230-244): lane = path, T sequential steps, state carried in f64; paths [P][T+1][2]
+// environment.py:151-165): lane = path, T sequential steps, state carried in f64; paths [P][T+1][2]
 // f64; reward (nullable) = -||f32(s_T) - goal|| as compute_reward on the float32 planning_paths
-// row (environment.py:243, 261-262).
+// row (environment.py:164, 182-183).
 __global__ __launch_bounds__(kBlock) void k_rollout(const float2* __restrict__ field, int64_t P,
                                                     int32_t T, const double2* __restrict__ start,
                                                     const double2* __restrict__ actions,

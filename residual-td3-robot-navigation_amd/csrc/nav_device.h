@@ -50,7 +50,7 @@ NAV_DEV int cell_of(double v) {
     return c < 0 ? 0 : (c > 99 ? 99 : c);
 }
 
-// environment.py:177-198 Environment.dynamics. Field values come from the interleaved table
+// environment.py:98-119 Environment.dynamics. Field values come from the interleaved table
 // (speed, angle) — one 8-byte gather per call.
 NAV_DEV double2 dynamics(const float2* __restrict__ field, double2 s, double2 a) {
     const double a0 = clipd(a.x, -5.0, 5.0), a1 = clipd(a.y, -5.0, 5.0);
@@ -68,10 +68,10 @@ NAV_DEV double2 dynamics(const float2* __restrict__ field, double2 s, double2 a)
     return n;
 }
 
-// environment.py:204 commit test.
+// environment.py:125 commit test.
 NAV_DEV bool in_world(double2 n) { return 0.0 <= n.x && n.x < 100.0 && 0.0 <= n.y && n.y < 100.0; }
 
-// environment.py:214-216 uniform([l, b], [r, t]).
+// environment.py:135-137 uniform([l, b], [r, t]).
 NAV_DEV double2 region_sample(const double* reg, double u0, double u1) {
     return make_double2(reg[0] + (reg[1] - reg[0]) * u0, reg[2] + (reg[3] - reg[2]) * u1);
 }

@@ -1,4 +1,4 @@
-"""Drop-in `Environment` (environment.py:15-262) on the MI355X kernels.
+"""Drop-in `Environment` (environment.py:14-183) on the MI355X kernels.
 
 Same constructor, attributes (robot_state, robot_init_region, goal_state, dynamics_speed,
 dynamics_angle), methods and return conventions as the reference, numpy float64 in and out. All

@@ -1,4 +1,4 @@
-"""Dynamics fields (environment.py:138-174 set_dynamics), generated without `perlin_noise`.
+"""Dynamics fields (environment.py:59-95 set_dynamics), generated without `perlin_noise`.
 
 The reference builds its speed field from three PerlinNoise(octaves=5/10/20, seed=RANDOM_SEED)
 functions (weights 1, .5, .25) sampled at (col/100, row/100), min-max normalises, then stretches
@@ -16,7 +16,7 @@ def _gradient_noise(rng, octaves, n=100):
     g = rng.standard_normal((octaves + 1, octaves + 1, 2))
     g /= np.linalg.norm(g, axis=-1, keepdims=True) + 1e-12
     u = np.arange(n) / n * octaves
-    x, y = np.meshgrid(u, u, indexing="ij")  # [col][row] like environment.py:148-154
+    x, y = np.meshgrid(u, u, indexing="ij")  # [col][row] like environment.py:69-75
     x0, y0 = np.floor(x).astype(int), np.floor(y).astype(int)
     fx, fy = x - x0, y - y0
 

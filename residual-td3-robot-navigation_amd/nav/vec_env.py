@@ -109,18 +109,18 @@ class VecEnv:
         if init:
             self.init(demo_flag)
 
-    # environment.py:107-135 + robot.py:413-438 (vectorised, Philox)
+    # environment.py:28-56 + robot.py:413-438 (vectorised, Philox)
     def init(self, demo_flag=True, stream=None):
         lib().nav_env_init(C.byref(self.p), C.byref(self.soa), self.envs_per_group,
                            int(bool(demo_flag)), ptr(self.goal_draws), stream_handle(stream))
 
-    # environment.py:209-216
+    # environment.py:130-137
     def reset(self, mask=None, uniforms=None, stream=None):
         lib().nav_env_reset(C.byref(self.p), C.byref(self.soa), ptr(mask), ptr(uniforms),
                             stream_handle(stream))
         return self.state
 
-    # environment.py:201-206 (pure Environment.step over all envs)
+    # environment.py:122-127 (pure Environment.step over all envs)
     def step(self, action, next_state=None, stream=None):
         with prof.region("env_step", float(prof.ENV_STEP_BYTES * self.n)):
             lib().nav_env_step(C.byref(self.p), C.byref(self.soa), ptr(self.field), ptr(action),
@@ -142,7 +142,7 @@ class VecEnv:
             self.demo_off = torch.as_tensor(demo_off, dtype=torch.int64).to(self.device)
         self.demo_index = DemoIndex(self.demo_xy, self.demo_off) if index else None
 
-    # one fused training tick (robot.py:443-506, 645-675 + environment.py:201-216)
+    # one fused training tick (robot.py:443-506, 645-675 + environment.py:122-137)
     def agent_step(self, action, replay, stream=None, reward_out=None):
         base = replay.position
         s = stream_handle(stream)

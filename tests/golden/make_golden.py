@@ -44,7 +44,7 @@ def import_reference():
 
 def make_fields(seed):
     """Synthetic fields with the value ranges set_dynamics produces (speed = sigmoid-stretched in
-    (0,1), angle in [0,1]); float32 [100,100], x-major like environment.py:146-174."""
+    (0,1), angle in [0,1]); float32 [100,100], x-major like environment.py:67-95."""
     rng = np.random.default_rng(seed)
     x = np.linspace(0, 1, 100)
     base = np.zeros((100, 100))

@@ -7,7 +7,7 @@ from conftest import golden
 
 
 def test_legacy_rng_stream_matches_numpy(orc):
-    # numpy legacy RandomState is the reference's RNG (environment.py:108-132, robot.py:111, 640)
+    # numpy legacy RandomState is the reference's RNG (environment.py:29-53, robot.py:111, 640)
     for seed in (1707366464, 0, 1, 987654321):
         rs = np.random.RandomState(seed)
         o = orc.LegacyRandomState(seed)
