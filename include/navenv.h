@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define NAV_ABI_VERSION 1
+#define NAV_ABI_VERSION 2
 #define NAV_EINVAL (-100000)
 
 #define NAV_WORLD_CELLS 100 /* field = float32 [100][100][2] (speed, angle), x-major: cell cx*100+cy
@@ -213,26 +213,56 @@ int nav_act(const nav_params* p, const nav_mlp* actor, int64_t n, const double* 
  * x = in[m*ld_in + in_col + 0..d_in) (f32). out_mode 0: out[m*ld_out + out_col + j] = y;
  * out_mode 1 (target policy smoothing, robot.py:336-339): out = clamp(y + clamp(policy_noise*eps,
  * +-noise_clip), +-max_action) with eps from `eps` [M][2] f32 if given else Philox
- * (NAV_TAG_TNOISE, counter). acts (nullable, per net): [n_hidden][M][hp] saved post-ReLU
- * activations (for nav_mlp_wgrad); masks (nullable, per net): nav_mlp_mask_count u16 words of
- * ReLU-derivative bits (for nav_mlp_backward). */
+ * (NAV_TAG_TNOISE, counter). acts (nullable, per net): [n_hidden][M][hp] post-ReLU activations,
+ * layer L written when bit L of save_mask is set; masks (nullable, per net): nav_mlp_mask_count
+ * u16 words of ReLU-derivative bits (for nav_mlp_backward / nav_mlp_wgrad). */
 int nav_mlp_forward(const nav_mlp* nets, int32_t n_nets, int64_t M, const float* in,
                     int32_t ld_in, int32_t in_col, float* const* out, int32_t ld_out,
                     int32_t out_col, int32_t out_mode, const float* eps, float policy_noise,
                     float noise_clip, float max_action, uint32_t seed_lo, uint32_t seed_hi,
-                    uint32_t counter, float* const* acts, uint16_t* const* masks, void* stream);
+                    uint32_t counter, float* const* acts, uint32_t save_mask,
+                    uint16_t* const* masks, void* stream);
 /* u16 words of the ReLU mask image for M rows (layout: [n_hidden][row tiles][hp/32][64]). */
 int64_t nav_mlp_mask_count(int32_t hidden_pad, int32_t n_hidden, int64_t M);
-/* Row-local backward of one network: given dL/dy [M][d_out] and the forward's ReLU masks, writes
- * dZ [n_hidden][M][hp] (dL/d pre-activation per hidden layer) and, if dx != NULL, dL/dx [M][d_in]. */
-int nav_mlp_backward(const nav_mlp* net, int64_t M, const float* dy, const uint16_t* masks,
-                     float* dz, float* dx, void* stream);
-/* Weight gradients of one network as `splits` partial slabs [splits][param_count] (row range of
- * split s = [s*M/splits, (s+1)*M/splits)); combine with nav_grad_reduce. */
+/* Parameter gradients are produced in two parts that nav_grad_reduce combines:
+ *  - edge slabs [row blocks][nav_mlp_edge_count]: per row block of the forward/backward launches
+ *    (nav_mlp_row_blocks(M) blocks), partial sums of every parameter except the hidden x hidden
+ *    weights, in the flat order with those segments cut out (W0 | b0 .. b_{n_hidden-1} | Wo | bo);
+ *  - hidden slabs [splits][nav_mlp_hidden_count]: nav_mlp_wgrad's split-M partials of
+ *    W_1 .. W_{n_hidden-1}. */
+int64_t nav_mlp_row_blocks(int64_t M);
+int64_t nav_mlp_edge_count(int32_t d_in, int32_t d_out, int32_t hidden_pad, int32_t n_hidden);
+int64_t nav_mlp_hidden_count(int32_t hidden_pad, int32_t n_hidden);
+/* train_critic's online twin forward (robot.py:341-361), nets[2] critics (d_out 1) on
+ * x = in[b*ld_in + in_col + 0..4): y = r + gamma*min(q1t, q2t)*(1 - done) from the replay batch
+ * [B][8] (r at column 4, done at 7); dq[i] [B] = 2*(q_i - y)/B (mse_loss backward);
+ * loss_part[i] [row blocks] = block sums of (q_i - y)^2; edge_slabs[i] (nullable) receive the
+ * output layer's Wo / bo partials; acts/save_mask as nav_mlp_forward; masks[i] required. */
+int nav_td3_critic_forward(const nav_mlp* nets, int64_t B, const float* in, int32_t ld_in,
+                           int32_t in_col, const float* batch, const float* q1t, const float* q2t,
+                           float gamma, float* const* dq, float* const* loss_part,
+                           float* const* edge_slabs, float* const* acts, uint32_t save_mask,
+                           uint16_t* const* masks, void* stream);
+/* Row-local backward of one network (autograd of robot.py:355-395) given dL/dy rows
+ * dy[m*ld_dy + 0..d_out) (ld_dy 0: one row for all) and the forward's ReLU masks: dL/dz of every
+ * hidden layer, dz_L written to dz [n_hidden][M][hp] for bits L of save_mask; dx (nullable)
+ * [M][d_in] = dL/dx. edge_slabs (nullable): per-block W0 / bias partials (input rows from `in`),
+ * plus Wo / bo when h_top [M][hp] (the top hidden activations) is given. */
+int nav_mlp_backward(const nav_mlp* net, int64_t M, const float* dy, int32_t ld_dy,
+                     const uint16_t* masks, const float* in, int32_t ld_in, int32_t in_col,
+                     const float* h_top, float* dz, uint32_t save_mask, float* dx,
+                     float* edge_slabs, void* stream);
+/* Hidden x hidden weight gradients dW_L = dz_L^T h_{L-1} as `splits` partial slabs
+ * [splits][nav_mlp_hidden_count] (rows of split s = [s*ceil(M/splits), ...)). h_0 is recomputed
+ * from `in`, dz_{n_hidden-1} from dy and the masks; acts / dz (saved layers 1 .. n_hidden-2) are
+ * read only for n_hidden > 2. */
 int nav_mlp_wgrad(const nav_mlp* net, int64_t M, const float* in, int32_t ld_in, int32_t in_col,
-                  const float* acts, const float* dz, const float* dy, float* slabs,
-                  int32_t splits, void* stream);
-int nav_grad_reduce(const float* slabs, int32_t splits, int64_t count, float* grad, void* stream);
+                  const float* acts, const float* dz, const float* dy, int32_t ld_dy,
+                  const uint16_t* masks, float* slabs, int32_t splits, void* stream);
+/* grad [param_count] = sum of the hidden slabs (hidden weights) and of the edge slabs (the rest),
+ * in a fixed order. */
+int nav_grad_reduce(const nav_mlp* net, const float* hidden_slabs, int32_t splits,
+                    const float* edge_slabs, int64_t edge_blocks, float* grad, void* stream);
 /* torch.optim.Adam step (robot.py:236-239; torch 2.10 single-tensor semantics) on a flat buffer,
  * step_size = lr/(1-b1^t), bc2_sqrt = sqrt(1-b2^t) precomputed by the caller; refreshes `packed`
  * of `net` (net->params must equal params). */
@@ -249,15 +279,7 @@ int nav_mlp_pack(const nav_mlp* net, void* stream);
 int nav_replay_sample(const nav_replay* replay, int64_t size, int64_t B, const int64_t* idx,
                       uint32_t seed_lo, uint32_t seed_hi, uint32_t counter, float* batch,
                       void* stream);
-/* train_critic target and loss gradients (robot.py:341-353): y = r + gamma*min(q1t,q2t)*(1-d);
- * dq_i = 2*(q_i - y)/B; loss_part [gridDim][2] partial sums of (q_i - y)^2 (nullable). */
-int nav_td3_critic_loss(int64_t B, const float* batch, const float* q1t, const float* q2t,
-                        const float* q1, const float* q2, float gamma, float* dq1, float* dq2,
-                        float* y_out, float* loss_part, void* stream);
-/* Build the critic input [B][4] = (s, a) from a batch [B][8]. */
-int nav_batch_sa(int64_t B, const float* batch, float* sa, void* stream);
-/* train_actor (robot.py:386-390): dL/dq = -1/B everywhere; and the actor's dL/da from the
- * critic's dL/dx [B][4] (columns 2..3). */
+/* Fill / strided copy helpers of the TD3 glue (robot.py:329-339, 386-390). */
 int nav_fill(float* x, int64_t n, float value, void* stream);
 int nav_strided_copy(const float* src, int32_t ld_src, int32_t col_src, float* dst, int32_t ld_dst,
                      int32_t col_dst, int64_t rows, int32_t cols, void* stream);

@@ -57,7 +57,46 @@ bool make_dev(const nav_mlp* n, MlpDev* d) {
     return true;
 }
 
+// Edge-gradient layout: every parameter except the hidden x hidden weights W_1 .. W_{nh-1}, in
+// the flat order with those segments cut out (W0 | b0 | b1 .. b_{nh-1} | Wo | bo). The forward /
+// backward kernels sum these per row block while the operands sit in LDS (edge slabs
+// [blocks][edge_count]); nav_grad_reduce folds them and the weight-gradient slabs into the flat
+// gradient.
+__host__ __device__ inline int64_t hidden_w_count(const MlpDev& d) {
+    return (int64_t)(d.n_hidden - 1) * d.hp * d.hp;
+}
+__host__ __device__ inline int64_t edge_count(const MlpDev& d) { return d.count - hidden_w_count(d); }
+// edge index of b_L (L < n_hidden), of Wo and of bo
+__host__ __device__ inline int64_t e_b(const MlpDev& d, int L) {
+    return d.b_off[L] - (int64_t)L * d.hp * d.hp;
+}
+__host__ __device__ inline int64_t e_wo(const MlpDev& d) { return d.w_off[d.n_hidden] - hidden_w_count(d); }
+__host__ __device__ inline int64_t e_bo(const MlpDev& d) { return d.b_off[d.n_hidden] - hidden_w_count(d); }
+// flat parameter index of edge index e
+__host__ __device__ inline int64_t edge_to_flat(const MlpDev& d, int64_t e) {
+    const int nh = d.n_hidden;
+    if (nh == 1 || e < d.w_off[1]) return e;
+    if (e >= e_wo(d)) return e + hidden_w_count(d);
+    const int64_t L = (e - d.w_off[1]) / d.hp + 1;  // inside the b_L run
+    return e + L * d.hp * d.hp;
+}
+
 inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// One hidden unit of layer 0 (K = d_in <= 4; absent inputs and weights are 0). The forward and the
+// weight-gradient kernel's recompute of h_0 share this fma order, so both produce the same bits.
+NAV_DEV float layer0_unit(float4 x, float w0, float w1, float w2, float w3, float b) {
+    float v = b;
+    v = fmaf(x.x, w0, v);
+    v = fmaf(x.y, w1, v);
+    v = fmaf(x.z, w2, v);
+    v = fmaf(x.w, w3, v);
+    return fmaxf(v, 0.f);
+}
+
+// dL/dz of the top hidden layer before its ReLU mask: dy . Wo[:, n] (d_out <= 2; absent = 0).
+// Shared by the backward and the weight-gradient recompute of dz_{nh-1}.
+NAV_DEV float top_unit(float g0, float g1, float w0, float w1) { return fmaf(g1, w1, g0 * w0); }
 
 NAV_DEV f32x16 mfma(float a, float b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
@@ -141,7 +180,7 @@ NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const float* __restr
 }
 
 enum { IN_F32 = 0, IN_BASELINE = 1 };
-enum { OUT_F32 = 0, OUT_TARGET = 1, OUT_ACT = 2 };
+enum { OUT_F32 = 0, OUT_TARGET = 1, OUT_ACT = 2, OUT_LOSS = 3 };
 
 // ReLU masks: one 16-bit word per (row tile, column tile, lane) holding the lane's 16 C-layout
 // elements' (value > 0) bits; [n_hidden][row tiles][NT][64]. The backward reads 2 bytes per 16
@@ -158,7 +197,17 @@ struct FwdArgs {
     float* out[2];
     int ld_out, out_col;
     float* acts[2];
+    uint32_t save_mask;  // bit L: hidden layer L's output rows are copied to acts + L*M*hp
     uint16_t* masks[2];
+    // OUT_LOSS: train_critic's online twin forward with the TD error and the output layer's
+    // gradient partials (robot.py:341-361)
+    const float* batch;  // [M][8] replay rows (r at 4, done at 7)
+    const float* qt[2];  // target twin values q1', q2' [M]
+    float gamma, norm;   // discount, 2/B (mse_loss backward)
+    float* dq[2];        // [M] dL/dq
+    float* loss_part[2]; // [blocks] sum of (q - y)^2 over the block's rows
+    float* eslab[2];     // [blocks][edge_count]: Wo / bo partials (nullable)
+    int64_t ecount;
     // OUT_TARGET
     const float* eps;
     float policy_noise, noise_clip, max_action;
@@ -217,6 +266,90 @@ NAV_DEV void copy_rows(const float* act, int S_, float* g, int64_t row0, int64_t
         if (row0 + r < M)
             *reinterpret_cast<float4*>(g + (row0 + r) * hp + 4 * c4) =
                 *reinterpret_cast<const float4*>(act + r * S_ + 4 * c4);
+    }
+}
+
+// Edge partials over the block's TM LDS rows, one thread per column n < hp, rows summed in order.
+template <int TM>
+NAV_DEV void edge_col_sums(const float* act, int S_, int hp, float* out) {
+    const int n = threadIdx.x;
+    if (n >= hp) return;
+    float s = 0.f;
+#pragma unroll 8
+    for (int r = 0; r < TM; ++r) s += act[r * S_ + n];
+    out[n] = s;
+}
+
+// dW0 partial: out[n*d_in + k] = sum_r dz0[r][n] * x[r][k]
+template <int TM>
+NAV_DEV void edge_w0(const float* act, int S_, int hp, const float* xin, int d_in, float* out) {
+    const int n = threadIdx.x;
+    if (n >= hp) return;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+#pragma unroll 8
+    for (int r = 0; r < TM; ++r) {
+        const float g = act[r * S_ + n];
+        const float4 x = *reinterpret_cast<const float4*>(xin + 4 * r);
+        s0 = fmaf(g, x.x, s0);
+        s1 = fmaf(g, x.y, s1);
+        s2 = fmaf(g, x.z, s2);
+        s3 = fmaf(g, x.w, s3);
+    }
+    out[n * d_in] = s0;
+    if (d_in > 1) out[n * d_in + 1] = s1;
+    if (d_in > 2) out[n * d_in + 2] = s2;
+    if (d_in > 3) out[n * d_in + 3] = s3;
+}
+
+// OUT_LOSS (d_out = 1): q from the output-layer partials, the TD target of robot.py:341-345
+// y = r + gamma * min(q1', q2') * (1 - done), mse_loss's gradient dq = (q - y) * 2/B, the block's
+// sum of (q - y)^2, and the output layer's gradient partials dWo = dq^T h_top, dbo = sum dq while
+// h_top is still in LDS. `red` = the [2][PARTS][TM] partial-sum scratch (second half reused).
+template <int NT, int RT>
+NAV_DEV void loss_epilogue(const FwdArgs& a, const MlpDev& net, const float* act, float* red,
+                           int64_t row0) {
+    constexpr int hp = NT * 32, SS = hp + 4, TM = RT * 32, PARTS = kBlock / TM;
+    const int tid = threadIdx.x, nh = net.n_hidden, q = blockIdx.y;
+    const int64_t r = row0 + tid;
+    float dqv = 0.f, e2 = 0.f;
+    if (tid < TM && r < a.M) {
+        float y = 0.f;
+#pragma unroll
+        for (int p = 0; p < PARTS; ++p) y += red[p * TM + tid];
+        y += net.params[net.b_off[nh]];
+        const float rw = a.batch[r * NAV_ROW + 4], dn = a.batch[r * NAV_ROW + 7];
+        const float mn = fminf(a.qt[0][r], a.qt[1][r]);
+        const float yt = rw + (a.gamma * mn) * (1.0f - dn);
+        const float e = y - yt;
+        dqv = e * a.norm;
+        e2 = e * e;
+        a.dq[q][r] = dqv;
+    }
+    float* dqs = red + kBlock;  // [TM] dq, then [kBlock/64] wave sums
+    float* ws = dqs + TM;
+    if (tid < TM) dqs[tid] = dqv;
+    const float w = wave_sum(e2);
+    if ((tid & 63) == 0) ws[tid >> 6] = w;
+    __syncthreads();
+    if (tid == 0) {
+        float s = 0.f;
+#pragma unroll
+        for (int k = 0; k < kBlock / 64; ++k) s += ws[k];
+        a.loss_part[q][blockIdx.x] = s;
+    }
+    if (!a.eslab[q]) return;
+    float* es = a.eslab[q] + (int64_t)blockIdx.x * a.ecount;
+    if (tid < hp) {
+        float s = 0.f;
+#pragma unroll 8
+        for (int rr = 0; rr < TM; ++rr) s = fmaf(dqs[rr], act[rr * SS + tid], s);
+        es[e_wo(net) + tid] = s;
+    }
+    if (tid < 4) {  // bo and its 3 padding floats
+        float s = 0.f;
+        if (tid == 0)
+            for (int rr = 0; rr < TM; ++rr) s += dqs[rr];
+        es[e_bo(net) + tid] = s;
     }
 }
 
@@ -287,13 +420,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
                     const int ro = rt * 32 + (i & 3) + 8 * (i >> 2);
-                    const float4 x = xs[i];
-                    float v = b;
-                    v = fmaf(x.x, w[0], v);
-                    v = fmaf(x.y, w[1], v);
-                    v = fmaf(x.z, w[2], v);
-                    v = fmaf(x.w, w[3], v);
-                    v = fmaxf(v, 0.f);
+                    const float v = layer0_unit(xs[i], w[0], w[1], w[2], w[3], b);
                     col[ro * SS] = v;
                     bits |= (v > 0.f ? 1u : 0u) << i;
                 }
@@ -302,7 +429,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
         }
     }
     __syncthreads();
-    if (act_save) copy_rows<NT, RT>(act, SS, act_save, row0, M);
+    if (act_save && (a.save_mask & 1u)) copy_rows<NT, RT>(act, SS, act_save, row0, M);
 
     // ---- hidden x hidden layers on MFMA
     for (int L = 1; L < nh; ++L) {
@@ -322,7 +449,8 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
         store_layer<NT, RT>(acc, act, SS, masks ? masks + (size_t)L * n_rt * NT * 64 : nullptr,
                             rt0);
         __syncthreads();
-        if (act_save) copy_rows<NT, RT>(act, SS, act_save + (int64_t)L * M * hp, row0, M);
+        if (act_save && ((a.save_mask >> L) & 1u))
+            copy_rows<NT, RT>(act, SS, act_save + (int64_t)L * M * hp, row0, M);
     }
 
     // ---- output layer (N = d_out <= 2) on the VALU: every thread takes one row and one K slice
@@ -353,6 +481,10 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
     const int rloc = tid % TM;
     const int j = tid / TM;
     const int64_t r = row0 + rloc;
+    if (OUT_MODE == OUT_LOSS) {
+        loss_epilogue<NT, RT>(a, net, act, xin + TM * 4, row0);
+        return;
+    }
     if (r >= M || j >= d_out) return;
     float y = 0.f;
     {
@@ -404,9 +536,16 @@ struct BwdArgs {
     MlpDev net;
     int64_t M;
     const float* dy;
+    int ld_dy;               // dy row stride (0: one row broadcast to every row)
     const uint16_t* masks;
-    float* dz;
+    const float* in;         // the forward's input rows (dW0 partials), with eslab
+    int ld_in, in_col;
+    const float* h_top;      // nullable: [M][hp] top activations -> Wo / bo partials here
+    float* dz;               // [n_hidden][M][hp], layers with a save_mask bit written
+    uint32_t save_mask;
     float* dx;
+    float* eslab;            // nullable: [blocks][edge_count] W0 / bias (/ Wo / bo) partials
+    int64_t ecount;
 };
 
 template <int NT, int RT>
@@ -441,20 +580,52 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_bwd(BwdArgs a) {
     const int64_t rt0 = (int64_t)blockIdx.x * RT;
     const int64_t n_rt = mask_rowtiles(M);
     float* act = smem;
-    float* dys = smem + TM * SS;
+    float* dys = smem + TM * SS;  // [TM][4] dy rows
+    float* xin = dys + TM * 4;    // [TM][4] forward input rows (dW0), inside the 2*kBlock scratch
     const int d_in = net.d_in, d_out = net.d_out, nh = net.n_hidden;
     const int64_t MH = M * hp;
     const WaveCols<NT> wc(wv);
     const size_t mstride = (size_t)n_rt * NT * 64;
+    float* es = a.eslab ? a.eslab + (int64_t)blockIdx.x * a.ecount : nullptr;
 
     if (tid < TM) {
         const int64_t r = row0 + tid;
         float x[2] = {0.f, 0.f};
-        if (r < M)
-            for (int j = 0; j < d_out; ++j) x[j] = a.dy[r * d_out + j];
+        float xi[4] = {0.f, 0.f, 0.f, 0.f};
+        if (r < M) {
+            for (int j = 0; j < d_out; ++j) x[j] = a.dy[r * a.ld_dy + j];
+            if (es)
+                for (int k = 0; k < d_in; ++k) xi[k] = a.in[r * a.ld_in + a.in_col + k];
+        }
         *reinterpret_cast<float4*>(dys + tid * 4) = make_float4(x[0], x[1], 0.f, 0.f);
+        *reinterpret_cast<float4*>(xin + tid * 4) = make_float4(xi[0], xi[1], xi[2], xi[3]);
     }
     __syncthreads();
+    if (es) {
+        // output layer (robot.py:361 / 392 backward): dWo = dy^T h_top, dbo = sum dy, when the
+        // forward did not produce them (it does for the critic's TD loss)
+        if (a.h_top) {
+            const int n = tid;
+            if (n < hp) {
+                float s0 = 0.f, s1 = 0.f;
+                const int rows = (int)(M - row0 < TM ? M - row0 : TM);
+#pragma unroll 4
+                for (int rr = 0; rr < rows; ++rr) {
+                    const float h = a.h_top[(row0 + rr) * hp + n];
+                    s0 = fmaf(dys[rr * 4], h, s0);
+                    s1 = fmaf(dys[rr * 4 + 1], h, s1);
+                }
+                es[e_wo(net) + n] = s0;
+                if (d_out > 1) es[e_wo(net) + hp + n] = s1;
+            }
+            if (tid < 4) {
+                float s = 0.f;
+                if (tid < d_out)
+                    for (int rr = 0; rr < TM; ++rr) s += dys[rr * 4 + tid];
+                es[e_bo(net) + tid] = s;
+            }
+        }
+    }
 
     // top hidden layer: dz = (dy . Wo) * relu'(.), in the C layout
     {
@@ -480,14 +651,23 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_bwd(BwdArgs a) {
                 for (int i = 0; i < 16; ++i) {
                     const int ro = rt * 32 + (i & 3) + 8 * (i >> 2);
                     const float4 g = gs[i];
-                    const float v = fmaf(g.y, w1, g.x * w0);
+                    const float v = top_unit(g.x, g.y, w0, w1);
                     col[ro * SS] = (bits >> i) & 1u ? v : 0.f;
                 }
             }
         }
     }
     __syncthreads();
-    copy_rows<NT, RT>(act, SS, a.dz + (int64_t)(nh - 1) * MH, row0, M);
+    // per layer: bias gradient db_L = column sums of dz_L (and dW0 at L = 0), then the rows
+    // themselves only where the weight-gradient kernel cannot recompute them (save_mask)
+    auto finish_layer = [&](int L) {
+        if (es) {
+            edge_col_sums<TM>(act, SS, hp, es + e_b(net, L));
+            if (L == 0) edge_w0<TM>(act, SS, hp, xin, d_in, es + net.w_off[0]);
+        }
+        if ((a.save_mask >> L) & 1u) copy_rows<NT, RT>(act, SS, a.dz + (int64_t)L * MH, row0, M);
+    };
+    finish_layer(nh - 1);
 
     // hidden layers, top-down: dz_{L-1} = (dz_L . W_L) * relu'(act_{L-1}), B = packed Wb_L
     for (int L = nh - 1; L >= 1; --L) {
@@ -497,7 +677,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_bwd(BwdArgs a) {
         __syncthreads();
         mask_and_store<NT, RT>(acc, a.masks + (size_t)(L - 1) * mstride, act, SS, rt0);
         __syncthreads();
-        copy_rows<NT, RT>(act, SS, a.dz + (int64_t)(L - 1) * MH, row0, M);
+        finish_layer(L - 1);
     }
 
     // dx = dz_0 . W0 : thread = (row, input pair)
@@ -514,65 +694,62 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_bwd(BwdArgs a) {
     }
 }
 
-// ---------------- weight gradients (split-M partial slabs) ----------------
+// ---------------- hidden x hidden weight gradients (split-M partial slabs) ----------------
+// dW_L = dz_L^T h_{L-1} for L = 1 .. nh-1 over the rows of each split. The thin layers' gradients
+// (W0, every bias, Wo, bo) are edge partials of the forward / backward kernels instead.
 struct WgradArgs {
     MlpDev net;
     int64_t M;
-    const float* in;
+    const float* in;        // layer-0 input rows: h_0 is recomputed (layer0_unit)
     int ld_in, in_col;
-    const float* acts;
-    const float* dz;
-    const float* dy;
-    float* slabs;
+    const float* acts;      // [nh][M][hp]: saved h_L, 1 <= L <= nh-2
+    const float* dz;        // [nh][M][hp]: saved dz_L, 1 <= L <= nh-2
+    const float* dy;        // dz_{nh-1} is recomputed: top_unit(dy row, Wo) under the ReLU bit
+    int ld_dy;
+    const uint16_t* masks;  // the forward's ReLU bit image
+    float* slabs;           // [splits][(nh-1) hp hp]
     int splits;
-    int T;        // 64-wide column panels across hp (edge kinds)
-    int TA;       // 128-wide tiles across hp (hidden kind)
-    int n_hid;    // hidden-kind jobs = (nh - 1) * TA * TA
+    int TA;                 // 128-wide tiles across hp
+    int n_hid;              // jobs = (nh - 1) * TA * TA
 };
 
-constexpr int WG_MC = 32;    // rows per staged chunk
-constexpr int WG_LD = 68;    // LDS row stride of the staged 64-column panels (edge kinds)
-constexpr int WA_W = 128;    // hidden-kind tile width
-constexpr int WA_LD = 132;   // LDS row stride of its 128-column panels
+constexpr int WG_MC = 32;   // rows per staged chunk
+constexpr int WA_W = 128;   // tile width
+constexpr int WA_LD = 132;  // LDS row stride of the 128-column panels
 
-inline size_t wgrad_lds_bytes() {
-    const size_t hid = (2 * 2 * WG_MC * WA_LD + 2 * WA_W) * 4;
-    const size_t edge = (2 * 2 * WG_MC * WG_LD + 2 * WG_MC * 4 + 4 * 64 * 6) * 4;
-    return hid > edge ? hid : edge;
-}
+inline size_t wgrad_lds_bytes() { return (size_t)2 * 2 * WG_MC * WA_LD * 4; }
 
 // v if c else 0, per component (a float4-wide select would be lowered through the stack)
 NAV_DEV float4 sel4(bool c, float4 v) {
     return make_float4(c ? v.x : 0.f, c ? v.y : 0.f, c ? v.z : 0.f, c ? v.w : 0.f);
 }
 
-// Hidden x hidden layer L, one 128x128 tile (tn, tk) of dW_L = dz_L^T act_{L-1} over the rows of
-// one split: the 4 waves own 64x64 quadrants (2x2 v_mfma_f32_32x32x2_f32 tiles each; the MFMA K
-// dimension is the row index). 32-row chunks of the two 128-column panels are double-buffered in
-// LDS with the next chunk's global loads in flight during the current chunk's MFMAs. Tiles with
-// tk == 0 also produce db_L = column sums of dz_L.
-template <bool FULL>
+// One 128x128 tile (tn, tk) of dW_L over the rows of one split: the 4 waves own 64x64 quadrants
+// (2x2 v_mfma_f32_32x32x2_f32 tiles each; the MFMA K dimension is the row index). 32-row chunks
+// of the P (dz_L columns) and Q (h_{L-1} columns) panels are double-buffered in LDS with the next
+// chunk's operands in flight during the current chunk's MFMAs.
+// PR / QR: the panel is recomputed instead of read from a saved [M][hp] tensor — for the top
+// layer dz = top_unit(dy, Wo) under the forward's ReLU bit (8 B of mask words per row and 4
+// columns), for layer 1 h_0 = layer0_unit(x, W0, b0) — the same bits the backward / forward
+// produced, so a 2-hidden-layer network's weight gradient reads no activation tensor at all.
+template <bool FULL, bool PR, bool QR>
 NAV_DEV void wgrad_hidden(const WgradArgs& a, int job, int split, float* smem) {
     const MlpDev& net = a.net;
-    const int hp = net.hp, TA = a.TA;
+    const int hp = net.hp, TA = a.TA, nh = net.n_hidden, d_in = net.d_in, d_out = net.d_out;
     const int L = job / (TA * TA) + 1;
     const int tn = (job % (TA * TA)) / TA, tk = job % TA;
     const int n0 = tn * WA_W, k0 = tk * WA_W;
-    const int64_t MH = a.M * hp;
-    const float* P = a.dz + (int64_t)L * MH;
-    const float* Q = a.acts + (int64_t)(L - 1) * MH;
-    float* Ps = smem;                          // [2][32][WA_LD]
-    float* Qs = smem + 2 * WG_MC * WA_LD;      // [2][32][WA_LD]
-    float* red = smem + 4 * WG_MC * WA_LD;     // [2][128]
+    const int64_t M = a.M, MH = M * hp;
+    float* Ps = smem;                      // [2][32][WA_LD]
+    float* Qs = smem + 2 * WG_MC * WA_LD;  // [2][32][WA_LD]
     const int tid = threadIdx.x, lane = tid & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
     const int wn = 64 * (wv >> 1), wk = 64 * (wv & 1);
     // 32x32 sub-tiles inside hp (wave-uniform)
     const bool n0k = n0 + wn < hp, n1k = n0 + wn + 32 < hp;
     const bool k0k = k0 + wk < hp, k1k = k0 + wk + 32 < hp;
-    const int64_t per = (a.M + a.splits - 1) / a.splits;
+    const int64_t per = (M + a.splits - 1) / a.splits;
     const int64_t m_lo = (int64_t)split * per;
-    const int64_t m_hi = m_lo + per < a.M ? m_lo + per : a.M;
-    const bool colsum = tk == 0;
+    const int64_t m_hi = m_lo + per < M ? m_lo + per : M;
     f32x16 acc[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -580,44 +757,103 @@ NAV_DEV void wgrad_hidden(const WgradArgs& a, int job, int split, float* smem) {
         for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-    float cs = 0.f;  // column sum: thread = (column tid & 127, row parity tid >> 7)
-    // staging: thread loads float4 (row rr, columns 4*c4..) for rr = (tid >> 5) + 8 f
+    // staging: thread = 4 columns from 4*c4 of each panel, rows rr0 + 8 f of the chunk. Every load
+    // comes from a clamped valid address; out-of-range values are zeroed at store time.
     const int c4 = tid & 31, rr0 = tid >> 5;
-    // loads are unconditional from clamped (valid) addresses; out-of-range values are zeroed
-    // in registers, so no load sits behind a branch or a pointer select
-    const bool pc_ok = n0 + 4 * c4 < hp, qc_ok = k0 + 4 * c4 < hp;
-    const float* Pc = P + (pc_ok ? n0 + 4 * c4 : 0);
-    const float* Qc = Q + (qc_ok ? k0 + 4 * c4 : 0);
-    // (zeroing happens at store time, so nothing consumes the loads before the chunk's MFMAs)
-    auto load = [&](int64_t m0, float4 (&rp)[4], float4 (&rq)[4]) {
+    const int pn = n0 + 4 * c4, qk = k0 + 4 * c4;
+    const bool pc_ok = pn < hp, qc_ok = qk < hp;
+    const int pnc = pc_ok ? pn : 0, qkc = qc_ok ? qk : 0;
+    const float* Pc = a.dz + (PR ? 0 : (int64_t)L * MH + pnc);
+    const float* Qc = a.acts + (QR ? 0 : (int64_t)(L - 1) * MH + qkc);
+    float wo0[4] = {0.f, 0.f, 0.f, 0.f}, wo1[4] = {0.f, 0.f, 0.f, 0.f};
+    float w0[4][4] = {}, b0[4] = {0.f, 0.f, 0.f, 0.f};
+    const uint16_t* mk = a.masks;
+    if (PR) {
+        const float* Wo = net.params + net.w_off[nh];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            wo0[c] = Wo[pnc + c];
+            wo1[c] = d_out > 1 ? Wo[hp + pnc + c] : 0.f;
+        }
+        mk += (size_t)(nh - 1) * mask_rowtiles(M) * (hp >> 5) * 64;
+    }
+    if (QR) {
+        const float* W0 = net.params + net.w_off[0];
+        const float* bb = net.params + net.b_off[0];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) w0[c][k] = k < d_in ? W0[(qkc + c) * d_in + k] : 0.f;
+            b0[c] = bb[qkc + c];
+        }
+    }
+    const int g1 = d_out > 1 ? 1 : 0;
+    const int x1 = d_in > 1 ? 1 : 0, x2 = d_in > 2 ? 2 : 0, x3 = d_in > 3 ? 3 : 0;
+    float4 rp[4], rq[4];
+    uint2 rm[4];
+    auto load = [&](int64_t m0) {
 #pragma unroll
         for (int f = 0; f < 4; ++f) {
             const int64_t m = m0 + rr0 + 8 * f;
             const int64_t mc = m < m_hi ? m : m_lo;
-            rp[f] = *reinterpret_cast<const float4*>(Pc + mc * hp);
-            rq[f] = *reinterpret_cast<const float4*>(Qc + mc * hp);
+            if (PR) {
+                const int rr = (int)(mc & 31);
+                rm[f] = *reinterpret_cast<const uint2*>(
+                    mk + mask_idx(mc >> 5, hp >> 5, pnc >> 5, (pnc & 31) + 32 * ((rr >> 2) & 1)));
+                const float* g = a.dy + mc * a.ld_dy;
+                rp[f] = make_float4(g[0], g[g1], 0.f, 0.f);
+            } else {
+                rp[f] = *reinterpret_cast<const float4*>(Pc + mc * hp);
+            }
+            if (QR) {
+                const float* x = a.in + mc * a.ld_in + a.in_col;
+                rq[f] = make_float4(x[0], x[x1], x[x2], x[x3]);
+            } else {
+                rq[f] = *reinterpret_cast<const float4*>(Qc + mc * hp);
+            }
         }
     };
-    auto store = [&](int buf, int64_t m0, const float4 (&rp)[4], const float4 (&rq)[4]) {
+    auto store = [&](int buf, int64_t m0) {
 #pragma unroll
         for (int f = 0; f < 4; ++f) {
             const int r = rr0 + 8 * f;
             const bool ok = m0 + r < m_hi;
+            float4 pv = rp[f], qv = rq[f];
+            if (PR) {
+                const int64_t mc = ok ? m0 + r : m_lo;
+                const int rr = (int)(mc & 31);
+                const int i = (rr & 3) + 4 * (rr >> 3);  // C-layout element of the row
+                const float gx = rp[f].x, gy = d_out > 1 ? rp[f].y : 0.f;
+                const uint32_t wx = rm[f].x, wy = rm[f].y;
+                pv.x = (wx >> i) & 1u ? top_unit(gx, gy, wo0[0], wo1[0]) : 0.f;
+                pv.y = (wx >> (16 + i)) & 1u ? top_unit(gx, gy, wo0[1], wo1[1]) : 0.f;
+                pv.z = (wy >> i) & 1u ? top_unit(gx, gy, wo0[2], wo1[2]) : 0.f;
+                pv.w = (wy >> (16 + i)) & 1u ? top_unit(gx, gy, wo0[3], wo1[3]) : 0.f;
+            }
+            if (QR) {
+                float4 x = rq[f];
+                x.y = d_in > 1 ? x.y : 0.f;
+                x.z = d_in > 2 ? x.z : 0.f;
+                x.w = d_in > 3 ? x.w : 0.f;
+                qv.x = layer0_unit(x, w0[0][0], w0[0][1], w0[0][2], w0[0][3], b0[0]);
+                qv.y = layer0_unit(x, w0[1][0], w0[1][1], w0[1][2], w0[1][3], b0[1]);
+                qv.z = layer0_unit(x, w0[2][0], w0[2][1], w0[2][2], w0[2][3], b0[2]);
+                qv.w = layer0_unit(x, w0[3][0], w0[3][1], w0[3][2], w0[3][3], b0[3]);
+            }
             *reinterpret_cast<float4*>(Ps + (buf * WG_MC + r) * WA_LD + 4 * c4) =
-                sel4(ok && pc_ok, rp[f]);
+                sel4(ok && pc_ok, pv);
             *reinterpret_cast<float4*>(Qs + (buf * WG_MC + r) * WA_LD + 4 * c4) =
-                sel4(ok && qc_ok, rq[f]);
+                sel4(ok && qc_ok, qv);
         }
     };
-    float4 rp[4], rq[4];
     const int nch = (int)((m_hi - m_lo + WG_MC - 1) / WG_MC);
     if (nch > 0) {
-        load(m_lo, rp, rq);
-        store(0, m_lo, rp, rq);
+        load(m_lo);
+        store(0, m_lo);
     }
     __syncthreads();
     for (int c = 0; c < nch; ++c) {
-        if (c + 1 < nch) load(m_lo + (int64_t)(c + 1) * WG_MC, rp, rq);
+        if (c + 1 < nch) load(m_lo + (int64_t)(c + 1) * WG_MC);
         const int buf = c & 1;
         const float* pb = Ps + buf * WG_MC * WA_LD;
         const float* qb = Qs + buf * WG_MC * WA_LD;
@@ -627,7 +863,7 @@ NAV_DEV void wgrad_hidden(const WgradArgs& a, int job, int split, float* smem) {
             // the scheduler cannot sink the reads onto their uses)
             const float* pw = pb + h * WA_LD + wn + l32;
             const float* qw = qb + h * WA_LD + wk + l32;
-            float a0 = pw[0], a1 = pw[32], b0 = qw[0], b1 = qw[32];
+            float a0 = pw[0], a1 = pw[32], bq0 = qw[0], bq1 = qw[32];
 #pragma unroll
             for (int s = 0; s < WG_MC / 2; ++s) {
                 float a0n = 0.f, a1n = 0.f, b0n = 0.f, b1n = 0.f;
@@ -639,35 +875,30 @@ NAV_DEV void wgrad_hidden(const WgradArgs& a, int job, int split, float* smem) {
                     b1n = qw[o + 32];
                 }
                 __builtin_amdgcn_sched_barrier(0);
-                acc[0][0] = mfma(a0, b0, acc[0][0]);
-                acc[0][1] = mfma(a0, b1, acc[0][1]);
-                acc[1][0] = mfma(a1, b0, acc[1][0]);
-                acc[1][1] = mfma(a1, b1, acc[1][1]);
+                acc[0][0] = mfma(a0, bq0, acc[0][0]);
+                acc[0][1] = mfma(a0, bq1, acc[0][1]);
+                acc[1][0] = mfma(a1, bq0, acc[1][0]);
+                acc[1][1] = mfma(a1, bq1, acc[1][1]);
                 __builtin_amdgcn_sched_barrier(0);
-                a0 = a0n; a1 = a1n; b0 = b0n; b1 = b1n;
+                a0 = a0n; a1 = a1n; bq0 = b0n; bq1 = b1n;
             }
         } else {
 #pragma unroll
             for (int s = 0; s < WG_MC / 2; ++s) {
                 const int row = 2 * s + h;
                 const float a0 = pb[row * WA_LD + wn + l32], a1 = pb[row * WA_LD + wn + 32 + l32];
-                const float b0 = qb[row * WA_LD + wk + l32], b1 = qb[row * WA_LD + wk + 32 + l32];
-                if (n0k && k0k) acc[0][0] = mfma(a0, b0, acc[0][0]);
-                if (n0k && k1k) acc[0][1] = mfma(a0, b1, acc[0][1]);
-                if (n1k && k0k) acc[1][0] = mfma(a1, b0, acc[1][0]);
-                if (n1k && k1k) acc[1][1] = mfma(a1, b1, acc[1][1]);
+                const float bq0 = qb[row * WA_LD + wk + l32], bq1 = qb[row * WA_LD + wk + 32 + l32];
+                if (n0k && k0k) acc[0][0] = mfma(a0, bq0, acc[0][0]);
+                if (n0k && k1k) acc[0][1] = mfma(a0, bq1, acc[0][1]);
+                if (n1k && k0k) acc[1][0] = mfma(a1, bq0, acc[1][0]);
+                if (n1k && k1k) acc[1][1] = mfma(a1, bq1, acc[1][1]);
             }
         }
-        if (colsum) {
-#pragma unroll
-            for (int r = 0; r < WG_MC / 2; ++r) cs += pb[(2 * r + (tid >> 7)) * WA_LD + (tid & 127)];
-        }
         __builtin_amdgcn_sched_barrier(0);
-        if (c + 1 < nch) store(buf ^ 1, m_lo + (int64_t)(c + 1) * WG_MC, rp, rq);
+        if (c + 1 < nch) store(buf ^ 1, m_lo + (int64_t)(c + 1) * WG_MC);
         __syncthreads();
     }
-    float* out = a.slabs + (int64_t)split * net.count;
-    float* o = out + net.w_off[L];
+    float* o = a.slabs + (int64_t)split * hidden_w_count(net) + (int64_t)(L - 1) * hp * hp;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -677,180 +908,81 @@ NAV_DEV void wgrad_hidden(const WgradArgs& a, int job, int split, float* smem) {
 #pragma unroll
             for (int e = 0; e < 16; ++e) o[(int64_t)(nb + acc_row(e, h)) * hp + kb + l32] = acc[i][j][e];
         }
-    if (!colsum) return;
-    red[tid] = cs;
-    __syncthreads();
-    if (tid < WA_W && n0 + tid < hp) out[net.b_off[L] + n0 + tid] = red[tid] + red[WA_W + tid];
 }
 
-// Edge layers, one 64-column panel per job (VALU, K = d_in or d_out):
-//  kind B (layer 0): dW_0 = dz_0^T x and db_0 = column sums of dz_0;
-//  kind C (output layer): dW_o = dy^T act_top and db_o = sums of dy.
-NAV_DEV void wgrad_edge(const WgradArgs& a, int job, int split, float* smem) {
-    typedef float Panel[WG_MC][WG_LD];
-    Panel* pa = reinterpret_cast<Panel*>(smem);                       // [2]
-    float (*sm)[WG_MC][4] = reinterpret_cast<float (*)[WG_MC][4]>(smem + 2 * WG_MC * WG_LD);
-    float (*red)[64][6] = reinterpret_cast<float (*)[64][6]>(smem + 2 * WG_MC * WG_LD +
-                                                              2 * WG_MC * 4);
-    const MlpDev& net = a.net;
-    const int hp = net.hp, T = a.T, nh = net.n_hidden;
-    const int kind = job < T ? 1 : 2;
-    const int tcol = kind == 1 ? job : job - T;
-    const int c0 = tcol * 64;
-    const int64_t MH = a.M * hp;
-    const float* src = kind == 1 ? a.dz : a.acts + (int64_t)(nh - 1) * MH;
-    const int tid = threadIdx.x;
-    const int64_t per = (a.M + a.splits - 1) / a.splits;
-    const int64_t m_lo = (int64_t)split * per;
-    const int64_t m_hi = m_lo + per < a.M ? m_lo + per : a.M;
-    const int d_in = net.d_in, d_out = net.d_out;
-    // thread = (column c = tid & 63, row group g = tid >> 6: rows g, g+4, ..)
-    const int vc = tid & 63, vg = tid >> 6;
-    float va[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    auto load = [&](int64_t m0, float4 (&ra)[2], float4& rs) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int i = tid + kBlock * j;
-            const int rr = i >> 4, cc = (i & 15) * 4;
-            const int64_t m = m0 + rr;
-            ra[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (m < m_hi && c0 + cc < hp)
-                ra[j] = *reinterpret_cast<const float4*>(src + m * hp + c0 + cc);
-        }
-        rs = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (tid < WG_MC && m0 + tid < m_hi) {
-            const int64_t m = m0 + tid;
-            if (kind == 1) {
-                const float* x = a.in + m * a.ld_in + a.in_col;
-                rs.x = x[0];
-                if (d_in > 1) rs.y = x[1];
-                if (d_in > 2) rs.z = x[2];
-                if (d_in > 3) rs.w = x[3];
-            } else {
-                rs.x = a.dy[m * d_out];
-                if (d_out > 1) rs.y = a.dy[m * d_out + 1];
-            }
-        }
-    };
-    auto store = [&](int buf, float4 (&ra)[2], float4 rs) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int i = tid + kBlock * j;
-            const int rr = i >> 4, cc = (i & 15) * 4;
-            *reinterpret_cast<float4*>(&pa[buf][rr][cc]) = ra[j];
-        }
-        if (tid < WG_MC) *reinterpret_cast<float4*>(&sm[buf][tid][0]) = rs;
-    };
-    float4 ra[2], rs;
-    const int nch = (int)((m_hi - m_lo + WG_MC - 1) / WG_MC);
-    if (nch > 0) {
-        load(m_lo, ra, rs);
-        store(0, ra, rs);
-    }
-    __syncthreads();
-    for (int c = 0; c < nch; ++c) {
-        if (c + 1 < nch) load(m_lo + (int64_t)(c + 1) * WG_MC, ra, rs);
-        const int buf = c & 1;
-        if (kind == 1) {
-#pragma unroll
-            for (int rr = vg; rr < WG_MC; rr += 4) {
-                const float g = pa[buf][rr][vc];
-                const float4 x = *reinterpret_cast<const float4*>(&sm[buf][rr][0]);
-                va[0] = fmaf(g, x.x, va[0]);
-                va[1] = fmaf(g, x.y, va[1]);
-                va[2] = fmaf(g, x.z, va[2]);
-                va[3] = fmaf(g, x.w, va[3]);
-                va[4] += g;
-            }
-        } else {
-#pragma unroll
-            for (int rr = vg; rr < WG_MC; rr += 4) {
-                const float x = pa[buf][rr][vc];
-                const float4 g = *reinterpret_cast<const float4*>(&sm[buf][rr][0]);
-                va[0] = fmaf(g.x, x, va[0]);
-                va[1] = fmaf(g.y, x, va[1]);
-                va[2] += g.x;
-                va[3] += g.y;
-            }
-        }
-        if (c + 1 < nch) store(buf ^ 1, ra, rs);
-        __syncthreads();
-    }
-    float* out = a.slabs + (int64_t)split * net.count;
-    // reduce the 4 row groups of the VALU accumulators
-#pragma unroll
-    for (int q = 0; q < 6; ++q) red[vg][vc][q] = va[q];
-    __syncthreads();
-    if (tid >= 64) return;
-    float s[6];
-#pragma unroll
-    for (int q = 0; q < 6; ++q) s[q] = red[0][tid][q] + red[1][tid][q] + red[2][tid][q] + red[3][tid][q];
-    const int n = c0 + tid;
-    if (kind == 1) {
-        if (n < hp) {
-            for (int k = 0; k < d_in; ++k) out[net.w_off[0] + n * d_in + k] = s[k];
-            out[net.b_off[0] + n] = s[4];
-        }
-    } else {
-        if (n < hp) {
-            out[net.w_off[nh] + n] = s[0];
-            if (d_out > 1) out[net.w_off[nh] + hp + n] = s[1];
-        }
-        if (tcol == 0 && tid == 0) {
-            out[net.b_off[nh]] = s[2];
-            if (d_out > 1) out[net.b_off[nh] + 1] = s[3];
-        }
-    }
-}
-
-// One launch computes every parameter gradient of a network. The 1-D grid lists the hidden-layer
-// 128x128 MFMA tiles of every row split first, then the edge panels (T layer-0 + T output) of
-// every split: the dispatcher hands out the MFMA-bound blocks one per CU before the VALU/memory
-// bound edge blocks fill the second slots, so the two kinds share CUs instead of stacking up.
+// One launch per network: the 1-D grid lists the hidden-layer 128x128 tiles of every row split.
+// Which operand is recomputed depends on the layer (top: P, layer 1: Q), chosen per block.
 __global__ __launch_bounds__(kBlock) void k_wgrad(WgradArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int b = blockIdx.x;
-    const int n_hid_blocks = a.n_hid * a.splits;
-    if (b < n_hid_blocks) {
-        const int job = b % a.n_hid, split = b / a.n_hid;
-        // tiles entirely inside hp take the branch-free MFMA body
-        const int TA = a.TA, t = job % (TA * TA);
-        const bool full = (t / TA + 1) * WA_W <= a.net.hp && (t % TA + 1) * WA_W <= a.net.hp;
-        if (full)
-            wgrad_hidden<true>(a, job, split, smem);
-        else
-            wgrad_hidden<false>(a, job, split, smem);
+    const int job = b % a.n_hid, split = b / a.n_hid;
+    const int TA = a.TA, t = job % (TA * TA);
+    const int L = job / (TA * TA) + 1, nh = a.net.n_hidden;
+    // tiles entirely inside hp take the branch-free MFMA body
+    const bool full = (t / TA + 1) * WA_W <= a.net.hp && (t % TA + 1) * WA_W <= a.net.hp;
+    const bool pr = L == nh - 1, qr = L == 1;
+#define NAV_WG(F)                                                                       \
+    if (pr && qr) wgrad_hidden<F, true, true>(a, job, split, smem);                     \
+    else if (pr) wgrad_hidden<F, true, false>(a, job, split, smem);                     \
+    else if (qr) wgrad_hidden<F, false, true>(a, job, split, smem);                     \
+    else wgrad_hidden<F, false, false>(a, job, split, smem);
+    if (full) {
+        NAV_WG(true)
     } else {
-        const int e = b - n_hid_blocks, ne = 2 * a.T;
-        wgrad_edge(a, e % ne, e / ne, smem);
+        NAV_WG(false)
     }
+#undef NAV_WG
 }
 
-// grad = sum of the split slabs, in a fixed order: block = 64 float4 columns x 4 split groups
-// (group g sums splits g, g+4, ..), the 4 group sums added in order through LDS.
-__global__ __launch_bounds__(kBlock) void k_grad_reduce(const float4* __restrict__ slabs,
-                                                        int splits, int64_t n4,
+// grad = hidden-W entries: sum of the weight-gradient split slabs (block = 64 float4 columns x 4
+// split groups, the group sums added in order through LDS); every other entry: sum of the
+// per-row-block edge slabs (one wave per float4, lanes take blocks b = lane, lane + 64, ..., a
+// fixed xor tree adds the lanes). Deterministic: the same order on every run.
+__global__ __launch_bounds__(kBlock) void k_grad_reduce(MlpDev net, const float4* __restrict__ hs,
+                                                        int splits, int64_t hw4, int nbh,
+                                                        const float4* __restrict__ es,
+                                                        int64_t nblk, int64_t e4,
                                                         float4* __restrict__ grad) {
     __shared__ float4 part[4][64];
     const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
-    const int64_t i = (int64_t)blockIdx.x * 64 + c;
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (i < n4) {
+    if ((int)blockIdx.x < nbh) {
+        const int64_t i = (int64_t)blockIdx.x * 64 + c;
+        float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (i < hw4) {
 #pragma unroll 4
-        for (int k = g; k < splits; k += 4) {
-            const float4 v = slabs[(int64_t)k * n4 + i];
-            s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+            for (int k = g; k < splits; k += 4) {
+                const float4 v = hs[(int64_t)k * hw4 + i];
+                s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+            }
         }
-    }
-    part[g][c] = s;
-    __syncthreads();
-    if (g != 0 || i >= n4) return;
-    float4 r = part[0][c];
+        part[g][c] = s;
+        __syncthreads();
+        if (g != 0 || i >= hw4) return;
+        float4 r = part[0][c];
 #pragma unroll
-    for (int q = 1; q < 4; ++q) {
-        r.x += part[q][c].x; r.y += part[q][c].y; r.z += part[q][c].z; r.w += part[q][c].w;
+        for (int q = 1; q < 4; ++q) {
+            r.x += part[q][c].x; r.y += part[q][c].y; r.z += part[q][c].z; r.w += part[q][c].w;
+        }
+        const int64_t per = (int64_t)net.hp * net.hp / 4;
+        const int L = (int)(i / per) + 1;
+        grad[net.w_off[L] / 4 + i % per] = r;
+        return;
     }
-    grad[i] = r;
+    const int64_t o = ((int64_t)blockIdx.x - nbh) * 4 + g;
+    if (o >= e4) return;  // wave-uniform
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t b = c; b < nblk; b += 64) {
+        const float4 v = es[b * e4 + o];
+        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) {
+        s.x += __shfl_xor(s.x, d, 64);
+        s.y += __shfl_xor(s.y, d, 64);
+        s.z += __shfl_xor(s.z, d, 64);
+        s.w += __shfl_xor(s.w, d, 64);
+    }
+    if (c == 0) grad[edge_to_flat(net, 4 * o) / 4] = s;
 }
 
 // ---------------- optimizer / target update, refreshing the packed images ----------------
@@ -946,42 +1078,6 @@ __global__ __launch_bounds__(kBlock) void k_replay_sample(const float4* __restri
     }
     batch[2 * b] = rows[2 * k];
     batch[2 * b + 1] = rows[2 * k + 1];
-}
-
-__global__ __launch_bounds__(kBlock) void k_critic_loss(int64_t B, const float* __restrict__ bt,
-                                                        const float* q1t, const float* q2t,
-                                                        const float* q1, const float* q2,
-                                                        float gamma, float norm, float* dq1,
-                                                        float* dq2, float* y_out,
-                                                        float* loss_part) {
-    const int64_t b = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    float l1 = 0.f, l2 = 0.f;
-    if (b < B) {
-        // robot.py:331-345: y = r + gamma * min(q1', q2') * (1 - done)
-        const float r = bt[b * NAV_ROW + 4], d = bt[b * NAV_ROW + 7];
-        const float nd = 1.0f - d;
-        const float mn = fminf(q1t[b], q2t[b]);
-        const float y = r + (gamma * mn) * nd;
-        // torch mse_loss backward: (q - y) * (2/B)
-        const float e1 = q1[b] - y, e2 = q2[b] - y;
-        dq1[b] = e1 * norm;
-        dq2[b] = e2 * norm;
-        if (y_out) y_out[b] = y;
-        l1 = e1 * e1;
-        l2 = e2 * e2;
-    }
-    if (loss_part) {
-        __shared__ float part[kBlock / 64][2];
-        const float s1 = wave_sum(l1), s2 = wave_sum(l2);
-        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-        if (lane == 0) { part[wv][0] = s1; part[wv][1] = s2; }
-        __syncthreads();
-        if (threadIdx.x < 2) {
-            float acc = 0.f;
-            for (int w = 0; w < kBlock / 64; ++w) acc += part[w][threadIdx.x];
-            loss_part[(int64_t)blockIdx.x * 2 + threadIdx.x] = acc;
-        }
-    }
 }
 
 __global__ __launch_bounds__(kBlock) void k_fill(float* x, int64_t n, float v) {
@@ -1134,7 +1230,8 @@ int nav_mlp_forward(const nav_mlp* nets, int32_t n_nets, int64_t M, const float*
                     int32_t ld_in, int32_t in_col, float* const* out, int32_t ld_out,
                     int32_t out_col, int32_t out_mode, const float* eps, float policy_noise,
                     float noise_clip, float max_action, uint32_t seed_lo, uint32_t seed_hi,
-                    uint32_t counter, float* const* acts, uint16_t* const* masks, void* stream) {
+                    uint32_t counter, float* const* acts, uint32_t save_mask,
+                    uint16_t* const* masks, void* stream) {
     FwdArgs a{};
     if (!nets || n_nets < 1 || n_nets > 2 || M < 0 || !out) return NAV_EINVAL;
     for (int i = 0; i < n_nets; ++i) {
@@ -1154,6 +1251,7 @@ int nav_mlp_forward(const nav_mlp* nets, int32_t n_nets, int64_t M, const float*
     a.in_col = in_col;
     a.ld_out = ld_out;
     a.out_col = out_col;
+    a.save_mask = save_mask;
     a.eps = eps;
     a.policy_noise = policy_noise;
     a.noise_clip = noise_clip;
@@ -1169,33 +1267,105 @@ int nav_mlp_forward(const nav_mlp* nets, int32_t n_nets, int64_t M, const float*
     return NAV_EINVAL;
 }
 
+int64_t nav_mlp_row_blocks(int64_t M) {
+    if (M < 0) return NAV_EINVAL;
+    const int64_t tm = (int64_t)row_tiles() * 32;
+    return (M + tm - 1) / tm;
+}
+
+int64_t nav_mlp_edge_count(int32_t d_in, int32_t d_out, int32_t hidden_pad, int32_t n_hidden) {
+    nav_mlp n{d_in, d_out, hidden_pad, hidden_pad, n_hidden, reinterpret_cast<float*>(16),
+              reinterpret_cast<float*>(16)};
+    MlpDev d;
+    if (!make_dev(&n, &d)) return NAV_EINVAL;
+    return edge_count(d);
+}
+
+int64_t nav_mlp_hidden_count(int32_t hidden_pad, int32_t n_hidden) {
+    if (hidden_pad < 32 || hidden_pad > 256 || (hidden_pad & 31) || n_hidden < 1)
+        return NAV_EINVAL;
+    return (int64_t)(n_hidden - 1) * hidden_pad * hidden_pad;
+}
+
+int nav_td3_critic_forward(const nav_mlp* nets, int64_t B, const float* in, int32_t ld_in,
+                           int32_t in_col, const float* batch, const float* q1t, const float* q2t,
+                           float gamma, float* const* dq, float* const* loss_part,
+                           float* const* edge_slabs, float* const* acts, uint32_t save_mask,
+                           uint16_t* const* masks, void* stream) {
+    FwdArgs a{};
+    if (!nets || B < 1 || !in || !batch || !q1t || !q2t || !dq || !loss_part || !masks)
+        return NAV_EINVAL;
+    for (int i = 0; i < 2; ++i) {
+        if (!make_dev(&nets[i], &a.net[i]) || nets[i].d_out != 1 || !dq[i] || !loss_part[i] ||
+            !masks[i])
+            return NAV_EINVAL;
+        if (a.net[i].hp != a.net[0].hp || a.net[i].d_in != a.net[0].d_in ||
+            a.net[i].n_hidden != a.net[0].n_hidden)
+            return NAV_EINVAL;
+        a.out[i] = dq[i];  // unused by OUT_LOSS, non-null for uniformity
+        a.acts[i] = acts ? acts[i] : nullptr;
+        if (save_mask && !a.acts[i]) return NAV_EINVAL;
+        a.masks[i] = masks[i];
+        a.dq[i] = dq[i];
+        a.loss_part[i] = loss_part[i];
+        a.eslab[i] = edge_slabs ? edge_slabs[i] : nullptr;
+    }
+    if (in_col < 0 || in_col + a.net[0].d_in > ld_in) return NAV_EINVAL;
+    a.M = B;
+    a.in = in;
+    a.ld_in = ld_in;
+    a.in_col = in_col;
+    a.save_mask = save_mask;
+    a.batch = batch;
+    a.qt[0] = q1t;
+    a.qt[1] = q2t;
+    a.gamma = gamma;
+    a.norm = (float)(2.0 / (double)B);
+    a.ecount = edge_count(a.net[0]);
+    return launch_fwd<IN_F32, OUT_LOSS>(a, 2, S(stream));
+}
+
 int64_t nav_mlp_mask_count(int32_t hidden_pad, int32_t n_hidden, int64_t M) {
     if (hidden_pad < 32 || hidden_pad > 256 || (hidden_pad & 31) || n_hidden < 1 || M < 0)
         return NAV_EINVAL;
     return (int64_t)n_hidden * mask_rowtiles(M) * (hidden_pad / 32) * 64;
 }
 
-int nav_mlp_backward(const nav_mlp* net, int64_t M, const float* dy, const uint16_t* masks,
-                     float* dz, float* dx, void* stream) {
+int nav_mlp_backward(const nav_mlp* net, int64_t M, const float* dy, int32_t ld_dy,
+                     const uint16_t* masks, const float* in, int32_t ld_in, int32_t in_col,
+                     const float* h_top, float* dz, uint32_t save_mask, float* dx,
+                     float* edge_slabs, void* stream) {
     BwdArgs a{};
-    if (!make_dev(net, &a.net) || M < 0) return NAV_EINVAL;
+    if (!make_dev(net, &a.net) || M < 0 || ld_dy < 0) return NAV_EINVAL;
     if (M == 0) return 0;
-    if (!dy || !masks || !dz) return NAV_EINVAL;
+    if (!dy || !masks || (save_mask && !dz) || (save_mask >> net->n_hidden) ||
+        (edge_slabs && (!in || in_col < 0 || in_col + net->d_in > ld_in)))
+        return NAV_EINVAL;
     a.M = M;
     a.dy = dy;
+    a.ld_dy = ld_dy;
     a.masks = masks;
+    a.in = in;
+    a.ld_in = ld_in;
+    a.in_col = in_col;
+    a.h_top = h_top;
     a.dz = dz;
+    a.save_mask = save_mask;
     a.dx = dx;
+    a.eslab = edge_slabs;
+    a.ecount = edge_count(a.net);
     return launch_bwd(a, S(stream));
 }
 
 int nav_mlp_wgrad(const nav_mlp* net, int64_t M, const float* in, int32_t ld_in, int32_t in_col,
-                  const float* acts, const float* dz, const float* dy, float* slabs,
-                  int32_t splits, void* stream) {
+                  const float* acts, const float* dz, const float* dy, int32_t ld_dy,
+                  const uint16_t* masks, float* slabs, int32_t splits, void* stream) {
     WgradArgs a{};
-    if (!make_dev(net, &a.net) || M < 1 || splits < 1 || !in || !acts || !dz || !dy || !slabs ||
-        in_col < 0 || in_col + net->d_in > ld_in)
+    if (!make_dev(net, &a.net) || M < 1 || splits < 1 || !in || !dy || ld_dy < 0 || !masks ||
+        !slabs || in_col < 0 || in_col + net->d_in > ld_in ||
+        (net->n_hidden > 2 && (!acts || !dz)))
         return NAV_EINVAL;
+    if (net->n_hidden < 2) return 0;
     a.M = M;
     a.in = in;
     a.ld_in = ld_in;
@@ -1203,27 +1373,32 @@ int nav_mlp_wgrad(const nav_mlp* net, int64_t M, const float* in, int32_t ld_in,
     a.acts = acts;
     a.dz = dz;
     a.dy = dy;
+    a.ld_dy = ld_dy;
+    a.masks = masks;
     a.slabs = slabs;
     a.splits = splits;
-    a.T = (a.net.hp + 63) / 64;
     a.TA = (a.net.hp + WA_W - 1) / WA_W;
     a.n_hid = (a.net.n_hidden - 1) * a.TA * a.TA;
     const size_t lds = wgrad_lds_bytes();
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wgrad),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(k_wgrad, dim3((unsigned)((a.n_hid + 2 * a.T) * splits)), dim3(kBlock), lds,
-                       S(stream), a);
+    hipLaunchKernelGGL(k_wgrad, dim3((unsigned)(a.n_hid * splits)), dim3(kBlock), lds, S(stream),
+                       a);
     NAV_CHECK_LAUNCH();
     return 0;
 }
 
-int nav_grad_reduce(const float* slabs, int32_t splits, int64_t count, float* grad,
-                    void* stream) {
-    if (!slabs || !grad || splits < 1 || count < 0 || (count & 3)) return NAV_EINVAL;
-    if (count == 0) return 0;
-    const int64_t n4 = count / 4;
-    hipLaunchKernelGGL(k_grad_reduce, dim3((unsigned)((n4 + 63) / 64)), dim3(kBlock), 0, S(stream),
-                       reinterpret_cast<const float4*>(slabs), splits, n4,
+int nav_grad_reduce(const nav_mlp* net, const float* hidden_slabs, int32_t splits,
+                    const float* edge_slabs, int64_t edge_blocks, float* grad, void* stream) {
+    MlpDev d;
+    if (!make_dev(net, &d) || !grad || !edge_slabs || edge_blocks < 1 ||
+        (d.n_hidden > 1 && (!hidden_slabs || splits < 1)))
+        return NAV_EINVAL;
+    const int64_t hw4 = hidden_w_count(d) / 4, e4 = edge_count(d) / 4;
+    const int nbh = (int)((hw4 + 63) / 64), nbe = (int)((e4 + 3) / 4);
+    hipLaunchKernelGGL(k_grad_reduce, dim3((unsigned)(nbh + nbe)), dim3(kBlock), 0, S(stream), d,
+                       reinterpret_cast<const float4*>(hidden_slabs), splits, hw4, nbh,
+                       reinterpret_cast<const float4*>(edge_slabs), edge_blocks, e4,
                        reinterpret_cast<float4*>(grad));
     NAV_CHECK_LAUNCH();
     return 0;
@@ -1281,21 +1456,6 @@ int nav_replay_sample(const nav_replay* replay, int64_t size, int64_t B, const i
                        seed_hi, counter, reinterpret_cast<float4*>(batch));
     NAV_CHECK_LAUNCH();
     return 0;
-}
-
-int nav_td3_critic_loss(int64_t B, const float* batch, const float* q1t, const float* q2t,
-                        const float* q1, const float* q2, float gamma, float* dq1, float* dq2,
-                        float* y_out, float* loss_part, void* stream) {
-    if (B < 1 || !batch || !q1t || !q2t || !q1 || !q2 || !dq1 || !dq2) return NAV_EINVAL;
-    const float norm = (float)(2.0 / (double)B);
-    hipLaunchKernelGGL(k_critic_loss, dim3(blocks_for(B)), dim3(kBlock), 0, S(stream), B, batch,
-                       q1t, q2t, q1, q2, gamma, norm, dq1, dq2, y_out, loss_part);
-    NAV_CHECK_LAUNCH();
-    return 0;
-}
-
-int nav_batch_sa(int64_t B, const float* batch, float* sa, void* stream) {
-    return nav_strided_copy(batch, NAV_ROW, 0, sa, 4, 0, B, 4, stream);
 }
 
 int nav_fill(float* x, int64_t n, float value, void* stream) {

@@ -12,7 +12,7 @@ import torch  # noqa: F401  (must be loaded first: provides the HIP runtime)
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libnavenv.so")
 NAV_EINVAL = -100000
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 _dp = C.POINTER(C.c_double)
 _vp = C.c_void_p
@@ -88,28 +88,33 @@ SIGNATURES = [
     ("nav_mlp_forward", C.c_int, [_P(NavMlp), C.c_int32, C.c_int64, _vp, C.c_int32, C.c_int32,
                                   _P(_vp), C.c_int32, C.c_int32, C.c_int32, _vp, C.c_float,
                                   C.c_float, C.c_float, C.c_uint32, C.c_uint32, C.c_uint32,
-                                  _P(_vp), _P(_vp), _vp]),
+                                  _P(_vp), C.c_uint32, _P(_vp), _vp]),
     ("nav_mlp_mask_count", C.c_int64, [C.c_int32, C.c_int32, C.c_int64]),
-    ("nav_mlp_backward", C.c_int, [_P(NavMlp), C.c_int64, _vp, _vp, _vp, _vp, _vp]),
+    ("nav_mlp_row_blocks", C.c_int64, [C.c_int64]),
+    ("nav_mlp_edge_count", C.c_int64, [C.c_int32] * 4),
+    ("nav_mlp_hidden_count", C.c_int64, [C.c_int32] * 2),
+    ("nav_td3_critic_forward", C.c_int, [_P(NavMlp), C.c_int64, _vp, C.c_int32, C.c_int32, _vp,
+                                         _vp, _vp, C.c_float, _P(_vp), _P(_vp), _P(_vp),
+                                         _P(_vp), C.c_uint32, _P(_vp), _vp]),
+    ("nav_mlp_backward", C.c_int, [_P(NavMlp), C.c_int64, _vp, C.c_int32, _vp, _vp, C.c_int32,
+                                   C.c_int32, _vp, _vp, C.c_uint32, _vp, _vp, _vp]),
     ("nav_mlp_wgrad", C.c_int, [_P(NavMlp), C.c_int64, _vp, C.c_int32, C.c_int32, _vp, _vp, _vp,
-                                _vp, C.c_int32, _vp]),
-    ("nav_grad_reduce", C.c_int, [_vp, C.c_int32, C.c_int64, _vp, _vp]),
+                                C.c_int32, _vp, _vp, C.c_int32, _vp]),
+    ("nav_grad_reduce", C.c_int, [_P(NavMlp), _vp, C.c_int32, _vp, C.c_int64, _vp, _vp]),
     ("nav_adam", C.c_int, [_P(NavMlp), _vp, _vp, _vp, C.c_float, C.c_float, C.c_float,
                            C.c_float, C.c_float, _vp]),
     ("nav_polyak", C.c_int, [_P(NavMlp), _P(NavMlp), C.c_float, _vp]),
     ("nav_mlp_pack", C.c_int, [_P(NavMlp), _vp]),
     ("nav_replay_sample", C.c_int, [_P(NavReplay), C.c_int64, C.c_int64, _vp, C.c_uint32,
                                     C.c_uint32, C.c_uint32, _vp, _vp]),
-    ("nav_td3_critic_loss", C.c_int, [C.c_int64, _vp, _vp, _vp, _vp, _vp, C.c_float, _vp, _vp,
-                                      _vp, _vp, _vp]),
-    ("nav_batch_sa", C.c_int, [C.c_int64, _vp, _vp, _vp]),
     ("nav_fill", C.c_int, [_vp, C.c_int64, C.c_float, _vp]),
     ("nav_strided_copy", C.c_int, [_vp, C.c_int32, C.c_int32, _vp, C.c_int32, C.c_int32,
                                    C.c_int64, C.c_int32, _vp]),
 ]
 
 # Entry points that return int64 counts (negative = error) rather than a status code.
-_COUNT_FNS = {"nav_mlp_param_count", "nav_mlp_packed_count", "nav_mlp_mask_count"}
+_COUNT_FNS = {"nav_mlp_param_count", "nav_mlp_packed_count", "nav_mlp_mask_count",
+              "nav_mlp_row_blocks", "nav_mlp_edge_count", "nav_mlp_hidden_count"}
 
 
 class NavError(RuntimeError):

@@ -51,6 +51,14 @@ class DeviceMLP:
                    self.params.data_ptr(), self.packed.data_ptr())
         return d
 
+    def middle_layers(self):
+        """save_mask bits of the hidden layers 1 .. n_hidden-2: the only activations / dz rows the
+        weight-gradient kernel reads (h_0 and the top dz are recomputed)."""
+        return sum(1 << l for l in range(1, self.n_hidden - 1))
+
+    def top_layer(self):
+        return 1 << (self.n_hidden - 1)
+
     def mask_buffer(self, M):
         """ReLU-derivative bit image for M rows (nav_mlp_mask_count u16 words)."""
         n = lib().nav_mlp_mask_count(self.hp, self.n_hidden, M)
@@ -120,8 +128,9 @@ class DeviceMLP:
 
 def forward(nets, inp, ld_in, in_col, outs, ld_out, out_col, M, out_mode=0, eps=None,
             policy_noise=0.2, noise_clip=0.5, max_action=5.0, seed=(0, 0), counter=0, acts=None,
-            masks=None, stream=None):
-    """nav_mlp_forward for 1 or 2 networks sharing `inp`."""
+            masks=None, save_mask=None, stream=None):
+    """nav_mlp_forward for 1 or 2 networks sharing `inp`. With `acts`, hidden layer L is saved
+    for bits L of save_mask (default: every layer)."""
     from ._lib import stream_handle
     n = len(nets)
     descs = (NavMlp * n)(*[x.desc() for x in nets])
@@ -133,9 +142,11 @@ def forward(nets, inp, ld_in, in_col, outs, ld_out, out_col, M, out_mode=0, eps=
     if masks is not None:
         masks_arr = (C.c_void_p * n)(*[(m.data_ptr() if m is not None else None) for m in masks])
     net = nets[0]
+    if save_mask is None:
+        save_mask = (1 << net.n_hidden) - 1 if acts is not None else 0
     flops = n * prof.mlp_fwd_flops(net.d_in, net.d_out, net.hidden, net.n_hidden, M)
     with prof.region("mlp_fwd", flops):
         lib().nav_mlp_forward(descs, n, M, ptr(inp), ld_in, in_col, out_arr, ld_out, out_col,
                               out_mode, ptr(eps), policy_noise, noise_clip, max_action,
-                              seed[0], seed[1], counter, acts_arr, masks_arr,
+                              seed[0], seed[1], counter, acts_arr, save_mask, masks_arr,
                               stream_handle(stream))

@@ -23,12 +23,18 @@ def mlp_fwd_flops(d_in, d_out, h, nh, rows):
     return 2.0 * rows * (d_in * h + (nh - 1) * h * h + h * d_out)
 
 
-def mlp_bwd_flops(d_in, d_out, h, nh, rows, dx=False):
-    return 2.0 * rows * (d_out * h + (nh - 1) * h * h + (h * d_in if dx else 0))
+def mlp_bwd_flops(d_in, d_out, h, nh, rows, dx=False, edges=False, wo=False):
+    """row backward (dy . Wo, (nh-1) hidden GEMMs, dx) plus, with edges, the per-block
+    parameter-gradient partials it sums: dW0 (2 d_in h), biases (nh h), dWo (2 d_out h)."""
+    f = d_out * h + (nh - 1) * h * h + (h * d_in if dx else 0)
+    if edges:
+        f += d_in * h + 0.5 * nh * h + (d_out * h if wo else 0)
+    return 2.0 * rows * f
 
 
-def mlp_wgrad_flops(d_in, d_out, h, nh, rows):
-    return 2.0 * rows * (d_in * h + (nh - 1) * h * h + h * d_out)
+def mlp_wgrad_flops(h, nh, rows):
+    """hidden x hidden weight gradients only (the edge layers are summed by fwd / bwd)."""
+    return 2.0 * rows * (nh - 1) * h * h
 
 
 def demo_flops(n_env, m):

@@ -13,7 +13,7 @@ import torch
 
 from . import config as K
 from . import prof
-from ._lib import lib, ptr, stream_handle
+from ._lib import NavMlp, lib, ptr, stream_handle
 from .mlp import DeviceMLP, forward
 
 
@@ -72,44 +72,58 @@ class TD3:
             return
         d, hp, nh = self.device, self.actor_network.hp, self.actor_network.n_hidden
         f = lambda *s: torch.zeros(*s, dtype=torch.float32, device=d)  # noqa: E731
+        L = lib()
         self.batch = f(B, 8)
         self.batch2 = f(B, 8)
-        self.sa = f(B, 4)
         self.tgt_in = f(B, 4)
-        self.q1t, self.q2t, self.q1, self.q2 = f(B), f(B), f(B), f(B)
-        self.dq1, self.dq2, self.y = f(B), f(B), f(B)
-        self.acts1, self.acts2 = f(nh, B, hp), f(nh, B, hp)
-        self.dz1, self.dz2 = f(nh, B, hp), f(nh, B, hp)
-        self.acts_a, self.dz_a = f(nh, B, hp), f(nh, B, hp)
+        self.q1t, self.q2t, self.q1 = f(B), f(B), f(B)
+        self.dq1, self.dq2 = f(B), f(B)
+        # train_actor: d(-mean Q)/dQ = -1/B for every row, one broadcast row (ld_dy = 0)
+        self.dq_actor = torch.full((1,), -1.0 / B, dtype=torch.float32, device=d)
+        # saved rows: only hidden layers 1 .. nh-2 (+ the actor's top layer for dWo); h_0 and the
+        # top dz are recomputed by the weight-gradient kernel
+        self.acts1, self.acts2, self.acts_a = f(nh, B, hp), f(nh, B, hp), f(nh, B, hp)
+        self.dz1, self.dz2, self.dz_a = f(nh, B, hp), f(nh, B, hp), f(nh, B, hp)
         self.mask1 = self.critic_network_1.mask_buffer(B)
         self.mask2 = self.critic_network_1.mask_buffer(B)
         self.mask_a = self.actor_network.mask_buffer(B)
         self.dx = f(B, 4)
-        self.da = f(B, 2)
-        self.loss_part = f((B + 255) // 256, 2)
+        self.nblk = L.nav_mlp_row_blocks(B)
+        self.loss_part = f(2, self.nblk)
+        ec = L.nav_mlp_edge_count(4, 1, hp, nh)
+        self.eslab1, self.eslab2 = f(self.nblk, ec), f(self.nblk, ec)
+        self.eslab_a = f(self.nblk, L.nav_mlp_edge_count(2, 2, hp, nh))
         self.splits = max(1, min(64, B // 512))
-        cmax = max(self.actor_network.count, self.critic_network_1.count)
-        self.slabs = f(self.splits, cmax)
+        self.hslab = f(self.splits, max(4, L.nav_mlp_hidden_count(hp, nh)))
         self.grad_a = f(self.actor_network.count)
         self.grad_c1 = f(self.critic_network_1.count)
         self.grad_c2 = f(self.critic_network_1.count)
         self._B = B
 
-    def _grads(self, net, M, inp, ld_in, in_col, acts, dz, dy, grad, s):
-        with prof.region("mlp_wgrad", prof.mlp_wgrad_flops(net.d_in, net.d_out, net.hidden,
-                                                             net.n_hidden, M)):
-            lib().nav_mlp_wgrad(C.byref(net.desc()), M, ptr(inp), ld_in, in_col, ptr(acts),
-                                ptr(dz), ptr(dy), ptr(self.slabs), self.splits, s)
-        with prof.region("grad_reduce", 4.0 * (self.splits + 1) * net.count):
-            lib().nav_grad_reduce(ptr(self.slabs), self.splits, net.count, ptr(grad), s)
+    def _grads(self, net, M, inp, ld_in, in_col, acts, dz, dy, ld_dy, masks, eslab, grad, s):
+        """Hidden weight gradients (MFMA, split-M slabs) + the fixed-order reduce that folds them
+        and the fwd/bwd edge partials into the flat gradient."""
+        d = C.byref(net.desc())
+        if net.n_hidden > 1:
+            with prof.region("mlp_wgrad", prof.mlp_wgrad_flops(net.hidden, net.n_hidden, M)):
+                lib().nav_mlp_wgrad(d, M, ptr(inp), ld_in, in_col, ptr(acts), ptr(dz), ptr(dy),
+                                    ld_dy, ptr(masks), ptr(self.hslab), self.splits, s)
+        nbytes = 4.0 * (self.splits * (net.count - eslab.shape[1]) + eslab.numel() + net.count)
+        with prof.region("grad_reduce", nbytes):
+            lib().nav_grad_reduce(d, ptr(self.hslab), self.splits, ptr(eslab), self.nblk,
+                                  ptr(grad), s)
         if self.grad_hook is not None:
             self.grad_hook(grad)
 
-    def _bwd(self, net, M, dy, masks, dz, dx, s):
+    def _bwd(self, net, M, dy, ld_dy, masks, s, inp=None, ld_in=0, in_col=0, h_top=None, dz=None,
+             save_mask=0, dx=None, eslab=None):
+        edges = eslab is not None
         with prof.region("mlp_bwd", prof.mlp_bwd_flops(net.d_in, net.d_out, net.hidden,
-                                                         net.n_hidden, M, dx is not None)):
-            lib().nav_mlp_backward(C.byref(net.desc()), M, ptr(dy), ptr(masks), ptr(dz),
-                                   ptr(dx), s)
+                                                         net.n_hidden, M, dx is not None, edges,
+                                                         h_top is not None)):
+            lib().nav_mlp_backward(C.byref(net.desc()), M, ptr(dy), ld_dy, ptr(masks), ptr(inp),
+                                   ld_in, in_col, ptr(h_top), ptr(dz), save_mask, ptr(dx),
+                                   ptr(eslab), s)
 
     def _sample(self, replay, B, out, idx=None, stream=None):
         """ReplayBuffer.sample (robot.py:98-115) into a [B][8] batch."""
@@ -135,25 +149,31 @@ class TD3:
                 counter=self.update_counter, stream=stream)
         forward([self.target_critic_network_1, self.target_critic_network_2], self.tgt_in, 4, 0,
                 [self.q1t, self.q2t], 1, 0, B, stream=stream)
-        lib().nav_batch_sa(B, ptr(bt), ptr(self.sa), s)
-        forward([self.critic_network_1, self.critic_network_2], self.sa, 4, 0,
-                [self.q1, self.q2], 1, 0, B, acts=[self.acts1, self.acts2],
-                masks=[self.mask1, self.mask2], stream=stream)
-        lib().nav_td3_critic_loss(B, ptr(bt), ptr(self.q1t), ptr(self.q2t), ptr(self.q1),
-                                  ptr(self.q2), c.gamma, ptr(self.dq1), ptr(self.dq2),
-                                  ptr(self.y), ptr(self.loss_part), s)
-        for net, opt, acts, mask, dz, dq, grad in (
-                (self.critic_network_1, self.critic_optimizer_1, self.acts1, self.mask1, self.dz1,
-                 self.dq1, self.grad_c1),
-                (self.critic_network_2, self.critic_optimizer_2, self.acts2, self.mask2, self.dz2,
-                 self.dq2, self.grad_c2)):
-            self._bwd(net, B, dq, mask, dz, None, s)
-            self._grads(net, B, self.sa, 4, 0, acts, dz, dq, grad, s)
+        # online twin forward on (s, a) = batch columns 0..3, fused with the TD target, the MSE
+        # gradient and the output layer's gradient partials
+        c1, c2 = self.critic_network_1, self.critic_network_2
+        mid = c1.middle_layers()
+        arr = lambda *t: (C.c_void_p * len(t))(*[x.data_ptr() for x in t])  # noqa: E731
+        descs = (NavMlp * 2)(c1.desc(), c2.desc())
+        with prof.region("mlp_fwd", 2 * prof.mlp_fwd_flops(4, 1, c1.hidden, c1.n_hidden, B)):
+            lib().nav_td3_critic_forward(descs, B, ptr(bt), 8, 0, ptr(bt), ptr(self.q1t),
+                                         ptr(self.q2t), c.gamma, arr(self.dq1, self.dq2),
+                                         arr(self.loss_part[0], self.loss_part[1]),
+                                         arr(self.eslab1, self.eslab2), arr(self.acts1, self.acts2),
+                                         mid, arr(self.mask1, self.mask2), s)
+        for net, opt, acts, mask, dz, dq, es, grad in (
+                (c1, self.critic_optimizer_1, self.acts1, self.mask1, self.dz1, self.dq1,
+                 self.eslab1, self.grad_c1),
+                (c2, self.critic_optimizer_2, self.acts2, self.mask2, self.dz2, self.dq2,
+                 self.eslab2, self.grad_c2)):
+            self._bwd(net, B, dq, 1, mask, s, inp=bt, ld_in=8, in_col=0, dz=dz, save_mask=mid,
+                      eslab=es)
+            self._grads(net, B, bt, 8, 0, acts, dz, dq, 1, mask, es, grad, s)
             opt.step(grad, stream)
 
     def critic_loss_values(self):
         """(loss1, loss2) of the last train_critic (mean squared TD error), synchronising."""
-        t = self.loss_part.sum(0) / self._B
+        t = self.loss_part.sum(1) / self._B
         return t[0].item(), t[1].item()
 
     # robot.py:369-398
@@ -164,18 +184,22 @@ class TD3:
         s = stream_handle(stream)
         self._sample(replay, B, self.batch2, idx, stream)
         bt = self.batch2
-        lib().nav_strided_copy(ptr(bt), 8, 0, ptr(self.sa), 4, 0, B, 2, s)
-        forward([self.actor_network], bt, 8, 0, [self.sa], 4, 2, B, acts=[self.acts_a],
-                masks=[self.mask_a], stream=stream)
-        forward([self.critic_network_1], self.sa, 4, 0, [self.q1], 1, 0, B, masks=[self.mask1],
-                stream=stream)
-        # d(-mean Q)/dQ = -1/B; backprop through critic 1 to its action input
-        lib().nav_fill(ptr(self.dq1), B, -1.0 / B, s)
-        self._bwd(self.critic_network_1, B, self.dq1, self.mask1, self.dz1, self.dx, s)
-        lib().nav_strided_copy(ptr(self.dx), 4, 2, ptr(self.da), 2, 0, B, 2, s)
         net = self.actor_network
-        self._bwd(net, B, self.da, self.mask_a, self.dz_a, None, s)
-        self._grads(net, B, bt, 8, 0, self.acts_a, self.dz_a, self.da, self.grad_a, s)
+        c1 = self.critic_network_1
+        # actor(s) overwrites the stored action (columns 2..3): the critic then reads (s, pi(s))
+        # straight from the batch rows
+        forward([net], bt, 8, 0, [bt], 8, 2, B, acts=[self.acts_a],
+                save_mask=net.middle_layers() | net.top_layer(), masks=[self.mask_a],
+                stream=stream)
+        forward([c1], bt, 8, 0, [self.q1], 1, 0, B, masks=[self.mask1], stream=stream)
+        # backprop -mean(Q) through critic 1 to its action input (its own grads are discarded)
+        self._bwd(c1, B, self.dq_actor, 0, self.mask1, s, dx=self.dx)
+        da = self.dx.view(-1)[2:]  # dL/da = columns 2..3 of dL/dx, row stride 4
+        self._bwd(net, B, da, 4, self.mask_a, s, inp=bt, ld_in=8, in_col=0,
+                  h_top=self.acts_a[net.n_hidden - 1], dz=self.dz_a,
+                  save_mask=net.middle_layers(), eslab=self.eslab_a)
+        self._grads(net, B, bt, 8, 0, self.acts_a, self.dz_a, da, 4, self.mask_a, self.eslab_a,
+                    self.grad_a, s)
         self.actor_optimizer.step(self.grad_a, stream)
 
     def actor_loss_value(self):

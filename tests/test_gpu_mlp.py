@@ -117,10 +117,26 @@ def test_act_vs_reference_golden(nav, orc):
     assert np.allclose(act.cpu().numpy(), g["action_test"], rtol=0, atol=2e-4)
 
 
+def _grad_flat_vs_autograd(net, tl, gflat, d_in, d_out, nh):
+    from nav.mlp import layer_offsets
+    offs, _ = layer_offsets(d_in, d_out, net.hp, nh)
+    for l, ((W, b), (w_off, b_off, fo, fi)) in enumerate(zip(tl, offs)):
+        o, i = W.shape
+        gW = gflat[w_off:w_off + fo * fi].view(fo, fi)
+        tol = 1e-5 * (W.grad.abs().max() + 1e-6)
+        assert torch.allclose(gW[:o, :i], W.grad, rtol=1e-3, atol=tol), l
+        assert (gW[o:, :] == 0).all() and (gW[:, i:] == 0).all()
+        gb = gflat[b_off:b_off + o]
+        assert torch.allclose(gb, b.grad, rtol=1e-3, atol=1e-5 * (b.grad.abs().max() + 1e-6)), l
+        assert (gflat[b_off + o:b_off + fo] == 0).all()
+
+
 @pytest.mark.parametrize("d_in,d_out,hidden,nh,M", [(4, 1, 200, 3, 100), (2, 2, 200, 3, 777),
                                                     (4, 1, 256, 2, 5000), (2, 2, 256, 2, 4096),
-                                                    (4, 1, 64, 1, 300)])
+                                                    (4, 1, 64, 1, 300), (2, 2, 96, 4, 333)])
 def test_backward_and_weight_grads_vs_autograd(nav, d_in, d_out, hidden, nh, M):
+    """Row backward + per-block edge partials + recomputing hidden weight gradients + reduce
+    against torch autograd; every gradient entry must be written (NaN-filled buffers)."""
     from nav._lib import lib, ptr, stream_handle
     from nav.mlp import forward
     net, layers = make_net(d_in, d_out, hidden, nh, 11)
@@ -130,35 +146,86 @@ def test_backward_and_weight_grads_vs_autograd(nav, d_in, d_out, hidden, nh, M):
     acts = torch.zeros(nh, M, net.hp, device=DEV)
     masks = net.mask_buffer(M)
     xd = x.to(DEV)
-    forward([net], xd, d_in, 0, [out], d_out, 0, M, acts=[acts], masks=[masks])
+    forward([net], xd, d_in, 0, [out], d_out, 0, M, acts=[acts],
+            save_mask=net.middle_layers() | net.top_layer(), masks=[masks])
     dz = torch.zeros(nh, M, net.hp, device=DEV)
     dx = torch.zeros(M, d_in, device=DEV)
     s = stream_handle()
     dyd = dy.to(DEV)
-    lib().nav_mlp_backward(C.byref(net.desc()), M, ptr(dyd), ptr(masks), ptr(dz), ptr(dx), s)
+    L = lib()
+    nblk = L.nav_mlp_row_blocks(M)
+    eslab = torch.full((nblk, L.nav_mlp_edge_count(d_in, d_out, net.hp, nh)), float("nan"),
+                       device=DEV)
+    L.nav_mlp_backward(C.byref(net.desc()), M, ptr(dyd), d_out, ptr(masks), ptr(xd), d_in, 0,
+                       ptr(acts[nh - 1]), ptr(dz), net.middle_layers(), ptr(dx), ptr(eslab), s)
     splits = 7
-    slabs = torch.zeros(splits, net.count, device=DEV)
-    grad = torch.zeros(net.count, device=DEV)
-    lib().nav_mlp_wgrad(C.byref(net.desc()), M, ptr(xd), d_in, 0, ptr(acts), ptr(dz), ptr(dyd),
-                        ptr(slabs), splits, s)
-    lib().nav_grad_reduce(ptr(slabs), splits, net.count, ptr(grad), s)
+    hs = torch.full((splits, max(4, L.nav_mlp_hidden_count(net.hp, nh))), float("nan"),
+                    device=DEV)
+    grad = torch.full((net.count,), float("nan"), device=DEV)
+    L.nav_mlp_wgrad(C.byref(net.desc()), M, ptr(xd), d_in, 0, ptr(acts), ptr(dz), ptr(dyd), d_out,
+                    ptr(masks), ptr(hs), splits, s)
+    L.nav_grad_reduce(C.byref(net.desc()), ptr(hs), splits, ptr(eslab), nblk, ptr(grad), s)
     # torch autograd reference
     tl = [(W.clone().requires_grad_(True), b.clone().requires_grad_(True)) for W, b in layers]
     xr = x.clone().requires_grad_(True)
     y = torch_mlp(tl, xr)
     (y * dy).sum().backward()
     assert torch.allclose(dx.cpu(), xr.grad, rtol=1e-3, atol=1e-6 * (xr.grad.abs().max() + 1e-3))
-    from nav.mlp import layer_offsets
-    offs, _ = layer_offsets(d_in, d_out, net.hp, nh)
     gflat = grad.cpu()
-    for l, ((W, b), (w_off, b_off, fo, fi)) in enumerate(zip(tl, offs)):
-        o, i = W.shape
-        gW = gflat[w_off:w_off + fo * fi].view(fo, fi)
-        tol = 1e-5 * (W.grad.abs().max() + 1e-6)
-        assert torch.allclose(gW[:o, :i], W.grad, rtol=1e-3, atol=tol), l
-        assert (gW[o:, :] == 0).all() and (gW[:, i:] == 0).all()
-        gb = gflat[b_off:b_off + o]
-        assert torch.allclose(gb, b.grad, rtol=1e-3, atol=1e-5 * (b.grad.abs().max() + 1e-6)), l
+    assert torch.isfinite(gflat).all()
+    _grad_flat_vs_autograd(net, tl, gflat, d_in, d_out, nh)
+
+
+@pytest.mark.parametrize("hidden,nh,B", [(200, 3, 777), (256, 2, 4096), (64, 1, 100)])
+def test_td3_critic_forward_gradients_vs_autograd(nav, hidden, nh, B):
+    """train_critic's fused online forward (robot.py:341-361): TD target, MSE loss and gradient,
+    then backward + weight gradients of both critics vs torch autograd of mse_loss(Q(s,a), y)."""
+    from nav._lib import NavMlp, lib, ptr, stream_handle
+    nets = [make_net(4, 1, hidden, nh, 31 + k) for k in range(2)]
+    g = torch.Generator().manual_seed(5)
+    batch = torch.zeros(B, 8)
+    batch[:, :4] = torch.randn(B, 4, generator=g) * 10
+    batch[:, 4] = torch.randn(B, generator=g) * 10
+    batch[:, 7] = (torch.rand(B, generator=g) < 0.2).float()
+    q1t, q2t = torch.randn(B, generator=g) * 20, torch.randn(B, generator=g) * 20
+    y = batch[:, 4] + 0.99 * torch.min(q1t, q2t) * (1 - batch[:, 7])
+    L = lib()
+    bt, q1d, q2d = batch.to(DEV), q1t.to(DEV), q2t.to(DEV)
+    nblk = L.nav_mlp_row_blocks(B)
+    hp = nets[0][0].hp
+    ec = L.nav_mlp_edge_count(4, 1, hp, nh)
+    dq = [torch.zeros(B, device=DEV) for _ in range(2)]
+    lp = torch.zeros(2, nblk, device=DEV)
+    es = [torch.full((nblk, ec), float("nan"), device=DEV) for _ in range(2)]
+    acts = [torch.zeros(nh, B, hp, device=DEV) for _ in range(2)]
+    dz = [torch.zeros(nh, B, hp, device=DEV) for _ in range(2)]
+    masks = [n.mask_buffer(B) for n, _ in nets]
+    arr = lambda t: (C.c_void_p * 2)(*[x.data_ptr() for x in t])  # noqa: E731
+    mid = nets[0][0].middle_layers()
+    s = stream_handle()
+    L.nav_td3_critic_forward((NavMlp * 2)(*[n.desc() for n, _ in nets]), B, ptr(bt), 8, 0,
+                             ptr(bt), ptr(q1d), ptr(q2d), 0.99, arr(dq), arr([lp[0], lp[1]]),
+                             arr(es), arr(acts), mid, arr(masks), s)
+    splits = 5
+    hs = torch.zeros(splits, max(4, L.nav_mlp_hidden_count(hp, nh)), device=DEV)
+    for k, (net, layers) in enumerate(nets):
+        grad = torch.full((net.count,), float("nan"), device=DEV)
+        L.nav_mlp_backward(C.byref(net.desc()), B, ptr(dq[k]), 1, ptr(masks[k]), ptr(bt), 8, 0,
+                           None, ptr(dz[k]), mid, None, ptr(es[k]), s)
+        L.nav_mlp_wgrad(C.byref(net.desc()), B, ptr(bt), 8, 0, ptr(acts[k]), ptr(dz[k]),
+                        ptr(dq[k]), 1, ptr(masks[k]), ptr(hs), splits, s)
+        L.nav_grad_reduce(C.byref(net.desc()), ptr(hs), splits, ptr(es[k]), nblk, ptr(grad), s)
+        tl = [(W.clone().requires_grad_(True), b.clone().requires_grad_(True)) for W, b in layers]
+        q = torch_mlp(tl, batch[:, :4])
+        loss = torch.nn.functional.mse_loss(q, y.unsqueeze(1))
+        loss.backward()
+        got_loss = lp[k].sum().item() / B
+        assert abs(got_loss - loss.item()) <= 1e-4 * loss.item()
+        ref_dq = 2 * (q.detach().squeeze(1) - y) / B
+        assert torch.allclose(dq[k].cpu(), ref_dq, rtol=1e-4, atol=1e-5 * ref_dq.abs().max())
+        gflat = grad.cpu()
+        assert torch.isfinite(gflat).all()
+        _grad_flat_vs_autograd(net, tl, gflat, 4, 1, nh)
 
 
 def test_adam_and_polyak_vs_oracle(nav):

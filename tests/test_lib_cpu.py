@@ -56,7 +56,7 @@ def test_gfx950_code_object_present(navlib):
 def test_abi_and_layout(navlib):
     from nav.mlp import layer_offsets
     from nav._lib import NavMlp
-    assert navlib.nav_abi_version() == 1
+    assert navlib.nav_abi_version() == 2
     for d_in, d_out, hidden, nh in ((2, 2, 200, 3), (4, 1, 200, 3), (2, 2, 256, 2),
                                     (4, 1, 256, 2), (4, 1, 32, 1)):
         hp = (hidden + 31) // 32 * 32
@@ -84,6 +84,12 @@ def test_host_argument_validation(navlib):
     with pytest.raises(NavError, match="invalid argument"):
         navlib.nav_env_step(C.byref(p), C.byref(bad), None, None, None, None)
     with pytest.raises(NavError, match="invalid argument"):
-        navlib.nav_grad_reduce(None, 1, 8, None, None)
+        navlib.nav_grad_reduce(None, None, 1, None, 1, None, None)
+    from nav._lib import NavMlp
+    d = NavMlp(4, 1, 256, 256, 2, 16, 16)
+    with pytest.raises(NavError, match="invalid argument"):  # no masks
+        navlib.nav_mlp_wgrad(C.byref(d), 64, 16, 4, 0, None, None, 16, 1, None, 16, 4, None)
+    assert navlib.nav_mlp_edge_count(4, 1, 256, 2) == 4 * 256 + 256 + 256 + 256 + 4
+    assert navlib.nav_mlp_hidden_count(256, 2) == 256 * 256
     empty = NavEnvSoa(0, None, None, None, None, None, None, None, None, None)
     navlib.nav_env_reset(C.byref(p), C.byref(empty), None, None, None)  # n = 0: no-op

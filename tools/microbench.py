@@ -38,47 +38,60 @@ def main():
     ap.add_argument("--quick", action="store_true", help="MLP kernels only (for counter runs)")
     args = ap.parse_args()
     from nav import prof
-    from nav._lib import lib, ptr, stream_handle
+    from nav._lib import NavMlp, lib, ptr, stream_handle
     from nav.mlp import DeviceMLP, forward
     from nav.trainer import VecTrainer
     dev = "cuda"
     H, L, B = args.hidden, args.layers, args.batch
     g = torch.Generator().manual_seed(0)
     crit = [DeviceMLP(4, 1, H, L, dev).init_kaiming(g) for _ in range(2)]
-    actor = DeviceMLP(2, 2, H, L, dev).init_kaiming(g)
-    x = torch.randn(B, 4, device=dev) * 10
+    DeviceMLP(2, 2, H, L, dev).init_kaiming(g)
+    bt = torch.randn(B, 8, device=dev) * 10
+    bt[:, 7] = 0
+    x = bt[:, :4].contiguous()
     q = [torch.zeros(B, 1, device=dev) for _ in range(2)]
-    acts = torch.zeros(L, B, crit[0].hp, device=dev)
-    mask = crit[0].mask_buffer(B)
+    acts = [torch.zeros(L, B, crit[0].hp, device=dev) for _ in range(2)]
+    masks = [crit[0].mask_buffer(B) for _ in range(2)]
     res = {}
     f1 = prof.mlp_fwd_flops(4, 1, H, L, B)
     us = timeit(lambda: forward(crit, x, 4, 0, q, 1, 0, B))
     res["fwd_twin_critic"] = {"us": us, "TFs": 2 * f1 / us / 1e6}
-    us = timeit(lambda: forward(crit[:1], x, 4, 0, q[:1], 1, 0, B, acts=[acts], masks=[mask]))
-    res["fwd_critic_save"] = {"us": us, "TFs": f1 / us / 1e6}
-    dy = torch.randn(B, 1, device=dev) / B
-    dz = torch.zeros_like(acts)
+    nblk = lib().nav_mlp_row_blocks(B)
+    ec = lib().nav_mlp_edge_count(4, 1, crit[0].hp, L)
+    es = [torch.zeros(nblk, ec, device=dev) for _ in range(2)]
+    dq = [torch.zeros(B, device=dev) for _ in range(2)]
+    lp = torch.zeros(2, nblk, device=dev)
+    arr = lambda t: (C.c_void_p * 2)(*[v.data_ptr() for v in t])  # noqa: E731
+    descs = (NavMlp * 2)(*[c.desc() for c in crit])
     s = stream_handle()
+    mid = crit[0].middle_layers()
+    us = timeit(lambda: lib().nav_td3_critic_forward(descs, B, ptr(bt), 8, 0, ptr(bt), ptr(q[0]),
+                                                     ptr(q[1]), 0.99, arr(dq), arr([lp[0], lp[1]]),
+                                                     arr(es), arr(acts), mid, arr(masks), s))
+    res["fwd_twin_critic_loss"] = {"us": us, "TFs": 2 * f1 / us / 1e6}
+    dz = torch.zeros_like(acts[0])
     d = crit[0].desc()
-    us = timeit(lambda: lib().nav_mlp_backward(C.byref(d), B, ptr(dy), ptr(mask), ptr(dz), None,
+    us = timeit(lambda: lib().nav_mlp_backward(C.byref(d), B, ptr(dq[0]), 1, ptr(masks[0]),
+                                               ptr(bt), 8, 0, None, ptr(dz), mid, None, ptr(es[0]),
                                                s))
-    fb = prof.mlp_bwd_flops(4, 1, H, L, B)
-    res["bwd_critic"] = {"us": us, "TFs": fb / us / 1e6}
-    splits = max(1, min(64, B // 512))
-    slabs = torch.zeros(splits, crit[0].count, device=dev)
-    us = timeit(lambda: lib().nav_mlp_wgrad(C.byref(d), B, ptr(x), 4, 0, ptr(acts), ptr(dz),
-                                            ptr(dy), ptr(slabs), splits, s))
-    fw = prof.mlp_wgrad_flops(4, 1, H, L, B)
-    res["wgrad_critic"] = {"us": us, "TFs": fw / us / 1e6, "splits": splits}
+    fb = prof.mlp_bwd_flops(4, 1, H, L, B, False, True)
+    res["bwd_critic_edges"] = {"us": us, "TFs": fb / us / 1e6}
+    dxb = torch.zeros(B, 4, device=dev)
+    us = timeit(lambda: lib().nav_mlp_backward(C.byref(d), B, ptr(dq[0]), 1, ptr(masks[0]), None,
+                                               0, 0, None, None, 0, ptr(dxb), None, s))
+    res["bwd_critic_dx"] = {"us": us, "TFs": prof.mlp_bwd_flops(4, 1, H, L, B, True) / us / 1e6}
+    hc = max(4, lib().nav_mlp_hidden_count(crit[0].hp, L))
     grad = torch.zeros(crit[0].count, device=dev)
-    us = timeit(lambda: lib().nav_grad_reduce(ptr(slabs), splits, crit[0].count, ptr(grad), s))
-    res["grad_reduce"] = {"us": us, "GBs": 4 * (splits + 1) * crit[0].count / us / 1e3}
-    # edge layers alone: a one-hidden-layer net has no hidden x hidden gradient tile
-    e1 = DeviceMLP(4, 1, H, 1, dev).init_kaiming(g)
-    d1 = e1.desc()
-    us = timeit(lambda: lib().nav_mlp_wgrad(C.byref(d1), B, ptr(x), 4, 0, ptr(acts), ptr(dz),
-                                            ptr(dy), ptr(slabs), splits, s))
-    res["wgrad_edges_only"] = {"us": us}
+    fw = prof.mlp_wgrad_flops(H, L, B)
+    for splits in (32, 64, 128):
+        sl = torch.zeros(splits, hc, device=dev)
+        us_w = timeit(lambda: lib().nav_mlp_wgrad(C.byref(d), B, ptr(bt), 8, 0, ptr(acts[0]),
+                                                  ptr(dz), ptr(dq[0]), 1, ptr(masks[0]), ptr(sl),
+                                                  splits, s))
+        us_r = timeit(lambda: lib().nav_grad_reduce(C.byref(d), ptr(sl), splits, ptr(es[0]), nblk,
+                                                    ptr(grad), s))
+        res[f"wgrad_splits{splits}"] = {"wgrad_us": us_w, "TFs": fw / us_w / 1e6,
+                                         "reduce_us": us_r}
     if args.quick:
         print(json.dumps(res), flush=True)
         return
@@ -125,13 +138,6 @@ def main():
     torch.cuda.synchronize()
     t2 = time.perf_counter()
     res["train_step"] = {"host_issue_us": (t1 - t0) * 1e5, "wall_us": (t2 - t0) * 1e5}
-    for splits in (32, 64, 128):
-        sl = torch.zeros(splits, crit[0].count, device=dev)
-        us_w = timeit(lambda: lib().nav_mlp_wgrad(C.byref(d), B, ptr(x), 4, 0, ptr(acts),
-                                                  ptr(dz), ptr(dy), ptr(sl), splits, s))
-        us_r = timeit(lambda: lib().nav_grad_reduce(ptr(sl), splits, crit[0].count, ptr(grad),
-                                                    s))
-        res[f"wgrad_splits{splits}"] = {"wgrad_us": us_w, "reduce_us": us_r}
     print(json.dumps({k: {kk: round(vv, 3) if isinstance(vv, float) else vv
                           for kk, vv in v.items()} for k, v in res.items()}), flush=True)
 
