@@ -243,26 +243,40 @@ int nav_td3_critic_forward(const nav_mlp* nets, int64_t B, const float* in, int3
                            float gamma, float* const* dq, float* const* loss_part,
                            float* const* edge_slabs, float* const* acts, uint32_t save_mask,
                            uint16_t* const* masks, void* stream);
-/* Row-local backward of one network (autograd of robot.py:355-395) given dL/dy rows
- * dy[m*ld_dy + 0..d_out) (ld_dy 0: one row for all) and the forward's ReLU masks: dL/dz of every
- * hidden layer, dz_L written to dz [n_hidden][M][hp] for bits L of save_mask; dx (nullable)
- * [M][d_in] = dL/dx. edge_slabs (nullable): per-block W0 / bias partials (input rows from `in`),
- * plus Wo / bo when h_top [M][hp] (the top hidden activations) is given. */
-int nav_mlp_backward(const nav_mlp* net, int64_t M, const float* dy, int32_t ld_dy,
-                     const uint16_t* masks, const float* in, int32_t ld_in, int32_t in_col,
-                     const float* h_top, float* dz, uint32_t save_mask, float* dx,
-                     float* edge_slabs, void* stream);
-/* Hidden x hidden weight gradients dW_L = dz_L^T h_{L-1} as `splits` partial slabs
- * [splits][nav_mlp_hidden_count] (rows of split s = [s*ceil(M/splits), ...)). h_0 is recomputed
- * from `in`, dz_{n_hidden-1} from dy and the masks; acts / dz (saved layers 1 .. n_hidden-2) are
- * read only for n_hidden > 2. */
-int nav_mlp_wgrad(const nav_mlp* net, int64_t M, const float* in, int32_t ld_in, int32_t in_col,
-                  const float* acts, const float* dz, const float* dy, int32_t ld_dy,
-                  const uint16_t* masks, float* slabs, int32_t splits, void* stream);
+/* Row-local backward (autograd of robot.py:355-395) of 1 or 2 networks of the same shape that
+ * share the input rows (the twin critics: one launch): per net i, dL/dy rows
+ * dy[i][m*ld_dy + 0..d_out) (ld_dy 0: one row for all) and the forward's ReLU masks[i] give dL/dz
+ * of every hidden layer, dz_L written to dz[i] [n_hidden][M][hp] for bits L of save_mask;
+ * dx[i] (nullable) [M][d_in] = dL/dx. edge_slabs[i] (nullable): per-block W0 / bias partials
+ * (input rows from `in`), plus Wo / bo when h_top[i] [M][hp] (top hidden activations) is given.
+ * Pointer arrays themselves may be NULL where every entry would be. */
+int nav_mlp_backward(const nav_mlp* nets, int32_t n_nets, int64_t M, const float* const* dy,
+                     int32_t ld_dy, const uint16_t* const* masks, const float* in, int32_t ld_in,
+                     int32_t in_col, const float* const* h_top, float* const* dz,
+                     uint32_t save_mask, float* const* dx, float* const* edge_slabs,
+                     void* stream);
+/* Hidden x hidden weight gradients dW_L = dz_L^T h_{L-1} of 1 or 2 networks (one launch) as
+ * `splits` partial slabs slabs[i] [splits][nav_mlp_hidden_count] (rows of split s =
+ * [s*ceil(M/splits), ...)). h_0 is recomputed from `in`, dz_{n_hidden-1} from dy[i] and
+ * masks[i]; acts[i] / dz[i] (saved layers 1 .. n_hidden-2) are read only for n_hidden > 2. */
+int nav_mlp_wgrad(const nav_mlp* nets, int32_t n_nets, int64_t M, const float* in,
+                  int32_t ld_in, int32_t in_col, const float* const* acts,
+                  const float* const* dz, const float* const* dy, int32_t ld_dy,
+                  const uint16_t* const* masks, float* const* slabs, int32_t splits,
+                  void* stream);
 /* grad [param_count] = sum of the hidden slabs (hidden weights) and of the edge slabs (the rest),
  * in a fixed order. */
 int nav_grad_reduce(const nav_mlp* net, const float* hidden_slabs, int32_t splits,
                     const float* edge_slabs, int64_t edge_blocks, float* grad, void* stream);
+/* nav_grad_reduce fused with the Adam step (robot.py:236-239, as nav_adam) of 1 or 2 networks in
+ * one launch: per net i the reduced gradient (also stored to grads[i] when grads and grads[i]
+ * are non-NULL) updates nets[i].params with moments m[i], v[i], step_size[i] =
+ * lr/(1-b1^t), bc2_sqrt[i] = sqrt(1-b2^t) (host arrays); refreshes packed. */
+int nav_grad_reduce_adam(const nav_mlp* nets, int32_t n_nets, const float* const* hidden_slabs,
+                         int32_t splits, const float* const* edge_slabs, int64_t edge_blocks,
+                         float* const* grads, float* const* m, float* const* v, float beta1,
+                         float beta2, float eps, const float* step_size, const float* bc2_sqrt,
+                         void* stream);
 /* torch.optim.Adam step (robot.py:236-239; torch 2.10 single-tensor semantics) on a flat buffer,
  * step_size = lr/(1-b1^t), bc2_sqrt = sqrt(1-b2^t) precomputed by the caller; refreshes `packed`
  * of `net` (net->params must equal params). */
@@ -270,6 +284,9 @@ int nav_adam(const nav_mlp* net, const float* grad, float* m, float* v, float be
              float eps, float step_size, float bc2_sqrt, void* stream);
 /* robot.py:293-310 soft update target <- target*(1-tau) + source*tau, refreshing target packed. */
 int nav_polyak(const nav_mlp* target, const nav_mlp* source, float tau, void* stream);
+/* The same for n <= 4 (target, source) pairs in one launch (TD3.soft_update x 3, robot.py:283-285). */
+int nav_polyak_multi(const nav_mlp* targets, const nav_mlp* sources, int32_t n, float tau,
+                     void* stream);
 /* rebuild `packed` from `params` (after a host-side weight load). */
 int nav_mlp_pack(const nav_mlp* net, void* stream);
 

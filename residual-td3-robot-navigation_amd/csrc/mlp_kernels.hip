@@ -533,18 +533,18 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
 
 // ---------------- row-local backward ----------------
 struct BwdArgs {
-    MlpDev net;
+    MlpDev net[2];           // 1 or 2 networks (blockIdx.y), same shapes, same input rows
     int64_t M;
-    const float* dy;
+    const float* dy[2];
     int ld_dy;               // dy row stride (0: one row broadcast to every row)
-    const uint16_t* masks;
+    const uint16_t* masks[2];
     const float* in;         // the forward's input rows (dW0 partials), with eslab
     int ld_in, in_col;
-    const float* h_top;      // nullable: [M][hp] top activations -> Wo / bo partials here
-    float* dz;               // [n_hidden][M][hp], layers with a save_mask bit written
+    const float* h_top[2];   // nullable: [M][hp] top activations -> Wo / bo partials here
+    float* dz[2];            // [n_hidden][M][hp], layers with a save_mask bit written
     uint32_t save_mask;
-    float* dx;
-    float* eslab;            // nullable: [blocks][edge_count] W0 / bias (/ Wo / bo) partials
+    float* dx[2];
+    float* eslab[2];         // nullable: [blocks][edge_count] W0 / bias (/ Wo / bo) partials
     int64_t ecount;
 };
 
@@ -574,7 +574,8 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_bwd(BwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     constexpr int hp = NT * 32, SS = hp + 4, TM = RT * 32;
     const int tid = threadIdx.x, lane = tid & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
-    const MlpDev& net = a.net;
+    const int y = blockIdx.y;
+    const MlpDev& net = a.net[y];
     const int64_t M = a.M;
     const int64_t row0 = (int64_t)blockIdx.x * TM;
     const int64_t rt0 = (int64_t)blockIdx.x * RT;
@@ -586,14 +587,14 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_bwd(BwdArgs a) {
     const int64_t MH = M * hp;
     const WaveCols<NT> wc(wv);
     const size_t mstride = (size_t)n_rt * NT * 64;
-    float* es = a.eslab ? a.eslab + (int64_t)blockIdx.x * a.ecount : nullptr;
+    float* es = a.eslab[y] ? a.eslab[y] + (int64_t)blockIdx.x * a.ecount : nullptr;
 
     if (tid < TM) {
         const int64_t r = row0 + tid;
         float x[2] = {0.f, 0.f};
         float xi[4] = {0.f, 0.f, 0.f, 0.f};
         if (r < M) {
-            for (int j = 0; j < d_out; ++j) x[j] = a.dy[r * a.ld_dy + j];
+            for (int j = 0; j < d_out; ++j) x[j] = a.dy[y][r * a.ld_dy + j];
             if (es)
                 for (int k = 0; k < d_in; ++k) xi[k] = a.in[r * a.ld_in + a.in_col + k];
         }
@@ -604,14 +605,14 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_bwd(BwdArgs a) {
     if (es) {
         // output layer (robot.py:361 / 392 backward): dWo = dy^T h_top, dbo = sum dy, when the
         // forward did not produce them (it does for the critic's TD loss)
-        if (a.h_top) {
+        if (a.h_top[y]) {
             const int n = tid;
             if (n < hp) {
                 float s0 = 0.f, s1 = 0.f;
                 const int rows = (int)(M - row0 < TM ? M - row0 : TM);
 #pragma unroll 4
                 for (int rr = 0; rr < rows; ++rr) {
-                    const float h = a.h_top[(row0 + rr) * hp + n];
+                    const float h = a.h_top[y][(row0 + rr) * hp + n];
                     s0 = fmaf(dys[rr * 4], h, s0);
                     s1 = fmaf(dys[rr * 4 + 1], h, s1);
                 }
@@ -630,7 +631,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_bwd(BwdArgs a) {
     // top hidden layer: dz = (dy . Wo) * relu'(.), in the C layout
     {
         const float* Wo = net.params + net.w_off[nh];
-        const uint16_t* mk = a.masks + (size_t)(nh - 1) * mstride;
+        const uint16_t* mk = a.masks[y] + (size_t)(nh - 1) * mstride;
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             if (!(j == 0 ? wc.has0 : wc.has1)) continue;
@@ -665,7 +666,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_bwd(BwdArgs a) {
             edge_col_sums<TM>(act, SS, hp, es + e_b(net, L));
             if (L == 0) edge_w0<TM>(act, SS, hp, xin, d_in, es + net.w_off[0]);
         }
-        if ((a.save_mask >> L) & 1u) copy_rows<NT, RT>(act, SS, a.dz + (int64_t)L * MH, row0, M);
+        if ((a.save_mask >> L) & 1u) copy_rows<NT, RT>(act, SS, a.dz[y] + (int64_t)L * MH, row0, M);
     };
     finish_layer(nh - 1);
 
@@ -675,13 +676,13 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_bwd(BwdArgs a) {
         gemm_cols<NT, RT>(act, SS,
                           net.packed + (int64_t)(L - 1) * 2 * hp * hp + (int64_t)hp * hp, acc);
         __syncthreads();
-        mask_and_store<NT, RT>(acc, a.masks + (size_t)(L - 1) * mstride, act, SS, rt0);
+        mask_and_store<NT, RT>(acc, a.masks[y] + (size_t)(L - 1) * mstride, act, SS, rt0);
         __syncthreads();
         finish_layer(L - 1);
     }
 
     // dx = dz_0 . W0 : thread = (row, input pair)
-    if (a.dx) {
+    if (a.dx[y]) {
         const float* W0 = net.params + net.w_off[0];
         const int rloc = tid % TM;
         const int64_t r = row0 + rloc;
@@ -689,7 +690,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_bwd(BwdArgs a) {
         for (int jj = tid / TM; jj < d_in; jj += kBlock / TM) {
             float acc = 0.f;
             for (int c = 0; c < hp; ++c) acc = fmaf(zr[c], W0[c * d_in + jj], acc);
-            if (r < M) a.dx[r * d_in + jj] = acc;
+            if (r < M) a.dx[y][r * d_in + jj] = acc;
         }
     }
 }
@@ -698,24 +699,27 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_bwd(BwdArgs a) {
 // dW_L = dz_L^T h_{L-1} for L = 1 .. nh-1 over the rows of each split. The thin layers' gradients
 // (W0, every bias, Wo, bo) are edge partials of the forward / backward kernels instead.
 struct WgradArgs {
-    MlpDev net;
+    MlpDev net[2];          // 1 or 2 networks, same shapes, same input rows
     int64_t M;
     const float* in;        // layer-0 input rows: h_0 is recomputed (layer0_unit)
     int ld_in, in_col;
-    const float* acts;      // [nh][M][hp]: saved h_L, 1 <= L <= nh-2
-    const float* dz;        // [nh][M][hp]: saved dz_L, 1 <= L <= nh-2
-    const float* dy;        // dz_{nh-1} is recomputed: top_unit(dy row, Wo) under the ReLU bit
+    const float* acts[2];   // [nh][M][hp]: saved h_L, 1 <= L <= nh-2
+    const float* dz[2];     // [nh][M][hp]: saved dz_L, 1 <= L <= nh-2
+    const float* dy[2];     // dz_{nh-1} is recomputed: top_unit(dy row, Wo) under the ReLU bit
     int ld_dy;
-    const uint16_t* masks;  // the forward's ReLU bit image
-    float* slabs;           // [splits][(nh-1) hp hp]
+    const uint16_t* masks[2];  // the forward's ReLU bit image
+    float* slabs[2];        // [splits][(nh-1) hp hp]
     int splits;
     int TA;                 // 128-wide tiles across hp
-    int n_hid;              // jobs = (nh - 1) * TA * TA
+    int n_hid;              // jobs per network = (nh - 1) * TA * TA
 };
 
 constexpr int WG_MC = 32;   // rows per staged chunk
 constexpr int WA_W = 128;   // tile width
 constexpr int WA_LD = 132;  // LDS row stride of the 128-column panels
+#ifndef WG_STAGE0
+#define WG_STAGE0 8         // first MFMA step that stages the next chunk (its loads land first)
+#endif
 
 inline size_t wgrad_lds_bytes() { return (size_t)2 * 2 * WG_MC * WA_LD * 4; }
 
@@ -733,8 +737,8 @@ NAV_DEV float4 sel4(bool c, float4 v) {
 // columns), for layer 1 h_0 = layer0_unit(x, W0, b0) — the same bits the backward / forward
 // produced, so a 2-hidden-layer network's weight gradient reads no activation tensor at all.
 template <bool FULL, bool PR, bool QR>
-NAV_DEV void wgrad_hidden(const WgradArgs& a, int job, int split, float* smem) {
-    const MlpDev& net = a.net;
+NAV_DEV void wgrad_hidden(const WgradArgs& a, int y, int job, int split, float* smem) {
+    const MlpDev& net = a.net[y];
     const int hp = net.hp, TA = a.TA, nh = net.n_hidden, d_in = net.d_in, d_out = net.d_out;
     const int L = job / (TA * TA) + 1;
     const int tn = (job % (TA * TA)) / TA, tk = job % TA;
@@ -763,11 +767,11 @@ NAV_DEV void wgrad_hidden(const WgradArgs& a, int job, int split, float* smem) {
     const int pn = n0 + 4 * c4, qk = k0 + 4 * c4;
     const bool pc_ok = pn < hp, qc_ok = qk < hp;
     const int pnc = pc_ok ? pn : 0, qkc = qc_ok ? qk : 0;
-    const float* Pc = a.dz + (PR ? 0 : (int64_t)L * MH + pnc);
-    const float* Qc = a.acts + (QR ? 0 : (int64_t)(L - 1) * MH + qkc);
+    const float* Pc = a.dz[y] + (PR ? 0 : (int64_t)L * MH + pnc);
+    const float* Qc = a.acts[y] + (QR ? 0 : (int64_t)(L - 1) * MH + qkc);
     float wo0[4] = {0.f, 0.f, 0.f, 0.f}, wo1[4] = {0.f, 0.f, 0.f, 0.f};
     float w0[4][4] = {}, b0[4] = {0.f, 0.f, 0.f, 0.f};
-    const uint16_t* mk = a.masks;
+    const uint16_t* mk = a.masks[y];
     if (PR) {
         const float* Wo = net.params + net.w_off[nh];
 #pragma unroll
@@ -800,7 +804,7 @@ NAV_DEV void wgrad_hidden(const WgradArgs& a, int job, int split, float* smem) {
                 const int rr = (int)(mc & 31);
                 rm[f] = *reinterpret_cast<const uint2*>(
                     mk + mask_idx(mc >> 5, hp >> 5, pnc >> 5, (pnc & 31) + 32 * ((rr >> 2) & 1)));
-                const float* g = a.dy + mc * a.ld_dy;
+                const float* g = a.dy[y] + mc * a.ld_dy;
                 rp[f] = make_float4(g[0], g[g1], 0.f, 0.f);
             } else {
                 rp[f] = *reinterpret_cast<const float4*>(Pc + mc * hp);
@@ -813,62 +817,70 @@ NAV_DEV void wgrad_hidden(const WgradArgs& a, int job, int split, float* smem) {
             }
         }
     };
-    auto store = [&](int buf, int64_t m0) {
-#pragma unroll
-        for (int f = 0; f < 4; ++f) {
-            const int r = rr0 + 8 * f;
-            const bool ok = m0 + r < m_hi;
-            float4 pv = rp[f], qv = rq[f];
-            if (PR) {
-                const int64_t mc = ok ? m0 + r : m_lo;
-                const int rr = (int)(mc & 31);
-                const int i = (rr & 3) + 4 * (rr >> 3);  // C-layout element of the row
-                const float gx = rp[f].x, gy = d_out > 1 ? rp[f].y : 0.f;
-                const uint32_t wx = rm[f].x, wy = rm[f].y;
-                pv.x = (wx >> i) & 1u ? top_unit(gx, gy, wo0[0], wo1[0]) : 0.f;
-                pv.y = (wx >> (16 + i)) & 1u ? top_unit(gx, gy, wo0[1], wo1[1]) : 0.f;
-                pv.z = (wy >> i) & 1u ? top_unit(gx, gy, wo0[2], wo1[2]) : 0.f;
-                pv.w = (wy >> (16 + i)) & 1u ? top_unit(gx, gy, wo0[3], wo1[3]) : 0.f;
-            }
-            if (QR) {
-                float4 x = rq[f];
-                x.y = d_in > 1 ? x.y : 0.f;
-                x.z = d_in > 2 ? x.z : 0.f;
-                x.w = d_in > 3 ? x.w : 0.f;
-                qv.x = layer0_unit(x, w0[0][0], w0[0][1], w0[0][2], w0[0][3], b0[0]);
-                qv.y = layer0_unit(x, w0[1][0], w0[1][1], w0[1][2], w0[1][3], b0[1]);
-                qv.z = layer0_unit(x, w0[2][0], w0[2][1], w0[2][2], w0[2][3], b0[2]);
-                qv.w = layer0_unit(x, w0[3][0], w0[3][1], w0[3][2], w0[3][3], b0[3]);
-            }
-            *reinterpret_cast<float4*>(Ps + (buf * WG_MC + r) * WA_LD + 4 * c4) =
-                sel4(ok && pc_ok, pv);
-            *reinterpret_cast<float4*>(Qs + (buf * WG_MC + r) * WA_LD + 4 * c4) =
-                sel4(ok && qc_ok, qv);
+    // staging of row group f of a chunk into LDS buffer buf, one panel at a time
+    auto storeP = [&](int buf, int64_t m0, int f) {
+        const int r = rr0 + 8 * f;
+        const bool ok = m0 + r < m_hi;
+        float4 pv = rp[f];
+        if (PR) {
+            const int64_t mc = ok ? m0 + r : m_lo;
+            const int rr = (int)(mc & 31);
+            const int i = (rr & 3) + 4 * (rr >> 3);  // C-layout element of the row
+            const float gx = rp[f].x, gy = d_out > 1 ? rp[f].y : 0.f;
+            const uint32_t wx = rm[f].x, wy = rm[f].y;
+            pv.x = (wx >> i) & 1u ? top_unit(gx, gy, wo0[0], wo1[0]) : 0.f;
+            pv.y = (wx >> (16 + i)) & 1u ? top_unit(gx, gy, wo0[1], wo1[1]) : 0.f;
+            pv.z = (wy >> i) & 1u ? top_unit(gx, gy, wo0[2], wo1[2]) : 0.f;
+            pv.w = (wy >> (16 + i)) & 1u ? top_unit(gx, gy, wo0[3], wo1[3]) : 0.f;
         }
+        *reinterpret_cast<float4*>(Ps + (buf * WG_MC + r) * WA_LD + 4 * c4) = sel4(ok && pc_ok, pv);
+    };
+    auto storeQ = [&](int buf, int64_t m0, int f) {
+        const int r = rr0 + 8 * f;
+        const bool ok = m0 + r < m_hi;
+        float4 qv = rq[f];
+        if (QR) {
+            float4 x = rq[f];
+            x.y = d_in > 1 ? x.y : 0.f;
+            x.z = d_in > 2 ? x.z : 0.f;
+            x.w = d_in > 3 ? x.w : 0.f;
+            qv.x = layer0_unit(x, w0[0][0], w0[0][1], w0[0][2], w0[0][3], b0[0]);
+            qv.y = layer0_unit(x, w0[1][0], w0[1][1], w0[1][2], w0[1][3], b0[1]);
+            qv.z = layer0_unit(x, w0[2][0], w0[2][1], w0[2][2], w0[2][3], b0[2]);
+            qv.w = layer0_unit(x, w0[3][0], w0[3][1], w0[3][2], w0[3][3], b0[3]);
+        }
+        *reinterpret_cast<float4*>(Qs + (buf * WG_MC + r) * WA_LD + 4 * c4) = sel4(ok && qc_ok, qv);
     };
     const int nch = (int)((m_hi - m_lo + WG_MC - 1) / WG_MC);
     if (nch > 0) {
         load(m_lo);
-        store(0, m_lo);
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+            storeP(0, m_lo, f);
+            storeQ(0, m_lo, f);
+        }
     }
     __syncthreads();
     for (int c = 0; c < nch; ++c) {
-        if (c + 1 < nch) load(m_lo + (int64_t)(c + 1) * WG_MC);
+        const bool more = c + 1 < nch;
+        const int64_t mn = m_lo + (int64_t)(c + 1) * WG_MC;
+        if (FULL || more) load(mn);  // rows past m_hi load clamped addresses
         const int buf = c & 1;
         const float* pb = Ps + buf * WG_MC * WA_LD;
         const float* qb = Qs + buf * WG_MC * WA_LD;
         __builtin_amdgcn_sched_barrier(0);
         if (FULL) {
-            // branch-free: step s+1's operands are read before step s's 4 MFMAs (fenced so
-            // the scheduler cannot sink the reads onto their uses)
+            // branch-free: step s+1's operands are read before step s's 4 MFMAs; steps 4..11 also
+            // stage one (row group, panel) piece of the NEXT chunk into the other buffer, whose
+            // VALU / LDS work issues in the MFMAs' shadow instead of after the chunk
             const float* pw = pb + h * WA_LD + wn + l32;
             const float* qw = qb + h * WA_LD + wk + l32;
             float a0 = pw[0], a1 = pw[32], bq0 = qw[0], bq1 = qw[32];
 #pragma unroll
-            for (int s = 0; s < WG_MC / 2; ++s) {
+            for (int st = 0; st < WG_MC / 2; ++st) {
                 float a0n = 0.f, a1n = 0.f, b0n = 0.f, b1n = 0.f;
-                if (s + 1 < WG_MC / 2) {
-                    const int o = 2 * (s + 1) * WA_LD;
+                if (st + 1 < WG_MC / 2) {
+                    const int o = 2 * (st + 1) * WA_LD;
                     a0n = pw[o];
                     a1n = pw[o + 32];
                     b0n = qw[o];
@@ -879,13 +891,25 @@ NAV_DEV void wgrad_hidden(const WgradArgs& a, int job, int split, float* smem) {
                 acc[0][1] = mfma(a0, bq1, acc[0][1]);
                 acc[1][0] = mfma(a1, bq0, acc[1][0]);
                 acc[1][1] = mfma(a1, bq1, acc[1][1]);
+                if (st >= WG_STAGE0 && st < WG_STAGE0 + 8) {
+                    // unconditional (the last chunk stages clamped rows into the idle buffer), so
+                    // the piece shares the MFMAs' basic block: MFMA / VALU interleaved
+                    if ((st & 1) == 0) storeP(buf ^ 1, mn, (st - WG_STAGE0) >> 1);
+                    else storeQ(buf ^ 1, mn, (st - WG_STAGE0) >> 1);
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
+                        __builtin_amdgcn_sched_group_barrier(0x002, 12, 0);  // up to 12 VALU
+                    }
+                    __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);       // the ds_write
+                }
                 __builtin_amdgcn_sched_barrier(0);
                 a0 = a0n; a1 = a1n; bq0 = b0n; bq1 = b1n;
             }
         } else {
 #pragma unroll
-            for (int s = 0; s < WG_MC / 2; ++s) {
-                const int row = 2 * s + h;
+            for (int st = 0; st < WG_MC / 2; ++st) {
+                const int row = 2 * st + h;
                 const float a0 = pb[row * WA_LD + wn + l32], a1 = pb[row * WA_LD + wn + 32 + l32];
                 const float bq0 = qb[row * WA_LD + wk + l32], bq1 = qb[row * WA_LD + wk + 32 + l32];
                 if (n0k && k0k) acc[0][0] = mfma(a0, bq0, acc[0][0]);
@@ -893,12 +917,18 @@ NAV_DEV void wgrad_hidden(const WgradArgs& a, int job, int split, float* smem) {
                 if (n1k && k0k) acc[1][0] = mfma(a1, bq0, acc[1][0]);
                 if (n1k && k1k) acc[1][1] = mfma(a1, bq1, acc[1][1]);
             }
+            __builtin_amdgcn_sched_barrier(0);
+            if (more) {
+#pragma unroll
+                for (int f = 0; f < 4; ++f) {
+                    storeP(buf ^ 1, mn, f);
+                    storeQ(buf ^ 1, mn, f);
+                }
+            }
         }
-        __builtin_amdgcn_sched_barrier(0);
-        if (c + 1 < nch) store(buf ^ 1, m_lo + (int64_t)(c + 1) * WG_MC);
         __syncthreads();
     }
-    float* o = a.slabs + (int64_t)split * hidden_w_count(net) + (int64_t)(L - 1) * hp * hp;
+    float* o = a.slabs[y] + (int64_t)split * hidden_w_count(net) + (int64_t)(L - 1) * hp * hp;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -914,75 +944,25 @@ NAV_DEV void wgrad_hidden(const WgradArgs& a, int job, int split, float* smem) {
 // Which operand is recomputed depends on the layer (top: P, layer 1: Q), chosen per block.
 __global__ __launch_bounds__(kBlock) void k_wgrad(WgradArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int b = blockIdx.x;
+    const int per_net = a.n_hid * a.splits;
+    const int y = (int)blockIdx.x / per_net, b = (int)blockIdx.x % per_net;
     const int job = b % a.n_hid, split = b / a.n_hid;
     const int TA = a.TA, t = job % (TA * TA);
-    const int L = job / (TA * TA) + 1, nh = a.net.n_hidden;
+    const int L = job / (TA * TA) + 1, nh = a.net[0].n_hidden, hp = a.net[0].hp;
     // tiles entirely inside hp take the branch-free MFMA body
-    const bool full = (t / TA + 1) * WA_W <= a.net.hp && (t % TA + 1) * WA_W <= a.net.hp;
+    const bool full = (t / TA + 1) * WA_W <= hp && (t % TA + 1) * WA_W <= hp;
     const bool pr = L == nh - 1, qr = L == 1;
 #define NAV_WG(F)                                                                       \
-    if (pr && qr) wgrad_hidden<F, true, true>(a, job, split, smem);                     \
-    else if (pr) wgrad_hidden<F, true, false>(a, job, split, smem);                     \
-    else if (qr) wgrad_hidden<F, false, true>(a, job, split, smem);                     \
-    else wgrad_hidden<F, false, false>(a, job, split, smem);
+    if (pr && qr) wgrad_hidden<F, true, true>(a, y, job, split, smem);                     \
+    else if (pr) wgrad_hidden<F, true, false>(a, y, job, split, smem);                     \
+    else if (qr) wgrad_hidden<F, false, true>(a, y, job, split, smem);                     \
+    else wgrad_hidden<F, false, false>(a, y, job, split, smem);
     if (full) {
         NAV_WG(true)
     } else {
         NAV_WG(false)
     }
 #undef NAV_WG
-}
-
-// grad = hidden-W entries: sum of the weight-gradient split slabs (block = 64 float4 columns x 4
-// split groups, the group sums added in order through LDS); every other entry: sum of the
-// per-row-block edge slabs (one wave per float4, lanes take blocks b = lane, lane + 64, ..., a
-// fixed xor tree adds the lanes). Deterministic: the same order on every run.
-__global__ __launch_bounds__(kBlock) void k_grad_reduce(MlpDev net, const float4* __restrict__ hs,
-                                                        int splits, int64_t hw4, int nbh,
-                                                        const float4* __restrict__ es,
-                                                        int64_t nblk, int64_t e4,
-                                                        float4* __restrict__ grad) {
-    __shared__ float4 part[4][64];
-    const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
-    if ((int)blockIdx.x < nbh) {
-        const int64_t i = (int64_t)blockIdx.x * 64 + c;
-        float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (i < hw4) {
-#pragma unroll 4
-            for (int k = g; k < splits; k += 4) {
-                const float4 v = hs[(int64_t)k * hw4 + i];
-                s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-            }
-        }
-        part[g][c] = s;
-        __syncthreads();
-        if (g != 0 || i >= hw4) return;
-        float4 r = part[0][c];
-#pragma unroll
-        for (int q = 1; q < 4; ++q) {
-            r.x += part[q][c].x; r.y += part[q][c].y; r.z += part[q][c].z; r.w += part[q][c].w;
-        }
-        const int64_t per = (int64_t)net.hp * net.hp / 4;
-        const int L = (int)(i / per) + 1;
-        grad[net.w_off[L] / 4 + i % per] = r;
-        return;
-    }
-    const int64_t o = ((int64_t)blockIdx.x - nbh) * 4 + g;
-    if (o >= e4) return;  // wave-uniform
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int64_t b = c; b < nblk; b += 64) {
-        const float4 v = es[b * e4 + o];
-        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-    }
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) {
-        s.x += __shfl_xor(s.x, d, 64);
-        s.y += __shfl_xor(s.y, d, 64);
-        s.z += __shfl_xor(s.z, d, 64);
-        s.w += __shfl_xor(s.w, d, 64);
-    }
-    if (c == 0) grad[edge_to_flat(net, 4 * o) / 4] = s;
 }
 
 // ---------------- optimizer / target update, refreshing the packed images ----------------
@@ -1020,6 +1000,113 @@ NAV_DEV float adam1(float& p, float g, float& m, float& v, float b1w, float b2, 
     return p;
 }
 
+// ---------------- gradient reduce (+ fused Adam) ----------------
+// grad = hidden-W entries: sum of the weight-gradient split slabs (block = 64 float4 columns x 4
+// split groups, the group sums added in order through LDS); every other entry: sum of the
+// per-row-block edge slabs (one wave per float4, lanes take blocks b = lane, lane + 64, ..., a
+// fixed xor tree adds the lanes). Deterministic: the same order on every run. With ADAM the
+// finished gradient goes straight into torch's Adam update (robot.py:236-239) of the parameter
+// it belongs to and the packed MFMA images are refreshed; up to 2 networks per launch.
+struct RedNet {
+    MlpDev net;
+    const float4* hs;
+    const float4* es;
+    float4* grad;  // nullable with ADAM
+    float4* p;
+    float4* m;
+    float4* v;
+    float step_size, bc2s;
+    PackInfo pk;
+    int nbh, nbe;
+};
+
+struct RedArgs {
+    RedNet n[2];
+    int splits;
+    int64_t nblk;
+    float b1w, b2, omb2, eps;
+};
+
+template <bool ADAM>
+NAV_DEV void red_out(const RedArgs& a, const RedNet& rn, int64_t flat4, float4 g) {
+    if (rn.grad) rn.grad[flat4] = g;
+    if (!ADAM) return;
+    float4 pp = rn.p[flat4], mm = rn.m[flat4], vv = rn.v[flat4];
+    adam1(pp.x, g.x, mm.x, vv.x, a.b1w, a.b2, a.omb2, a.eps, rn.step_size, rn.bc2s);
+    adam1(pp.y, g.y, mm.y, vv.y, a.b1w, a.b2, a.omb2, a.eps, rn.step_size, rn.bc2s);
+    adam1(pp.z, g.z, mm.z, vv.z, a.b1w, a.b2, a.omb2, a.eps, rn.step_size, rn.bc2s);
+    adam1(pp.w, g.w, mm.w, vv.w, a.b1w, a.b2, a.omb2, a.eps, rn.step_size, rn.bc2s);
+    rn.p[flat4] = pp;
+    rn.m[flat4] = mm;
+    rn.v[flat4] = vv;
+    if (rn.pk.packed) repack(rn.pk, flat4 * 4, pp);
+}
+
+template <bool ADAM>
+__global__ __launch_bounds__(kBlock) void k_grad_reduce(RedArgs a) {
+    __shared__ float4 part[4][64];
+    const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
+    int b = blockIdx.x;
+    const bool second = b >= a.n[0].nbh + a.n[0].nbe;
+    const RedNet& rn = second ? a.n[1] : a.n[0];
+    if (second) b -= a.n[0].nbh + a.n[0].nbe;
+    const MlpDev& net = rn.net;
+    if (b < rn.nbh) {
+        const int64_t hw4 = hidden_w_count(net) / 4;
+        const int64_t i = (int64_t)b * 64 + c;
+        float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (i < hw4) {
+#pragma unroll 4
+            for (int k = g; k < a.splits; k += 4) {
+                const float4 v = rn.hs[(int64_t)k * hw4 + i];
+                s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+            }
+        }
+        part[g][c] = s;
+        __syncthreads();
+        if (g != 0 || i >= hw4) return;
+        float4 r = part[0][c];
+#pragma unroll
+        for (int q = 1; q < 4; ++q) {
+            r.x += part[q][c].x; r.y += part[q][c].y; r.z += part[q][c].z; r.w += part[q][c].w;
+        }
+        const int64_t per = (int64_t)net.hp * net.hp / 4;
+        const int L = (int)(i / per) + 1;
+        red_out<ADAM>(a, rn, net.w_off[L] / 4 + i % per, r);
+        return;
+    }
+    const int64_t e4 = edge_count(net) / 4;
+    const int64_t o = (int64_t)(b - rn.nbh) * 4 + g;
+    if (o >= e4) return;  // wave-uniform
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t k = c; k < a.nblk; k += 64) {
+        const float4 v = rn.es[k * e4 + o];
+        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) {
+        s.x += __shfl_xor(s.x, d, 64);
+        s.y += __shfl_xor(s.y, d, 64);
+        s.z += __shfl_xor(s.z, d, 64);
+        s.w += __shfl_xor(s.w, d, 64);
+    }
+    if (c == 0) red_out<ADAM>(a, rn, edge_to_flat(net, 4 * o) / 4, s);
+}
+
+// robot.py:293-310 soft update of up to 4 (target, source) pairs in one launch
+struct PolyPair {
+    float4* t;
+    const float4* s;
+    int64_t n4;
+    PackInfo pk;
+};
+struct PolyArgs {
+    PolyPair q[4];
+    int n;
+    int64_t total4;
+    float omt, tau;
+};
+
 __global__ __launch_bounds__(kBlock) void k_adam(float4* __restrict__ p,
                                                  const float4* __restrict__ g, float4* m,
                                                  float4* v, int64_t n4, float b1w, float b2,
@@ -1051,6 +1138,25 @@ __global__ __launch_bounds__(kBlock) void k_polyak(float4* __restrict__ t,
         a.w = a.w * omt + b.w * tau;
         t[i] = a;
         if (pk.packed) repack(pk, i * 4, a);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_polyak_multi(PolyArgs a) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < a.total4;
+         i += (int64_t)gridDim.x * kBlock) {
+        int64_t j = i;
+        int k = 0;
+        while (k < a.n - 1 && j >= a.q[k].n4) j -= a.q[k++].n4;
+        const PolyPair& q = a.q[k];
+        float4 t = q.t[j];
+        const float4 s = q.s[j];
+        // robot.py:309 target*(1-tau) + source*tau (two products, one sum)
+        t.x = t.x * a.omt + s.x * a.tau;
+        t.y = t.y * a.omt + s.y * a.tau;
+        t.z = t.z * a.omt + s.z * a.tau;
+        t.w = t.w * a.omt + s.w * a.tau;
+        q.t[j] = t;
+        if (q.pk.packed) repack(q.pk, j * 4, t);
     }
 }
 
@@ -1110,6 +1216,18 @@ PackInfo pack_info(const MlpDev& d, float* packed) {
     return pk;
 }
 
+bool red_net(const nav_mlp* net, const float* hs, int splits, const float* es, float* grad,
+             RedNet* rn) {
+    if (!make_dev(net, &rn->net)) return false;
+    if (rn->net.n_hidden > 1 && (!hs || splits < 1)) return false;
+    rn->hs = reinterpret_cast<const float4*>(hs);
+    rn->es = reinterpret_cast<const float4*>(es);
+    rn->grad = reinterpret_cast<float4*>(grad);
+    rn->nbh = (int)((hidden_w_count(rn->net) / 4 + 63) / 64);
+    rn->nbe = (int)((edge_count(rn->net) / 4 + 3) / 4);
+    return true;
+}
+
 // ---- launch helpers (template dispatch on NT = hp / 32 and RT = rows / 32) ----
 // Workgroup height: RT = 4 (128 rows, one workgroup per CU) or RT = 2 (64 rows, two per CU so one
 // workgroup's epilogue overlaps the other's MFMA loop). NAV_MLP_RT overrides (tuning only).
@@ -1151,23 +1269,23 @@ int launch_fwd(const FwdArgs& a, int n_nets, hipStream_t st) {
 }
 
 template <int NT, int RT>
-void launch_bwd_k(const BwdArgs& a, hipStream_t st) {
+void launch_bwd_k(const BwdArgs& a, int n_nets, hipStream_t st) {
     const size_t lds = lds_bytes(NT * 32, RT * 32);
     auto k = k_mlp_bwd<NT, RT>;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
-    const dim3 grid((unsigned)((a.M + RT * 32 - 1) / (RT * 32)));
+    const dim3 grid((unsigned)((a.M + RT * 32 - 1) / (RT * 32)), (unsigned)n_nets);
     hipLaunchKernelGGL(k, grid, dim3(kBlock), lds, st, a);
 }
 
-int launch_bwd(const BwdArgs& a, hipStream_t st) {
+int launch_bwd(const BwdArgs& a, int n_nets, hipStream_t st) {
     const int rt = row_tiles();
 #define NAV_BWD_CASE(NT_)                                                                    \
     case NT_:                                                                                \
-        if (rt == 4) launch_bwd_k<NT_, 4>(a, st);                                            \
-        else launch_bwd_k<NT_, 2>(a, st);                                                    \
+        if (rt == 4) launch_bwd_k<NT_, 4>(a, n_nets, st);                                    \
+        else launch_bwd_k<NT_, 2>(a, n_nets, st);                                            \
         break;
-    switch (a.net.hp / 32) {
+    switch (a.net[0].hp / 32) {
         NAV_BWD_CASE(1) NAV_BWD_CASE(2) NAV_BWD_CASE(3) NAV_BWD_CASE(4)
         NAV_BWD_CASE(5) NAV_BWD_CASE(6) NAV_BWD_CASE(7) NAV_BWD_CASE(8)
         default: return NAV_EINVAL;
@@ -1331,75 +1449,152 @@ int64_t nav_mlp_mask_count(int32_t hidden_pad, int32_t n_hidden, int64_t M) {
     return (int64_t)n_hidden * mask_rowtiles(M) * (hidden_pad / 32) * 64;
 }
 
-int nav_mlp_backward(const nav_mlp* net, int64_t M, const float* dy, int32_t ld_dy,
-                     const uint16_t* masks, const float* in, int32_t ld_in, int32_t in_col,
-                     const float* h_top, float* dz, uint32_t save_mask, float* dx,
-                     float* edge_slabs, void* stream) {
+int nav_mlp_backward(const nav_mlp* nets, int32_t n_nets, int64_t M, const float* const* dy,
+                     int32_t ld_dy, const uint16_t* const* masks, const float* in, int32_t ld_in,
+                     int32_t in_col, const float* const* h_top, float* const* dz,
+                     uint32_t save_mask, float* const* dx, float* const* edge_slabs,
+                     void* stream) {
     BwdArgs a{};
-    if (!make_dev(net, &a.net) || M < 0 || ld_dy < 0) return NAV_EINVAL;
+    if (!nets || n_nets < 1 || n_nets > 2 || M < 0 || ld_dy < 0 || !dy || !masks) return NAV_EINVAL;
+    bool any_edges = false;
+    for (int i = 0; i < n_nets; ++i) {
+        if (!make_dev(&nets[i], &a.net[i])) return NAV_EINVAL;
+        if (a.net[i].hp != a.net[0].hp || a.net[i].d_in != a.net[0].d_in ||
+            a.net[i].n_hidden != a.net[0].n_hidden || a.net[i].d_out != a.net[0].d_out)
+            return NAV_EINVAL;
+        a.dy[i] = dy[i];
+        a.masks[i] = masks[i];
+        a.h_top[i] = h_top ? h_top[i] : nullptr;
+        a.dz[i] = dz ? dz[i] : nullptr;
+        a.dx[i] = dx ? dx[i] : nullptr;
+        a.eslab[i] = edge_slabs ? edge_slabs[i] : nullptr;
+        if (M > 0 && (!a.dy[i] || !a.masks[i] || (save_mask && !a.dz[i]))) return NAV_EINVAL;
+        any_edges = any_edges || a.eslab[i];
+    }
     if (M == 0) return 0;
-    if (!dy || !masks || (save_mask && !dz) || (save_mask >> net->n_hidden) ||
-        (edge_slabs && (!in || in_col < 0 || in_col + net->d_in > ld_in)))
+    if ((save_mask >> a.net[0].n_hidden) ||
+        (any_edges && (!in || in_col < 0 || in_col + a.net[0].d_in > ld_in)))
         return NAV_EINVAL;
     a.M = M;
-    a.dy = dy;
     a.ld_dy = ld_dy;
-    a.masks = masks;
     a.in = in;
     a.ld_in = ld_in;
     a.in_col = in_col;
-    a.h_top = h_top;
-    a.dz = dz;
     a.save_mask = save_mask;
-    a.dx = dx;
-    a.eslab = edge_slabs;
-    a.ecount = edge_count(a.net);
-    return launch_bwd(a, S(stream));
+    a.ecount = edge_count(a.net[0]);
+    return launch_bwd(a, n_nets, S(stream));
 }
 
-int nav_mlp_wgrad(const nav_mlp* net, int64_t M, const float* in, int32_t ld_in, int32_t in_col,
-                  const float* acts, const float* dz, const float* dy, int32_t ld_dy,
-                  const uint16_t* masks, float* slabs, int32_t splits, void* stream) {
+int nav_mlp_wgrad(const nav_mlp* nets, int32_t n_nets, int64_t M, const float* in,
+                  int32_t ld_in, int32_t in_col, const float* const* acts,
+                  const float* const* dz, const float* const* dy, int32_t ld_dy,
+                  const uint16_t* const* masks, float* const* slabs, int32_t splits,
+                  void* stream) {
     WgradArgs a{};
-    if (!make_dev(net, &a.net) || M < 1 || splits < 1 || !in || !dy || ld_dy < 0 || !masks ||
-        !slabs || in_col < 0 || in_col + net->d_in > ld_in ||
-        (net->n_hidden > 2 && (!acts || !dz)))
+    if (!nets || n_nets < 1 || n_nets > 2 || M < 1 || splits < 1 || !in || !dy || ld_dy < 0 ||
+        !masks || !slabs)
         return NAV_EINVAL;
-    if (net->n_hidden < 2) return 0;
+    for (int i = 0; i < n_nets; ++i) {
+        if (!make_dev(&nets[i], &a.net[i]) || !dy[i] || !masks[i] || !slabs[i]) return NAV_EINVAL;
+        if (a.net[i].hp != a.net[0].hp || a.net[i].d_in != a.net[0].d_in ||
+            a.net[i].n_hidden != a.net[0].n_hidden || a.net[i].d_out != a.net[0].d_out)
+            return NAV_EINVAL;
+        a.acts[i] = acts ? acts[i] : nullptr;
+        a.dz[i] = dz ? dz[i] : nullptr;
+        if (a.net[i].n_hidden > 2 && (!a.acts[i] || !a.dz[i])) return NAV_EINVAL;
+        a.dy[i] = dy[i];
+        a.masks[i] = masks[i];
+        a.slabs[i] = slabs[i];
+    }
+    if (in_col < 0 || in_col + a.net[0].d_in > ld_in) return NAV_EINVAL;
+    if (a.net[0].n_hidden < 2) return 0;
     a.M = M;
     a.in = in;
     a.ld_in = ld_in;
     a.in_col = in_col;
-    a.acts = acts;
-    a.dz = dz;
-    a.dy = dy;
     a.ld_dy = ld_dy;
-    a.masks = masks;
-    a.slabs = slabs;
     a.splits = splits;
-    a.TA = (a.net.hp + WA_W - 1) / WA_W;
-    a.n_hid = (a.net.n_hidden - 1) * a.TA * a.TA;
+    a.TA = (a.net[0].hp + WA_W - 1) / WA_W;
+    a.n_hid = (a.net[0].n_hidden - 1) * a.TA * a.TA;
     const size_t lds = wgrad_lds_bytes();
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wgrad),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(k_wgrad, dim3((unsigned)(a.n_hid * splits)), dim3(kBlock), lds, S(stream),
-                       a);
+    hipLaunchKernelGGL(k_wgrad, dim3((unsigned)(n_nets * a.n_hid * splits)), dim3(kBlock), lds,
+                       S(stream), a);
     NAV_CHECK_LAUNCH();
     return 0;
 }
 
 int nav_grad_reduce(const nav_mlp* net, const float* hidden_slabs, int32_t splits,
                     const float* edge_slabs, int64_t edge_blocks, float* grad, void* stream) {
-    MlpDev d;
-    if (!make_dev(net, &d) || !grad || !edge_slabs || edge_blocks < 1 ||
-        (d.n_hidden > 1 && (!hidden_slabs || splits < 1)))
+    RedArgs a{};
+    if (!grad || !edge_slabs || edge_blocks < 1 || splits < 0 ||
+        !red_net(net, hidden_slabs, splits, edge_slabs, grad, &a.n[0]))
         return NAV_EINVAL;
-    const int64_t hw4 = hidden_w_count(d) / 4, e4 = edge_count(d) / 4;
-    const int nbh = (int)((hw4 + 63) / 64), nbe = (int)((e4 + 3) / 4);
-    hipLaunchKernelGGL(k_grad_reduce, dim3((unsigned)(nbh + nbe)), dim3(kBlock), 0, S(stream), d,
-                       reinterpret_cast<const float4*>(hidden_slabs), splits, hw4, nbh,
-                       reinterpret_cast<const float4*>(edge_slabs), edge_blocks, e4,
-                       reinterpret_cast<float4*>(grad));
+    a.splits = splits;
+    a.nblk = edge_blocks;
+    hipLaunchKernelGGL(k_grad_reduce<false>, dim3((unsigned)(a.n[0].nbh + a.n[0].nbe)),
+                       dim3(kBlock), 0, S(stream), a);
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_grad_reduce_adam(const nav_mlp* nets, int32_t n_nets, const float* const* hidden_slabs,
+                         int32_t splits, const float* const* edge_slabs, int64_t edge_blocks,
+                         float* const* grads, float* const* m, float* const* v, float beta1,
+                         float beta2, float eps, const float* step_size, const float* bc2_sqrt,
+                         void* stream) {
+    RedArgs a{};
+    if (!nets || n_nets < 1 || n_nets > 2 || !hidden_slabs || !edge_slabs || edge_blocks < 1 ||
+        splits < 0 || !m || !v || !step_size || !bc2_sqrt)
+        return NAV_EINVAL;
+    int blocks = 0;
+    for (int i = 0; i < n_nets; ++i) {
+        RedNet& rn = a.n[i];
+        if (!edge_slabs[i] || !m[i] || !v[i] ||
+            !red_net(&nets[i], hidden_slabs[i], splits, edge_slabs[i], grads ? grads[i] : nullptr,
+                     &rn))
+            return NAV_EINVAL;
+        rn.p = reinterpret_cast<float4*>(nets[i].params);
+        rn.m = reinterpret_cast<float4*>(m[i]);
+        rn.v = reinterpret_cast<float4*>(v[i]);
+        rn.step_size = step_size[i];
+        rn.bc2s = bc2_sqrt[i];
+        rn.pk = pack_info(rn.net, nets[i].packed);
+        blocks += rn.nbh + rn.nbe;
+    }
+    a.splits = splits;
+    a.nblk = edge_blocks;
+    a.b1w = 1.0f - beta1;
+    a.b2 = beta2;
+    a.omb2 = 1.0f - beta2;
+    a.eps = eps;
+    hipLaunchKernelGGL(k_grad_reduce<true>, dim3((unsigned)blocks), dim3(kBlock), 0, S(stream),
+                       a);
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_polyak_multi(const nav_mlp* targets, const nav_mlp* sources, int32_t n, float tau,
+                     void* stream) {
+    PolyArgs a{};
+    if (!targets || !sources || n < 1 || n > 4) return NAV_EINVAL;
+    for (int i = 0; i < n; ++i) {
+        MlpDev dt, ds;
+        if (!make_dev(&targets[i], &dt) || !make_dev(&sources[i], &ds) || dt.count != ds.count ||
+            dt.hp != ds.hp || dt.n_hidden != ds.n_hidden)
+            return NAV_EINVAL;
+        a.q[i].t = reinterpret_cast<float4*>(targets[i].params);
+        a.q[i].s = reinterpret_cast<const float4*>(sources[i].params);
+        a.q[i].n4 = dt.count / 4;
+        a.q[i].pk = pack_info(dt, targets[i].packed);
+        a.total4 += a.q[i].n4;
+    }
+    a.n = n;
+    a.omt = 1.0f - tau;
+    a.tau = tau;
+    hipLaunchKernelGGL(k_polyak_multi, dim3(grid_stride_blocks(a.total4)), dim3(kBlock), 0,
+                       S(stream), a);
     NAV_CHECK_LAUNCH();
     return 0;
 }

@@ -96,14 +96,20 @@ SIGNATURES = [
     ("nav_td3_critic_forward", C.c_int, [_P(NavMlp), C.c_int64, _vp, C.c_int32, C.c_int32, _vp,
                                          _vp, _vp, C.c_float, _P(_vp), _P(_vp), _P(_vp),
                                          _P(_vp), C.c_uint32, _P(_vp), _vp]),
-    ("nav_mlp_backward", C.c_int, [_P(NavMlp), C.c_int64, _vp, C.c_int32, _vp, _vp, C.c_int32,
-                                   C.c_int32, _vp, _vp, C.c_uint32, _vp, _vp, _vp]),
-    ("nav_mlp_wgrad", C.c_int, [_P(NavMlp), C.c_int64, _vp, C.c_int32, C.c_int32, _vp, _vp, _vp,
-                                C.c_int32, _vp, _vp, C.c_int32, _vp]),
+    ("nav_mlp_backward", C.c_int, [_P(NavMlp), C.c_int32, C.c_int64, _P(_vp), C.c_int32, _P(_vp),
+                                   _vp, C.c_int32, C.c_int32, _P(_vp), _P(_vp), C.c_uint32,
+                                   _P(_vp), _P(_vp), _vp]),
+    ("nav_mlp_wgrad", C.c_int, [_P(NavMlp), C.c_int32, C.c_int64, _vp, C.c_int32, C.c_int32,
+                                _P(_vp), _P(_vp), _P(_vp), C.c_int32, _P(_vp), _P(_vp), C.c_int32,
+                                _vp]),
     ("nav_grad_reduce", C.c_int, [_P(NavMlp), _vp, C.c_int32, _vp, C.c_int64, _vp, _vp]),
+    ("nav_grad_reduce_adam", C.c_int, [_P(NavMlp), C.c_int32, _P(_vp), C.c_int32, _P(_vp),
+                                       C.c_int64, _P(_vp), _P(_vp), _P(_vp), C.c_float, C.c_float,
+                                       C.c_float, _P(C.c_float), _P(C.c_float), _vp]),
     ("nav_adam", C.c_int, [_P(NavMlp), _vp, _vp, _vp, C.c_float, C.c_float, C.c_float,
                            C.c_float, C.c_float, _vp]),
     ("nav_polyak", C.c_int, [_P(NavMlp), _P(NavMlp), C.c_float, _vp]),
+    ("nav_polyak_multi", C.c_int, [_P(NavMlp), _P(NavMlp), C.c_int32, C.c_float, _vp]),
     ("nav_mlp_pack", C.c_int, [_P(NavMlp), _vp]),
     ("nav_replay_sample", C.c_int, [_P(NavReplay), C.c_int64, C.c_int64, _vp, C.c_uint32,
                                     C.c_uint32, C.c_uint32, _vp, _vp]),
@@ -172,6 +178,16 @@ def ptr(t):
         return None
     assert t.is_contiguous(), "nav tensors must be contiguous"
     return C.c_void_p(t.data_ptr())
+
+
+def parr(*tensors):
+    """C array of device pointers (None entries allowed) for the pointer-array parameters."""
+    return (C.c_void_p * len(tensors))(*[None if t is None else t.data_ptr() for t in tensors])
+
+
+def descs(*nets):
+    """C array of nav_mlp descriptors."""
+    return (NavMlp * len(nets))(*[n.desc() for n in nets])
 
 
 def stream_handle(stream=None):

@@ -13,7 +13,7 @@ import torch
 
 from . import config as K
 from . import prof
-from ._lib import NavMlp, lib, ptr, stream_handle
+from ._lib import descs, lib, parr, ptr, stream_handle
 from .mlp import DeviceMLP, forward
 
 
@@ -26,13 +26,18 @@ class _Adam:
         self.v = torch.zeros_like(net.params)
         self.step_count = 0
 
-    def step(self, grad, stream=None):
+    def advance(self):
+        """Next step's (step_size, bc2_sqrt) = (lr / (1 - b1^t), sqrt(1 - b2^t))."""
         self.step_count += 1
         bc1 = 1 - self.b1 ** self.step_count
         bc2 = 1 - self.b2 ** self.step_count
+        return self.lr / bc1, math.sqrt(bc2)
+
+    def step(self, grad, stream=None):
+        ss, bc2s = self.advance()
         d = self.net.desc()
         lib().nav_adam(C.byref(d), ptr(grad), ptr(self.m), ptr(self.v), self.b1, self.b2,
-                       self.eps, self.lr / bc1, math.sqrt(bc2), stream_handle(stream))
+                       self.eps, ss, bc2s, stream_handle(stream))
 
     def state_dict(self):
         return {"m": self.m.cpu(), "v": self.v.cpu(), "t": self.step_count}
@@ -94,36 +99,57 @@ class TD3:
         self.eslab1, self.eslab2 = f(self.nblk, ec), f(self.nblk, ec)
         self.eslab_a = f(self.nblk, L.nav_mlp_edge_count(2, 2, hp, nh))
         self.splits = max(1, min(64, B // 512))
-        self.hslab = f(self.splits, max(4, L.nav_mlp_hidden_count(hp, nh)))
+        hc = max(4, L.nav_mlp_hidden_count(hp, nh))
+        self.hslab, self.hslab2 = f(self.splits, hc), f(self.splits, hc)
         self.grad_a = f(self.actor_network.count)
         self.grad_c1 = f(self.critic_network_1.count)
         self.grad_c2 = f(self.critic_network_1.count)
         self._B = B
 
-    def _grads(self, net, M, inp, ld_in, in_col, acts, dz, dy, ld_dy, masks, eslab, grad, s):
-        """Hidden weight gradients (MFMA, split-M slabs) + the fixed-order reduce that folds them
-        and the fwd/bwd edge partials into the flat gradient."""
-        d = C.byref(net.desc())
+    def _grads_and_step(self, nets, opts, M, inp, ld_in, in_col, acts, dz, dy, ld_dy, masks,
+                        eslabs, grads, hslabs, s, stream):
+        """Hidden weight gradients of 1-2 same-shape nets (one MFMA launch, split-M slabs), then
+        the fixed-order reduce of those and the fwd/bwd edge partials fused with each net's Adam
+        step (robot.py:236-239). With a grad_hook (shared policy: RCCL all-reduce) the reduce
+        writes the flat gradients, the hook runs, then Adam steps separately."""
+        n = len(nets)
+        net = nets[0]
         if net.n_hidden > 1:
-            with prof.region("mlp_wgrad", prof.mlp_wgrad_flops(net.hidden, net.n_hidden, M)):
-                lib().nav_mlp_wgrad(d, M, ptr(inp), ld_in, in_col, ptr(acts), ptr(dz), ptr(dy),
-                                    ld_dy, ptr(masks), ptr(self.hslab), self.splits, s)
-        nbytes = 4.0 * (self.splits * (net.count - eslab.shape[1]) + eslab.numel() + net.count)
-        with prof.region("grad_reduce", nbytes):
-            lib().nav_grad_reduce(d, ptr(self.hslab), self.splits, ptr(eslab), self.nblk,
-                                  ptr(grad), s)
-        if self.grad_hook is not None:
-            self.grad_hook(grad)
+            with prof.region("mlp_wgrad", n * prof.mlp_wgrad_flops(net.hidden, net.n_hidden, M)):
+                lib().nav_mlp_wgrad(descs(*nets), n, M, ptr(inp), ld_in, in_col, parr(*acts),
+                                    parr(*dz), parr(*dy), ld_dy, parr(*masks), parr(*hslabs),
+                                    self.splits, s)
+        nbytes = sum(4.0 * (self.splits * (x.count - e.shape[1]) + e.numel() + 3 * x.count)
+                     for x, e in zip(nets, eslabs))
+        if self.grad_hook is None:
+            coeffs = [o.advance() for o in opts]
+            with prof.region("grad_reduce", nbytes):
+                lib().nav_grad_reduce_adam(
+                    descs(*nets), n, parr(*hslabs), self.splits, parr(*eslabs), self.nblk,
+                    parr(*grads), parr(*[o.m for o in opts]), parr(*[o.v for o in opts]),
+                    opts[0].b1, opts[0].b2, opts[0].eps,
+                    (C.c_float * n)(*[c[0] for c in coeffs]), (C.c_float * n)(*[c[1] for c in coeffs]),
+                    s)
+            return
+        for x, o, h, e, g in zip(nets, opts, hslabs, eslabs, grads):
+            with prof.region("grad_reduce", nbytes / n):
+                lib().nav_grad_reduce(C.byref(x.desc()), ptr(h), self.splits, ptr(e), self.nblk,
+                                      ptr(g), s)
+            self.grad_hook(g)
+            o.step(g, stream)
 
-    def _bwd(self, net, M, dy, ld_dy, masks, s, inp=None, ld_in=0, in_col=0, h_top=None, dz=None,
-             save_mask=0, dx=None, eslab=None):
-        edges = eslab is not None
-        with prof.region("mlp_bwd", prof.mlp_bwd_flops(net.d_in, net.d_out, net.hidden,
-                                                         net.n_hidden, M, dx is not None, edges,
-                                                         h_top is not None)):
-            lib().nav_mlp_backward(C.byref(net.desc()), M, ptr(dy), ld_dy, ptr(masks), ptr(inp),
-                                   ld_in, in_col, ptr(h_top), ptr(dz), save_mask, ptr(dx),
-                                   ptr(eslab), s)
+    def _bwd(self, nets, M, dy, ld_dy, masks, s, inp=None, ld_in=0, in_col=0, h_top=None,
+             dz=None, save_mask=0, dx=None, eslab=None):
+        net = nets[0]
+        n = len(nets)
+        with prof.region("mlp_bwd", n * prof.mlp_bwd_flops(net.d_in, net.d_out, net.hidden,
+                                                             net.n_hidden, M, dx is not None,
+                                                             eslab is not None,
+                                                             h_top is not None)):
+            nil = [None] * n
+            lib().nav_mlp_backward(descs(*nets), n, M, parr(*dy), ld_dy, parr(*masks), ptr(inp),
+                                   ld_in, in_col, parr(*(h_top or nil)), parr(*(dz or nil)),
+                                   save_mask, parr(*(dx or nil)), parr(*(eslab or nil)), s)
 
     def _sample(self, replay, B, out, idx=None, stream=None):
         """ReplayBuffer.sample (robot.py:98-115) into a [B][8] batch."""
@@ -153,23 +179,22 @@ class TD3:
         # gradient and the output layer's gradient partials
         c1, c2 = self.critic_network_1, self.critic_network_2
         mid = c1.middle_layers()
-        arr = lambda *t: (C.c_void_p * len(t))(*[x.data_ptr() for x in t])  # noqa: E731
-        descs = (NavMlp * 2)(c1.desc(), c2.desc())
         with prof.region("mlp_fwd", 2 * prof.mlp_fwd_flops(4, 1, c1.hidden, c1.n_hidden, B)):
-            lib().nav_td3_critic_forward(descs, B, ptr(bt), 8, 0, ptr(bt), ptr(self.q1t),
-                                         ptr(self.q2t), c.gamma, arr(self.dq1, self.dq2),
-                                         arr(self.loss_part[0], self.loss_part[1]),
-                                         arr(self.eslab1, self.eslab2), arr(self.acts1, self.acts2),
-                                         mid, arr(self.mask1, self.mask2), s)
-        for net, opt, acts, mask, dz, dq, es, grad in (
-                (c1, self.critic_optimizer_1, self.acts1, self.mask1, self.dz1, self.dq1,
-                 self.eslab1, self.grad_c1),
-                (c2, self.critic_optimizer_2, self.acts2, self.mask2, self.dz2, self.dq2,
-                 self.eslab2, self.grad_c2)):
-            self._bwd(net, B, dq, 1, mask, s, inp=bt, ld_in=8, in_col=0, dz=dz, save_mask=mid,
-                      eslab=es)
-            self._grads(net, B, bt, 8, 0, acts, dz, dq, 1, mask, es, grad, s)
-            opt.step(grad, stream)
+            lib().nav_td3_critic_forward(descs(c1, c2), B, ptr(bt), 8, 0, ptr(bt), ptr(self.q1t),
+                                         ptr(self.q2t), c.gamma, parr(self.dq1, self.dq2),
+                                         parr(self.loss_part[0], self.loss_part[1]),
+                                         parr(self.eslab1, self.eslab2),
+                                         parr(self.acts1, self.acts2), mid,
+                                         parr(self.mask1, self.mask2), s)
+        # both critics' backward, weight gradients and reduce + Adam: one launch each
+        crit, opts = [c1, c2], [self.critic_optimizer_1, self.critic_optimizer_2]
+        self._bwd(crit, B, [self.dq1, self.dq2], 1, [self.mask1, self.mask2], s, inp=bt, ld_in=8,
+                  in_col=0, dz=[self.dz1, self.dz2], save_mask=mid,
+                  eslab=[self.eslab1, self.eslab2])
+        self._grads_and_step(crit, opts, B, bt, 8, 0, [self.acts1, self.acts2],
+                             [self.dz1, self.dz2], [self.dq1, self.dq2], 1,
+                             [self.mask1, self.mask2], [self.eslab1, self.eslab2],
+                             [self.grad_c1, self.grad_c2], [self.hslab, self.hslab2], s, stream)
 
     def critic_loss_values(self):
         """(loss1, loss2) of the last train_critic (mean squared TD error), synchronising."""
@@ -193,14 +218,14 @@ class TD3:
                 stream=stream)
         forward([c1], bt, 8, 0, [self.q1], 1, 0, B, masks=[self.mask1], stream=stream)
         # backprop -mean(Q) through critic 1 to its action input (its own grads are discarded)
-        self._bwd(c1, B, self.dq_actor, 0, self.mask1, s, dx=self.dx)
+        self._bwd([c1], B, [self.dq_actor], 0, [self.mask1], s, dx=[self.dx])
         da = self.dx.view(-1)[2:]  # dL/da = columns 2..3 of dL/dx, row stride 4
-        self._bwd(net, B, da, 4, self.mask_a, s, inp=bt, ld_in=8, in_col=0,
-                  h_top=self.acts_a[net.n_hidden - 1], dz=self.dz_a,
-                  save_mask=net.middle_layers(), eslab=self.eslab_a)
-        self._grads(net, B, bt, 8, 0, self.acts_a, self.dz_a, da, 4, self.mask_a, self.eslab_a,
-                    self.grad_a, s)
-        self.actor_optimizer.step(self.grad_a, stream)
+        self._bwd([net], B, [da], 4, [self.mask_a], s, inp=bt, ld_in=8, in_col=0,
+                  h_top=[self.acts_a[net.n_hidden - 1]], dz=[self.dz_a],
+                  save_mask=net.middle_layers(), eslab=[self.eslab_a])
+        self._grads_and_step([net], [self.actor_optimizer], B, bt, 8, 0, [self.acts_a],
+                             [self.dz_a], [da], 4, [self.mask_a], [self.eslab_a], [self.grad_a],
+                             [self.hslab], s, stream)
 
     def actor_loss_value(self):
         return -(self.q1.sum() / self._B).item()
@@ -211,10 +236,12 @@ class TD3:
                          stream_handle(stream))
 
     def soft_update_all(self, stream=None):
+        """The three soft updates of robot.py:283-285 in one launch."""
         t = self.cfg.tau
-        self.soft_update(self.target_actor, self.actor_network, t, stream)
-        self.soft_update(self.target_critic_network_1, self.critic_network_1, t, stream)
-        self.soft_update(self.target_critic_network_2, self.critic_network_2, t, stream)
+        lib().nav_polyak_multi(
+            descs(self.target_actor, self.target_critic_network_1, self.target_critic_network_2),
+            descs(self.actor_network, self.critic_network_1, self.critic_network_2), 3, t,
+            stream_handle(stream))
 
     # robot.py:258-285
     def td3_update(self, replay, num_epochs=None, idx_fn=None, eps_fn=None, stream=None,

@@ -137,7 +137,7 @@ def _grad_flat_vs_autograd(net, tl, gflat, d_in, d_out, nh):
 def test_backward_and_weight_grads_vs_autograd(nav, d_in, d_out, hidden, nh, M):
     """Row backward + per-block edge partials + recomputing hidden weight gradients + reduce
     against torch autograd; every gradient entry must be written (NaN-filled buffers)."""
-    from nav._lib import lib, ptr, stream_handle
+    from nav._lib import descs, lib, parr, ptr, stream_handle
     from nav.mlp import forward
     net, layers = make_net(d_in, d_out, hidden, nh, 11)
     x = (torch.randn(M, d_in) * 10).contiguous()
@@ -156,14 +156,14 @@ def test_backward_and_weight_grads_vs_autograd(nav, d_in, d_out, hidden, nh, M):
     nblk = L.nav_mlp_row_blocks(M)
     eslab = torch.full((nblk, L.nav_mlp_edge_count(d_in, d_out, net.hp, nh)), float("nan"),
                        device=DEV)
-    L.nav_mlp_backward(C.byref(net.desc()), M, ptr(dyd), d_out, ptr(masks), ptr(xd), d_in, 0,
-                       ptr(acts[nh - 1]), ptr(dz), net.middle_layers(), ptr(dx), ptr(eslab), s)
+    L.nav_mlp_backward(descs(net), 1, M, parr(dyd), d_out, parr(masks), ptr(xd), d_in, 0,
+                       parr(acts[nh - 1]), parr(dz), net.middle_layers(), parr(dx), parr(eslab), s)
     splits = 7
     hs = torch.full((splits, max(4, L.nav_mlp_hidden_count(net.hp, nh))), float("nan"),
                     device=DEV)
     grad = torch.full((net.count,), float("nan"), device=DEV)
-    L.nav_mlp_wgrad(C.byref(net.desc()), M, ptr(xd), d_in, 0, ptr(acts), ptr(dz), ptr(dyd), d_out,
-                    ptr(masks), ptr(hs), splits, s)
+    L.nav_mlp_wgrad(descs(net), 1, M, ptr(xd), d_in, 0, parr(acts), parr(dz), parr(dyd), d_out,
+                    parr(masks), parr(hs), splits, s)
     L.nav_grad_reduce(C.byref(net.desc()), ptr(hs), splits, ptr(eslab), nblk, ptr(grad), s)
     # torch autograd reference
     tl = [(W.clone().requires_grad_(True), b.clone().requires_grad_(True)) for W, b in layers]
@@ -180,7 +180,7 @@ def test_backward_and_weight_grads_vs_autograd(nav, d_in, d_out, hidden, nh, M):
 def test_td3_critic_forward_gradients_vs_autograd(nav, hidden, nh, B):
     """train_critic's fused online forward (robot.py:341-361): TD target, MSE loss and gradient,
     then backward + weight gradients of both critics vs torch autograd of mse_loss(Q(s,a), y)."""
-    from nav._lib import NavMlp, lib, ptr, stream_handle
+    from nav._lib import NavMlp, descs, lib, parr, ptr, stream_handle
     nets = [make_net(4, 1, hidden, nh, 31 + k) for k in range(2)]
     g = torch.Generator().manual_seed(5)
     batch = torch.zeros(B, 8)
@@ -207,14 +207,16 @@ def test_td3_critic_forward_gradients_vs_autograd(nav, hidden, nh, B):
                              ptr(bt), ptr(q1d), ptr(q2d), 0.99, arr(dq), arr([lp[0], lp[1]]),
                              arr(es), arr(acts), mid, arr(masks), s)
     splits = 5
-    hs = torch.zeros(splits, max(4, L.nav_mlp_hidden_count(hp, nh)), device=DEV)
+    hs = [torch.zeros(splits, max(4, L.nav_mlp_hidden_count(hp, nh)), device=DEV)
+          for _ in range(2)]
+    dn = descs(*[n for n, _ in nets])
+    L.nav_mlp_backward(dn, 2, B, parr(*dq), 1, parr(*masks), ptr(bt), 8, 0, None, parr(*dz),
+                       mid, None, parr(*es), s)
+    L.nav_mlp_wgrad(dn, 2, B, ptr(bt), 8, 0, parr(*acts), parr(*dz), parr(*dq), 1, parr(*masks),
+                    parr(*hs), splits, s)
     for k, (net, layers) in enumerate(nets):
         grad = torch.full((net.count,), float("nan"), device=DEV)
-        L.nav_mlp_backward(C.byref(net.desc()), B, ptr(dq[k]), 1, ptr(masks[k]), ptr(bt), 8, 0,
-                           None, ptr(dz[k]), mid, None, ptr(es[k]), s)
-        L.nav_mlp_wgrad(C.byref(net.desc()), B, ptr(bt), 8, 0, ptr(acts[k]), ptr(dz[k]),
-                        ptr(dq[k]), 1, ptr(masks[k]), ptr(hs), splits, s)
-        L.nav_grad_reduce(C.byref(net.desc()), ptr(hs), splits, ptr(es[k]), nblk, ptr(grad), s)
+        L.nav_grad_reduce(C.byref(net.desc()), ptr(hs[k]), splits, ptr(es[k]), nblk, ptr(grad), s)
         tl = [(W.clone().requires_grad_(True), b.clone().requires_grad_(True)) for W, b in layers]
         q = torch_mlp(tl, batch[:, :4])
         loss = torch.nn.functional.mse_loss(q, y.unsqueeze(1))
@@ -266,6 +268,48 @@ def test_adam_and_polyak_vs_oracle(nav):
     for (W0, b0), (W1, b1), (Ws, bs) in zip(before, after, got):
         assert torch.equal(W1, W0 * (1.0 - 0.001) + Ws * 0.001)
         assert torch.equal(b1, b0 * (1.0 - 0.001) + bs * 0.001)
+
+
+def test_fused_reduce_adam_and_polyak_multi_bitwise(nav):
+    """nav_grad_reduce_adam (2 nets, one launch) == nav_grad_reduce + nav_adam per net, and
+    nav_polyak_multi == nav_polyak per pair, bit for bit (same op order)."""
+    from nav._lib import descs, lib, parr, ptr, stream_handle
+    L = lib()
+    s = stream_handle()
+    for hidden, nh in ((200, 3), (256, 2), (64, 1)):
+        nets = [make_net(4, 1, hidden, nh, 40 + k)[0] for k in range(2)]
+        twins = [make_net(4, 1, hidden, nh, 40 + k)[0] for k in range(2)]
+        hp = nets[0].hp
+        splits, nblk = 3, 5
+        hc, ec = max(4, L.nav_mlp_hidden_count(hp, nh)), L.nav_mlp_edge_count(4, 1, hp, nh)
+        hs = [torch.randn(splits, hc, device=DEV) for _ in range(2)]
+        es = [torch.randn(nblk, ec, device=DEV) for _ in range(2)]
+        m = [torch.randn(n.count, device=DEV) * 1e-3 for n in nets]
+        v = [torch.rand(n.count, device=DEV) * 1e-4 for n in nets]
+        m2, v2 = [x.clone() for x in m], [x.clone() for x in v]
+        g_sep = [torch.zeros(n.count, device=DEV) for n in nets]
+        g_fus = [torch.zeros(n.count, device=DEV) for n in nets]
+        ss, bc = (C.c_float * 2)(1e-3, 2e-3), (C.c_float * 2)(0.5, 0.25)
+        L.nav_grad_reduce_adam(descs(*nets), 2, parr(*hs), splits, parr(*es), nblk, parr(*g_fus),
+                               parr(*m), parr(*v), 0.9, 0.999, 1e-8, ss, bc, s)
+        for k in range(2):
+            L.nav_grad_reduce(C.byref(twins[k].desc()), ptr(hs[k]), splits, ptr(es[k]), nblk,
+                              ptr(g_sep[k]), s)
+            L.nav_adam(C.byref(twins[k].desc()), ptr(g_sep[k]), ptr(m2[k]), ptr(v2[k]), 0.9,
+                       0.999, 1e-8, ss[k], bc[k], s)
+        for k in range(2):
+            assert torch.equal(g_fus[k], g_sep[k])
+            assert torch.equal(nets[k].params, twins[k].params)
+            assert torch.equal(nets[k].packed, twins[k].packed)
+            assert torch.equal(m[k], m2[k]) and torch.equal(v[k], v2[k])
+        tg = [make_net(4, 1, hidden, nh, 50 + k)[0] for k in range(3)]
+        tg2 = [make_net(4, 1, hidden, nh, 50 + k)[0] for k in range(3)]
+        src = [nets[0], nets[1], twins[0]]
+        L.nav_polyak_multi(descs(*tg), descs(*src), 3, 0.001, s)
+        for t2, sr in zip(tg2, src):
+            L.nav_polyak(C.byref(t2.desc()), C.byref(sr.desc()), 0.001, s)
+        for t1, t2 in zip(tg, tg2):
+            assert torch.equal(t1.params, t2.params) and torch.equal(t1.packed, t2.packed)
 
 
 def test_td3_update_vs_oracle_and_reference(nav):

@@ -88,7 +88,8 @@ def test_host_argument_validation(navlib):
     from nav._lib import NavMlp
     d = NavMlp(4, 1, 256, 256, 2, 16, 16)
     with pytest.raises(NavError, match="invalid argument"):  # no masks
-        navlib.nav_mlp_wgrad(C.byref(d), 64, 16, 4, 0, None, None, 16, 1, None, 16, 4, None)
+        navlib.nav_mlp_wgrad(C.byref(d), 1, 64, 16, 4, 0, None, None,
+                             (C.c_void_p * 1)(16), 1, None, (C.c_void_p * 1)(16), 4, None)
     assert navlib.nav_mlp_edge_count(4, 1, 256, 2) == 4 * 256 + 256 + 256 + 256 + 4
     assert navlib.nav_mlp_hidden_count(256, 2) == 256 * 256
     empty = NavEnvSoa(0, None, None, None, None, None, None, None, None, None)

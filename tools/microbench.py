@@ -38,7 +38,7 @@ def main():
     ap.add_argument("--quick", action="store_true", help="MLP kernels only (for counter runs)")
     args = ap.parse_args()
     from nav import prof
-    from nav._lib import NavMlp, lib, ptr, stream_handle
+    from nav._lib import NavMlp, descs, lib, parr, ptr, stream_handle
     from nav.mlp import DeviceMLP, forward
     from nav.trainer import VecTrainer
     dev = "cuda"
@@ -62,34 +62,36 @@ def main():
     dq = [torch.zeros(B, device=dev) for _ in range(2)]
     lp = torch.zeros(2, nblk, device=dev)
     arr = lambda t: (C.c_void_p * 2)(*[v.data_ptr() for v in t])  # noqa: E731
-    descs = (NavMlp * 2)(*[c.desc() for c in crit])
+    cdescs = (NavMlp * 2)(*[c.desc() for c in crit])
     s = stream_handle()
     mid = crit[0].middle_layers()
-    us = timeit(lambda: lib().nav_td3_critic_forward(descs, B, ptr(bt), 8, 0, ptr(bt), ptr(q[0]),
+    us = timeit(lambda: lib().nav_td3_critic_forward(cdescs, B, ptr(bt), 8, 0, ptr(bt), ptr(q[0]),
                                                      ptr(q[1]), 0.99, arr(dq), arr([lp[0], lp[1]]),
                                                      arr(es), arr(acts), mid, arr(masks), s))
     res["fwd_twin_critic_loss"] = {"us": us, "TFs": 2 * f1 / us / 1e6}
     dz = torch.zeros_like(acts[0])
-    d = crit[0].desc()
-    us = timeit(lambda: lib().nav_mlp_backward(C.byref(d), B, ptr(dq[0]), 1, ptr(masks[0]),
-                                               ptr(bt), 8, 0, None, ptr(dz), mid, None, ptr(es[0]),
-                                               s))
+    dz2 = torch.zeros_like(acts[0])
+    us = timeit(lambda: lib().nav_mlp_backward(descs(*crit), 2, B, parr(*dq), 1, parr(*masks),
+                                               ptr(bt), 8, 0, None, parr(dz, dz2), mid, None,
+                                               parr(*es), s))
     fb = prof.mlp_bwd_flops(4, 1, H, L, B, False, True)
-    res["bwd_critic_edges"] = {"us": us, "TFs": fb / us / 1e6}
+    res["bwd_twin_critic_edges"] = {"us": us, "TFs": 2 * fb / us / 1e6}
     dxb = torch.zeros(B, 4, device=dev)
-    us = timeit(lambda: lib().nav_mlp_backward(C.byref(d), B, ptr(dq[0]), 1, ptr(masks[0]), None,
-                                               0, 0, None, None, 0, ptr(dxb), None, s))
+    us = timeit(lambda: lib().nav_mlp_backward(descs(crit[0]), 1, B, parr(dq[0]), 1,
+                                               parr(masks[0]), None, 0, 0, None, None, 0,
+                                               parr(dxb), None, s))
     res["bwd_critic_dx"] = {"us": us, "TFs": prof.mlp_bwd_flops(4, 1, H, L, B, True) / us / 1e6}
     hc = max(4, lib().nav_mlp_hidden_count(crit[0].hp, L))
     grad = torch.zeros(crit[0].count, device=dev)
     fw = prof.mlp_wgrad_flops(H, L, B)
     for splits in (32, 64, 128):
         sl = torch.zeros(splits, hc, device=dev)
-        us_w = timeit(lambda: lib().nav_mlp_wgrad(C.byref(d), B, ptr(bt), 8, 0, ptr(acts[0]),
-                                                  ptr(dz), ptr(dq[0]), 1, ptr(masks[0]), ptr(sl),
-                                                  splits, s))
-        us_r = timeit(lambda: lib().nav_grad_reduce(C.byref(d), ptr(sl), splits, ptr(es[0]), nblk,
-                                                    ptr(grad), s))
+        sl2 = torch.zeros(splits, hc, device=dev)
+        us_w = timeit(lambda: lib().nav_mlp_wgrad(descs(*crit), 2, B, ptr(bt), 8, 0, parr(*acts),
+                                                  parr(dz, dz2), parr(*dq), 1, parr(*masks),
+                                                  parr(sl, sl2), splits, s)) / 2
+        us_r = timeit(lambda: lib().nav_grad_reduce(C.byref(crit[0].desc()), ptr(sl), splits,
+                                                    ptr(es[0]), nblk, ptr(grad), s))
         res[f"wgrad_splits{splits}"] = {"wgrad_us": us_w, "TFs": fw / us_w / 1e6,
                                          "reduce_us": us_r}
     if args.quick:
