@@ -222,6 +222,32 @@ int nav_mlp_forward(const nav_mlp* nets, int32_t n_nets, int64_t M, const float*
                     float noise_clip, float max_action, uint32_t seed_lo, uint32_t seed_hi,
                     uint32_t counter, float* const* acts, uint32_t save_mask,
                     uint16_t* const* masks, void* stream);
+/* train_critic's row-local part (robot.py:329-353) in one launch: per batch row b, sample
+ * rows[k] of the replay ring (k = idx[b] if given, else Philox NAV_TAG_SAMPLE at 2*counter, with
+ * replacement over [0, size)) into batch [B][8]; a' = clamp(target_actor(s') + clamp(policy_noise
+ * * eps, +-noise_clip), +-max_action) with eps from `eps` [B][2] if given else Philox
+ * NAV_TAG_TNOISE at counter; y = r + gamma*min(target_critics[0](s', a'), target_critics[1](s',
+ * a'))*(1 - done); then both online critics on (s, a) as nav_td3_critic_forward (dq, loss_part,
+ * edge_slabs, acts/save_mask, masks). */
+int nav_td3_critic_rows(const nav_mlp* target_actor, const nav_mlp* target_critics,
+                        const nav_mlp* critics, const nav_replay* replay, int64_t size,
+                        int64_t B, const int64_t* idx, uint32_t seed_lo, uint32_t seed_hi,
+                        uint32_t counter, const float* eps, float policy_noise,
+                        float noise_clip, float max_action, float gamma, float* batch,
+                        float* const* dq, float* const* loss_part, float* const* edge_slabs,
+                        float* const* acts, uint32_t save_mask, uint16_t* const* masks,
+                        void* stream);
+/* train_actor's row-local part (robot.py:382-390) in one launch: sample rows (Philox
+ * NAV_TAG_SAMPLE at 2*counter + 1, or idx) into batch [B][8]; actor forward on s (ReLU bits to
+ * masks_actor, activations to acts for save_mask bits, which must include the top layer);
+ * q [B] (nullable) = critic(s, actor(s)); dL/da of L = -mean(q) through the critic (masks_critic)
+ * into da [B][2]; the actor's row backward with dz_save_mask rows to dz and its edge partials. */
+int nav_td3_actor_rows(const nav_mlp* actor, const nav_mlp* critic, const nav_replay* replay,
+                       int64_t size, int64_t B, const int64_t* idx, uint32_t seed_lo,
+                       uint32_t seed_hi, uint32_t counter, float* batch, float* q, float* da,
+                       float* acts, uint32_t save_mask, float* dz, uint32_t dz_save_mask,
+                       uint16_t* masks_actor, uint16_t* masks_critic, float* edge_slabs,
+                       void* stream);
 /* u16 words of the ReLU mask image for M rows (layout: [n_hidden][row tiles][hp/32][64]). */
 int64_t nav_mlp_mask_count(int32_t hidden_pad, int32_t n_hidden, int64_t M);
 /* Parameter gradients are produced in two parts that nav_grad_reduce combines:

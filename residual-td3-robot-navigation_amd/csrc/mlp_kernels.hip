@@ -301,29 +301,34 @@ NAV_DEV void edge_w0(const float* act, int S_, int hp, const float* xin, int d_i
     if (d_in > 3) out[n * d_in + 3] = s3;
 }
 
-// OUT_LOSS (d_out = 1): q from the output-layer partials, the TD target of robot.py:341-345
-// y = r + gamma * min(q1', q2') * (1 - done), mse_loss's gradient dq = (q - y) * 2/B, the block's
+// output j of block row rloc from fwd_net's partial sums
+template <int RT>
+NAV_DEV float out_y(const MlpDev& net, const float* red, int rloc, int j) {
+    constexpr int TM = RT * 32, PARTS = kBlock / TM;
+    float y = 0.f;
+#pragma unroll
+    for (int p = 0; p < PARTS; ++p) y += red[(j * PARTS + p) * TM + rloc];
+    return y + net.params[net.b_off[net.n_hidden] + j];
+}
+
+// OUT_LOSS (d_out = 1): q from the output-layer partials against the TD target yt of the thread's
+// row (robot.py:341-345, from the caller), mse_loss's gradient dq = (q - yt) * 2/B, the block's
 // sum of (q - y)^2, and the output layer's gradient partials dWo = dq^T h_top, dbo = sum dq while
 // h_top is still in LDS. `red` = the [2][PARTS][TM] partial-sum scratch (second half reused).
 template <int NT, int RT>
-NAV_DEV void loss_epilogue(const FwdArgs& a, const MlpDev& net, const float* act, float* red,
-                           int64_t row0) {
-    constexpr int hp = NT * 32, SS = hp + 4, TM = RT * 32, PARTS = kBlock / TM;
-    const int tid = threadIdx.x, nh = net.n_hidden, q = blockIdx.y;
+NAV_DEV void loss_epilogue(const MlpDev& net, const float* act, float* red, int64_t row0,
+                           int64_t M, float yt, float norm, float* dq, float* loss_slot,
+                           float* es) {
+    constexpr int hp = NT * 32, SS = hp + 4, TM = RT * 32;
+    const int tid = threadIdx.x;
     const int64_t r = row0 + tid;
     float dqv = 0.f, e2 = 0.f;
-    if (tid < TM && r < a.M) {
-        float y = 0.f;
-#pragma unroll
-        for (int p = 0; p < PARTS; ++p) y += red[p * TM + tid];
-        y += net.params[net.b_off[nh]];
-        const float rw = a.batch[r * NAV_ROW + 4], dn = a.batch[r * NAV_ROW + 7];
-        const float mn = fminf(a.qt[0][r], a.qt[1][r]);
-        const float yt = rw + (a.gamma * mn) * (1.0f - dn);
+    if (tid < TM && r < M) {
+        const float y = out_y<RT>(net, red, tid, 0);
         const float e = y - yt;
-        dqv = e * a.norm;
+        dqv = e * norm;
         e2 = e * e;
-        a.dq[q][r] = dqv;
+        dq[r] = dqv;
     }
     float* dqs = red + kBlock;  // [TM] dq, then [kBlock/64] wave sums
     float* ws = dqs + TM;
@@ -332,66 +337,34 @@ NAV_DEV void loss_epilogue(const FwdArgs& a, const MlpDev& net, const float* act
     if ((tid & 63) == 0) ws[tid >> 6] = w;
     __syncthreads();
     if (tid == 0) {
-        float s = 0.f;
+        float sum = 0.f;
 #pragma unroll
-        for (int k = 0; k < kBlock / 64; ++k) s += ws[k];
-        a.loss_part[q][blockIdx.x] = s;
+        for (int k = 0; k < kBlock / 64; ++k) sum += ws[k];
+        *loss_slot = sum;
     }
-    if (!a.eslab[q]) return;
-    float* es = a.eslab[q] + (int64_t)blockIdx.x * a.ecount;
+    if (!es) return;
     if (tid < hp) {
-        float s = 0.f;
+        float sum = 0.f;
 #pragma unroll 8
-        for (int rr = 0; rr < TM; ++rr) s = fmaf(dqs[rr], act[rr * SS + tid], s);
-        es[e_wo(net) + tid] = s;
+        for (int rr = 0; rr < TM; ++rr) sum = fmaf(dqs[rr], act[rr * SS + tid], sum);
+        es[e_wo(net) + tid] = sum;
     }
     if (tid < 4) {  // bo and its 3 padding floats
-        float s = 0.f;
+        float sum = 0.f;
         if (tid == 0)
-            for (int rr = 0; rr < TM; ++rr) s += dqs[rr];
-        es[e_bo(net) + tid] = s;
+            for (int rr = 0; rr < TM; ++rr) sum += dqs[rr];
+        es[e_bo(net) + tid] = sum;
     }
 }
 
-template <int NT, int RT, int IN_MODE, int OUT_MODE>
-__global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float smem[];
+template <int NT, int RT>
+NAV_DEV void fwd_net(const MlpDev& net, float* act, const float* xin, float* red,
+                     uint16_t* masks, int64_t n_rt, float* act_save, uint32_t save_mask,
+                     int64_t row0, int64_t M, int64_t rt0) {
     constexpr int hp = NT * 32, SS = hp + 4, TM = RT * 32;
     const int tid = threadIdx.x, lane = tid & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
-    const MlpDev& net = a.net[blockIdx.y];
-    float* act_save = a.acts[blockIdx.y];
-    uint16_t* masks = a.masks[blockIdx.y];
-    const int64_t M = a.M;
-    const int64_t row0 = (int64_t)blockIdx.x * TM;
-    const int64_t rt0 = (int64_t)blockIdx.x * RT;
-    const int64_t n_rt = mask_rowtiles(M);
-    float* act = smem;
-    float* xin = smem + TM * SS;  // [TM][4]
     const int d_in = net.d_in, d_out = net.d_out, nh = net.n_hidden;
     const WaveCols<NT> wc(wv);
-
-    // ---- input rows -> xin
-    if (tid < TM) {
-        const int64_t r = row0 + tid;
-        float x[4] = {0.f, 0.f, 0.f, 0.f};
-        if (r < M) {
-            if (IN_MODE == IN_F32) {
-                const float* src = a.in + r * a.ld_in + a.in_col;
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    if (k < d_in) x[k] = src[k];
-            } else {
-                // robot.py:556 baseline = state - goal, then torch.FloatTensor (f64 -> f32)
-                const double2 s = reinterpret_cast<const double2*>(a.state)[r];
-                const double2 g = reinterpret_cast<const double2*>(a.goal)[r];
-                x[0] = (float)(s.x - g.x);
-                x[1] = (float)(s.y - g.y);
-            }
-        }
-        *reinterpret_cast<float4*>(xin + tid * 4) = make_float4(x[0], x[1], x[2], x[3]);
-    }
-    __syncthreads();
-
     // ---- layer 0 (K = d_in) on the VALU, written in the C layout of the wave's column tiles
     {
         const float* W0 = net.params + net.w_off[0];
@@ -429,7 +402,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
         }
     }
     __syncthreads();
-    if (act_save && (a.save_mask & 1u)) copy_rows<NT, RT>(act, SS, act_save, row0, M);
+    if (act_save && (save_mask & 1u)) copy_rows<NT, RT>(act, SS, act_save, row0, M);
 
     // ---- hidden x hidden layers on MFMA
     for (int L = 1; L < nh; ++L) {
@@ -449,7 +422,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
         store_layer<NT, RT>(acc, act, SS, masks ? masks + (size_t)L * n_rt * NT * 64 : nullptr,
                             rt0);
         __syncthreads();
-        if (act_save && ((a.save_mask >> L) & 1u))
+        if (act_save && ((save_mask >> L) & 1u))
             copy_rows<NT, RT>(act, SS, act_save + (int64_t)L * M * hp, row0, M);
     }
 
@@ -473,27 +446,71 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
                 s1 = fmaf(x.z, w1.z, s1); s1 = fmaf(x.w, w1.w, s1);
             }
         }
-        float* red = xin + TM * 4;  // [2][PARTS][TM]
         red[part * TM + rl] = s0;
         red[(PARTS + part) * TM + rl] = s1;
     }
     __syncthreads();
+}
+
+template <int NT, int RT, int IN_MODE, int OUT_MODE>
+__global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    constexpr int hp = NT * 32, SS = hp + 4, TM = RT * 32;
+    const int tid = threadIdx.x;
+    const MlpDev& net = a.net[blockIdx.y];
+    float* act_save = a.acts[blockIdx.y];
+    uint16_t* masks = a.masks[blockIdx.y];
+    const int64_t M = a.M;
+    const int64_t row0 = (int64_t)blockIdx.x * TM;
+    const int64_t rt0 = (int64_t)blockIdx.x * RT;
+    const int64_t n_rt = mask_rowtiles(M);
+    float* act = smem;
+    float* xin = smem + TM * SS;  // [TM][4]
+    const int d_in = net.d_in, d_out = net.d_out;
+
+    // ---- input rows -> xin
+    if (tid < TM) {
+        const int64_t r = row0 + tid;
+        float x[4] = {0.f, 0.f, 0.f, 0.f};
+        if (r < M) {
+            if (IN_MODE == IN_F32) {
+                const float* src = a.in + r * a.ld_in + a.in_col;
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (k < d_in) x[k] = src[k];
+            } else {
+                // robot.py:556 baseline = state - goal, then torch.FloatTensor (f64 -> f32)
+                const double2 s = reinterpret_cast<const double2*>(a.state)[r];
+                const double2 g = reinterpret_cast<const double2*>(a.goal)[r];
+                x[0] = (float)(s.x - g.x);
+                x[1] = (float)(s.y - g.y);
+            }
+        }
+        *reinterpret_cast<float4*>(xin + tid * 4) = make_float4(x[0], x[1], x[2], x[3]);
+    }
+    __syncthreads();
+
+    float* red = xin + TM * 4;  // [2][PARTS][TM]
+    fwd_net<NT, RT>(net, act, xin, red, masks, n_rt, act_save, a.save_mask, row0, M, rt0);
     const int rloc = tid % TM;
     const int j = tid / TM;
     const int64_t r = row0 + rloc;
     if (OUT_MODE == OUT_LOSS) {
-        loss_epilogue<NT, RT>(a, net, act, xin + TM * 4, row0);
+        // robot.py:341-345 TD target y = r + gamma * min(q1', q2') * (1 - done)
+        float yt = 0.f;
+        if (tid < TM && r < M) {
+            const float rw = a.batch[r * NAV_ROW + 4], dn = a.batch[r * NAV_ROW + 7];
+            const float mn = fminf(a.qt[0][r], a.qt[1][r]);
+            yt = rw + (a.gamma * mn) * (1.0f - dn);
+        }
+        const int q = blockIdx.y;
+        loss_epilogue<NT, RT>(net, act, red, row0, M, yt, a.norm, a.dq[q],
+                              a.loss_part[q] + blockIdx.x,
+                              a.eslab[q] ? a.eslab[q] + (int64_t)blockIdx.x * a.ecount : nullptr);
         return;
     }
     if (r >= M || j >= d_out) return;
-    float y = 0.f;
-    {
-        constexpr int PARTS = kBlock / TM;
-        const float* red = xin + TM * 4 + j * PARTS * TM + rloc;
-#pragma unroll
-        for (int p = 0; p < PARTS; ++p) y += red[p * TM];
-        y += net.params[net.b_off[nh] + j];
-    }
+    const float y = out_y<RT>(net, red, rloc, j);
     if (OUT_MODE == OUT_F32) {
         a.out[blockIdx.y][r * a.ld_out + a.out_col + j] = y;
     } else if (OUT_MODE == OUT_TARGET) {
@@ -569,50 +586,31 @@ NAV_DEV void mask_and_store(f32x16 (&acc)[RT][2], const uint16_t* mask, float* a
     }
 }
 
+// One network's row backward over the block's TM rows: dy rows in dys [TM][4] (LDS, ready), the
+// forward's ReLU bits in masks; leaves dz_0 in the LDS rows `act`. With es: the per-block edge
+// partials (every bias, dW0 from the input rows xin [TM][4], and dWo / dbo when h_top [M][hp] is
+// given); dz_L rows to dz for save_mask bits.
 template <int NT, int RT>
-__global__ __launch_bounds__(kBlock, 1) void k_mlp_bwd(BwdArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float smem[];
+NAV_DEV void bwd_net(const MlpDev& net, float* act, const float* dys, const float* xin,
+                     const uint16_t* masks, int64_t n_rt, float* es, const float* h_top,
+                     float* dz, uint32_t save_mask, int64_t row0, int64_t M, int64_t rt0) {
     constexpr int hp = NT * 32, SS = hp + 4, TM = RT * 32;
     const int tid = threadIdx.x, lane = tid & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
-    const int y = blockIdx.y;
-    const MlpDev& net = a.net[y];
-    const int64_t M = a.M;
-    const int64_t row0 = (int64_t)blockIdx.x * TM;
-    const int64_t rt0 = (int64_t)blockIdx.x * RT;
-    const int64_t n_rt = mask_rowtiles(M);
-    float* act = smem;
-    float* dys = smem + TM * SS;  // [TM][4] dy rows
-    float* xin = dys + TM * 4;    // [TM][4] forward input rows (dW0), inside the 2*kBlock scratch
     const int d_in = net.d_in, d_out = net.d_out, nh = net.n_hidden;
     const int64_t MH = M * hp;
     const WaveCols<NT> wc(wv);
     const size_t mstride = (size_t)n_rt * NT * 64;
-    float* es = a.eslab[y] ? a.eslab[y] + (int64_t)blockIdx.x * a.ecount : nullptr;
-
-    if (tid < TM) {
-        const int64_t r = row0 + tid;
-        float x[2] = {0.f, 0.f};
-        float xi[4] = {0.f, 0.f, 0.f, 0.f};
-        if (r < M) {
-            for (int j = 0; j < d_out; ++j) x[j] = a.dy[y][r * a.ld_dy + j];
-            if (es)
-                for (int k = 0; k < d_in; ++k) xi[k] = a.in[r * a.ld_in + a.in_col + k];
-        }
-        *reinterpret_cast<float4*>(dys + tid * 4) = make_float4(x[0], x[1], 0.f, 0.f);
-        *reinterpret_cast<float4*>(xin + tid * 4) = make_float4(xi[0], xi[1], xi[2], xi[3]);
-    }
-    __syncthreads();
     if (es) {
         // output layer (robot.py:361 / 392 backward): dWo = dy^T h_top, dbo = sum dy, when the
         // forward did not produce them (it does for the critic's TD loss)
-        if (a.h_top[y]) {
+        if (h_top) {
             const int n = tid;
             if (n < hp) {
                 float s0 = 0.f, s1 = 0.f;
                 const int rows = (int)(M - row0 < TM ? M - row0 : TM);
 #pragma unroll 4
                 for (int rr = 0; rr < rows; ++rr) {
-                    const float h = a.h_top[y][(row0 + rr) * hp + n];
+                    const float h = h_top[(row0 + rr) * hp + n];
                     s0 = fmaf(dys[rr * 4], h, s0);
                     s1 = fmaf(dys[rr * 4 + 1], h, s1);
                 }
@@ -631,7 +629,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_bwd(BwdArgs a) {
     // top hidden layer: dz = (dy . Wo) * relu'(.), in the C layout
     {
         const float* Wo = net.params + net.w_off[nh];
-        const uint16_t* mk = a.masks[y] + (size_t)(nh - 1) * mstride;
+        const uint16_t* mk = masks + (size_t)(nh - 1) * mstride;
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             if (!(j == 0 ? wc.has0 : wc.has1)) continue;
@@ -666,7 +664,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_bwd(BwdArgs a) {
             edge_col_sums<TM>(act, SS, hp, es + e_b(net, L));
             if (L == 0) edge_w0<TM>(act, SS, hp, xin, d_in, es + net.w_off[0]);
         }
-        if ((a.save_mask >> L) & 1u) copy_rows<NT, RT>(act, SS, a.dz[y] + (int64_t)L * MH, row0, M);
+        if ((save_mask >> L) & 1u) copy_rows<NT, RT>(act, SS, dz + (int64_t)L * MH, row0, M);
     };
     finish_layer(nh - 1);
 
@@ -676,23 +674,263 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_bwd(BwdArgs a) {
         gemm_cols<NT, RT>(act, SS,
                           net.packed + (int64_t)(L - 1) * 2 * hp * hp + (int64_t)hp * hp, acc);
         __syncthreads();
-        mask_and_store<NT, RT>(acc, a.masks[y] + (size_t)(L - 1) * mstride, act, SS, rt0);
+        mask_and_store<NT, RT>(acc, masks + (size_t)(L - 1) * mstride, act, SS, rt0);
         __syncthreads();
         finish_layer(L - 1);
     }
 
-    // dx = dz_0 . W0 : thread = (row, input pair)
+}
+
+// dL/dx[row][jj] = dz_0[row] . W0[:, jj] from the LDS rows (after bwd_net)
+template <int NT>
+NAV_DEV float dx_unit(const MlpDev& net, const float* act, int rloc, int jj) {
+    constexpr int hp = NT * 32, SS = hp + 4;
+    const float* W0 = net.params + net.w_off[0];
+    const float* zr = act + rloc * SS;
+    float acc = 0.f;
+    for (int c = 0; c < hp; ++c) acc = fmaf(zr[c], W0[c * net.d_in + jj], acc);
+    return acc;
+}
+
+template <int NT, int RT>
+__global__ __launch_bounds__(kBlock, 1) void k_mlp_bwd(BwdArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    constexpr int hp = NT * 32, SS = hp + 4, TM = RT * 32;
+    const int tid = threadIdx.x;
+    const int y = blockIdx.y;
+    const MlpDev& net = a.net[y];
+    const int64_t M = a.M;
+    const int64_t row0 = (int64_t)blockIdx.x * TM;
+    const int64_t rt0 = (int64_t)blockIdx.x * RT;
+    const int64_t n_rt = mask_rowtiles(M);
+    float* act = smem;
+    float* dys = smem + TM * SS;  // [TM][4] dy rows
+    float* xin = dys + TM * 4;    // [TM][4] forward input rows (dW0), inside the 2*kBlock scratch
+    const int d_in = net.d_in, d_out = net.d_out;
+    static_assert(hp <= kBlock, "one thread per hidden column");
+    float* es = a.eslab[y] ? a.eslab[y] + (int64_t)blockIdx.x * a.ecount : nullptr;
+
+    if (tid < TM) {
+        const int64_t r = row0 + tid;
+        float x[2] = {0.f, 0.f};
+        float xi[4] = {0.f, 0.f, 0.f, 0.f};
+        if (r < M) {
+            for (int j = 0; j < d_out; ++j) x[j] = a.dy[y][r * a.ld_dy + j];
+            if (es)
+                for (int k = 0; k < d_in; ++k) xi[k] = a.in[r * a.ld_in + a.in_col + k];
+        }
+        *reinterpret_cast<float4*>(dys + tid * 4) = make_float4(x[0], x[1], 0.f, 0.f);
+        *reinterpret_cast<float4*>(xin + tid * 4) = make_float4(xi[0], xi[1], xi[2], xi[3]);
+    }
+    __syncthreads();
+    bwd_net<NT, RT>(net, act, dys, xin, a.masks[y], n_rt, es, a.h_top[y], a.dz[y], a.save_mask,
+                    row0, M, rt0);
+
+    // dx = dz_0 . W0 : thread = (row, input)
     if (a.dx[y]) {
-        const float* W0 = net.params + net.w_off[0];
         const int rloc = tid % TM;
         const int64_t r = row0 + rloc;
-        const float* zr = act + rloc * SS;
         for (int jj = tid / TM; jj < d_in; jj += kBlock / TM) {
-            float acc = 0.f;
-            for (int c = 0; c < hp; ++c) acc = fmaf(zr[c], W0[c * d_in + jj], acc);
-            if (r < M) a.dx[y][r * d_in + jj] = acc;
+            const float v = dx_unit<NT>(net, act, rloc, jj);
+            if (r < M) a.dx[y][r * d_in + jj] = v;
         }
     }
+}
+
+// ---------------- fused TD3 row programs ----------------
+// Everything in train_critic / train_actor that is local to a batch row runs as one launch per
+// row block, the rows staying in LDS between the network passes (the launches that remain are
+// the cross-row reductions: weight gradients and their reduce + Adam).
+
+// ReplayBuffer.sample (robot.py:98-115) of row b: injected index or Philox with replacement
+NAV_DEV void sample_row(const float* rows, int64_t size, const int64_t* idx, uint32_t s0,
+                        uint32_t s1, uint32_t ctr, int64_t b, float4& lo, float4& hi) {
+    int64_t k;
+    if (idx) {
+        k = idx[b];
+    } else {
+        const uint4 w = philox((uint32_t)b, 0u, NAV_TAG_SAMPLE, ctr, s0, s1);
+        k = (int64_t)(((uint64_t)w.x * (uint64_t)size) >> 32);
+    }
+    const float4* src = reinterpret_cast<const float4*>(rows) + 2 * k;
+    lo = src[0];
+    hi = src[1];
+}
+
+struct CriticRowsArgs {
+    MlpDev actor_t, critic_t[2], critic[2];
+    int64_t B;
+    const float* rows;
+    int64_t rsize;
+    const int64_t* idx;
+    uint32_t seed_lo, seed_hi, sample_ctr, noise_ctr;
+    const float* eps;
+    float policy_noise, noise_clip, max_action, gamma, norm;
+    float* batch;
+    float* dq[2];
+    float* loss_part[2];
+    float* eslab[2];
+    int64_t ecount;
+    float* acts[2];
+    uint32_t save_mask;
+    uint16_t* masks[2];
+};
+
+// train_critic (robot.py:329-353) for one block of TM batch rows: sample, target policy
+// smoothing through the target actor, twin target critics, TD target, then the twin online
+// critics with mse_loss's gradient, the loss and the output layers' gradient partials.
+template <int NT, int RT>
+__global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    constexpr int hp = NT * 32, SS = hp + 4, TM = RT * 32;
+    const int tid = threadIdx.x;
+    const int64_t B = a.B, row0 = (int64_t)blockIdx.x * TM, rt0 = (int64_t)blockIdx.x * RT;
+    const int64_t n_rt = mask_rowtiles(B);
+    float* act = smem;
+    float* xin = act + TM * SS;    // [TM][4] network input rows
+    float* red = xin + TM * 4;     // [2][PARTS][TM] output partial sums
+    float* brow = red + 2 * kBlock;  // [TM][8] the sampled replay rows
+    float* qv = brow + TM * 8;     // [TM] q1'
+    if (tid < TM) {
+        const int64_t b = row0 + tid;
+        float4 lo = make_float4(0.f, 0.f, 0.f, 0.f), hi = lo;
+        if (b < B) {
+            sample_row(a.rows, a.rsize, a.idx, a.seed_lo, a.seed_hi, a.sample_ctr, b, lo, hi);
+            float4* dst = reinterpret_cast<float4*>(a.batch) + 2 * b;
+            dst[0] = lo;
+            dst[1] = hi;
+        }
+        *reinterpret_cast<float4*>(brow + tid * 8) = lo;
+        *reinterpret_cast<float4*>(brow + tid * 8 + 4) = hi;
+        *reinterpret_cast<float4*>(xin + tid * 4) = make_float4(hi.y, hi.z, 0.f, 0.f);  // s'
+    }
+    __syncthreads();
+    // target actor; a' = clamp(pi'(s') + clamp(policy_noise * eps, +-noise_clip), +-max_action)
+    fwd_net<NT, RT>(a.actor_t, act, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0);
+    if (tid < 2 * TM) {
+        const int rloc = tid % TM, j = tid / TM;
+        const int64_t r = row0 + rloc;
+        float v = 0.f;
+        if (r < B) {
+            const float y = out_y<RT>(a.actor_t, red, rloc, j);
+            float e;
+            if (a.eps) {
+                e = a.eps[r * 2 + j];
+            } else {
+                const double2 z = gauss_pair(philox((uint32_t)r, 0u, NAV_TAG_TNOISE, a.noise_ctr,
+                                                    a.seed_lo, a.seed_hi));
+                e = (float)(j == 0 ? z.x : z.y);
+            }
+            float nz = e * a.policy_noise;
+            nz = fminf(fmaxf(nz, -a.noise_clip), a.noise_clip);
+            v = y + nz;
+            v = fminf(fmaxf(v, -a.max_action), a.max_action);
+        }
+        xin[rloc * 4 + 2 + j] = v;
+    }
+    __syncthreads();
+    // twin target critics on (s', a'), then y = r + gamma * min(q1', q2') * (1 - done), kept in
+    // the row's thread
+    fwd_net<NT, RT>(a.critic_t[0], act, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0);
+    if (tid < TM) qv[tid] = out_y<RT>(a.critic_t[0], red, tid, 0);
+    fwd_net<NT, RT>(a.critic_t[1], act, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0);
+    float yt = 0.f;
+    if (tid < TM) {
+        const float q2 = out_y<RT>(a.critic_t[1], red, tid, 0);
+        const float rw = brow[tid * 8 + 4], dn = brow[tid * 8 + 7];
+        yt = rw + (a.gamma * fminf(qv[tid], q2)) * (1.0f - dn);
+        *reinterpret_cast<float4*>(xin + tid * 4) = *reinterpret_cast<const float4*>(brow + tid * 8);
+    }
+    __syncthreads();
+    // online critics on (s, a)
+#pragma unroll 1
+    for (int q = 0; q < 2; ++q) {
+        fwd_net<NT, RT>(a.critic[q], act, xin, red, a.masks[q], n_rt, a.acts[q], a.save_mask, row0,
+                        B, rt0);
+        loss_epilogue<NT, RT>(a.critic[q], act, red, row0, B, yt, a.norm, a.dq[q],
+                              a.loss_part[q] + blockIdx.x,
+                              a.eslab[q] ? a.eslab[q] + (int64_t)blockIdx.x * a.ecount : nullptr);
+        __syncthreads();
+    }
+}
+
+struct ActorRowsArgs {
+    MlpDev actor, critic;
+    int64_t B;
+    const float* rows;
+    int64_t rsize;
+    const int64_t* idx;
+    uint32_t seed_lo, seed_hi, sample_ctr;
+    float dq;            // d(-mean Q)/dQ = -1/B
+    float* batch;        // [B][8] sampled rows
+    float* q;            // [B] Q1(s, pi(s)), nullable
+    float* da;           // [B][2] dL/da
+    float* acts;         // actor [nh][B][hp], save_mask layers (the top one feeds dWo)
+    uint32_t save_mask;
+    float* dz;           // actor [nh][B][hp], dz_save_mask layers
+    uint32_t dz_save_mask;
+    uint16_t* masks_a;
+    uint16_t* masks_c;
+    float* eslab;        // actor edge partials
+    int64_t ecount;
+};
+
+// train_actor (robot.py:382-390) for one block of TM batch rows: sample, actor forward,
+// critic-1 forward on (s, pi(s)), backward of -mean(Q) through critic 1 to its action input
+// (critic grads discarded, as zero_grad does), and the actor's row backward with its edge
+// partials.
+template <int NT, int RT>
+__global__ __launch_bounds__(kBlock, 1) void k_td3_actor_rows(ActorRowsArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    constexpr int hp = NT * 32, SS = hp + 4, TM = RT * 32;
+    const int tid = threadIdx.x;
+    const int64_t B = a.B, row0 = (int64_t)blockIdx.x * TM, rt0 = (int64_t)blockIdx.x * RT;
+    const int64_t n_rt = mask_rowtiles(B);
+    float* act = smem;
+    float* xin = act + TM * SS;      // [TM][4] (s, pi(s))
+    float* red = xin + TM * 4;       // [2][PARTS][TM]
+    float* dys = red + 2 * kBlock;   // [TM][4] critic dy
+    float* dys2 = dys + TM * 4;      // [TM][4] actor dy = dL/da
+    if (tid < TM) {
+        const int64_t b = row0 + tid;
+        float4 lo = make_float4(0.f, 0.f, 0.f, 0.f), hi = lo;
+        if (b < B) {
+            sample_row(a.rows, a.rsize, a.idx, a.seed_lo, a.seed_hi, a.sample_ctr, b, lo, hi);
+            float4* dst = reinterpret_cast<float4*>(a.batch) + 2 * b;
+            dst[0] = lo;
+            dst[1] = hi;
+        }
+        *reinterpret_cast<float4*>(xin + tid * 4) = make_float4(lo.x, lo.y, 0.f, 0.f);  // s
+        *reinterpret_cast<float4*>(dys + tid * 4) =
+            make_float4(b < B ? a.dq : 0.f, 0.f, 0.f, 0.f);
+    }
+    __syncthreads();
+    fwd_net<NT, RT>(a.actor, act, xin, red, a.masks_a, n_rt, a.acts, a.save_mask, row0, B, rt0);
+    if (tid < 2 * TM) {
+        const int rloc = tid % TM, j = tid / TM;
+        xin[rloc * 4 + 2 + j] = row0 + rloc < B ? out_y<RT>(a.actor, red, rloc, j) : 0.f;
+    }
+    __syncthreads();
+    fwd_net<NT, RT>(a.critic, act, xin, red, a.masks_c, n_rt, nullptr, 0u, row0, B, rt0);
+    if (tid < TM && a.q && row0 + tid < B) a.q[row0 + tid] = out_y<RT>(a.critic, red, tid, 0);
+    bwd_net<NT, RT>(a.critic, act, dys, xin, a.masks_c, n_rt, nullptr, nullptr, nullptr, 0u, row0,
+                    B, rt0);
+    if (tid < 2 * TM) {
+        const int rloc = tid % TM, j = tid / TM;
+        const int64_t r = row0 + rloc;
+        const float v = r < B ? dx_unit<NT>(a.critic, act, rloc, 2 + j) : 0.f;
+        dys2[rloc * 4 + j] = v;
+        if (r < B) a.da[r * 2 + j] = v;
+    }
+    if (tid < TM) {
+        dys2[tid * 4 + 2] = 0.f;
+        dys2[tid * 4 + 3] = 0.f;
+    }
+    __syncthreads();
+    bwd_net<NT, RT>(a.actor, act, dys2, xin, a.masks_a, n_rt,
+                    a.eslab + (int64_t)blockIdx.x * a.ecount,
+                    a.acts + (int64_t)(a.actor.n_hidden - 1) * B * hp, a.dz, a.dz_save_mask, row0, B,
+                    rt0);
 }
 
 // ---------------- hidden x hidden weight gradients (split-M partial slabs) ----------------
@@ -1295,6 +1533,46 @@ int launch_bwd(const BwdArgs& a, int n_nets, hipStream_t st) {
     return 0;
 }
 
+
+template <int NT, int RT>
+void launch_critic_rows_k(const CriticRowsArgs& a, hipStream_t st) {
+    constexpr int TM = RT * 32;
+    const size_t lds = ((size_t)TM * (NT * 32 + 4) + TM * 4 + 2 * kBlock + TM * 8 + TM) * 4;
+    auto k = k_td3_critic_rows<NT, RT>;
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    hipLaunchKernelGGL(k, dim3((unsigned)((a.B + TM - 1) / TM)), dim3(kBlock), lds, st, a);
+}
+
+template <int NT, int RT>
+void launch_actor_rows_k(const ActorRowsArgs& a, hipStream_t st) {
+    constexpr int TM = RT * 32;
+    const size_t lds = ((size_t)TM * (NT * 32 + 4) + TM * 4 + 2 * kBlock + TM * 8) * 4;
+    auto k = k_td3_actor_rows<NT, RT>;
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    hipLaunchKernelGGL(k, dim3((unsigned)((a.B + TM - 1) / TM)), dim3(kBlock), lds, st, a);
+}
+
+template <typename Args, void (*L2)(const Args&, hipStream_t), void (*L4)(const Args&, hipStream_t)>
+void pick_rt(const Args& a, hipStream_t st) {
+    if (row_tiles() == 4) L4(a, st);
+    else L2(a, st);
+}
+
+#define NAV_ROWS_SWITCH(HP, FN, ARGS, ST)                                                   \
+    switch ((HP) / 32) {                                                                    \
+        case 1: pick_rt<decltype(ARGS), FN<1, 2>, FN<1, 4>>(ARGS, ST); break;               \
+        case 2: pick_rt<decltype(ARGS), FN<2, 2>, FN<2, 4>>(ARGS, ST); break;               \
+        case 3: pick_rt<decltype(ARGS), FN<3, 2>, FN<3, 4>>(ARGS, ST); break;               \
+        case 4: pick_rt<decltype(ARGS), FN<4, 2>, FN<4, 4>>(ARGS, ST); break;               \
+        case 5: pick_rt<decltype(ARGS), FN<5, 2>, FN<5, 4>>(ARGS, ST); break;               \
+        case 6: pick_rt<decltype(ARGS), FN<6, 2>, FN<6, 4>>(ARGS, ST); break;               \
+        case 7: pick_rt<decltype(ARGS), FN<7, 2>, FN<7, 4>>(ARGS, ST); break;               \
+        case 8: pick_rt<decltype(ARGS), FN<8, 2>, FN<8, 4>>(ARGS, ST); break;               \
+        default: return NAV_EINVAL;                                                         \
+    }
+
 }  // namespace
 
 extern "C" {
@@ -1441,6 +1719,96 @@ int nav_td3_critic_forward(const nav_mlp* nets, int64_t B, const float* in, int3
     a.norm = (float)(2.0 / (double)B);
     a.ecount = edge_count(a.net[0]);
     return launch_fwd<IN_F32, OUT_LOSS>(a, 2, S(stream));
+}
+
+int nav_td3_critic_rows(const nav_mlp* target_actor, const nav_mlp* target_critics,
+                        const nav_mlp* critics, const nav_replay* replay, int64_t size,
+                        int64_t B, const int64_t* idx, uint32_t seed_lo, uint32_t seed_hi,
+                        uint32_t counter, const float* eps, float policy_noise,
+                        float noise_clip, float max_action, float gamma, float* batch,
+                        float* const* dq, float* const* loss_part, float* const* edge_slabs,
+                        float* const* acts, uint32_t save_mask, uint16_t* const* masks,
+                        void* stream) {
+    CriticRowsArgs a{};
+    if (!target_actor || !target_critics || !critics || !replay || !replay->rows || B < 1 ||
+        size < 1 || size > replay->capacity || size > ((int64_t)1 << 32) || !batch || !dq ||
+        !loss_part || !masks || !make_dev(target_actor, &a.actor_t) || target_actor->d_in != 2 ||
+        target_actor->d_out != 2)
+        return NAV_EINVAL;
+    for (int i = 0; i < 2; ++i) {
+        if (!make_dev(&target_critics[i], &a.critic_t[i]) || !make_dev(&critics[i], &a.critic[i]) ||
+            critics[i].d_in != 4 || critics[i].d_out != 1 || target_critics[i].d_in != 4 ||
+            target_critics[i].d_out != 1 || !dq[i] || !loss_part[i] || !masks[i])
+            return NAV_EINVAL;
+        if (a.critic_t[i].hp != a.actor_t.hp || a.critic[i].hp != a.actor_t.hp ||
+            a.critic[i].n_hidden != a.critic[0].n_hidden)
+            return NAV_EINVAL;
+        a.dq[i] = dq[i];
+        a.loss_part[i] = loss_part[i];
+        a.eslab[i] = edge_slabs ? edge_slabs[i] : nullptr;
+        a.acts[i] = acts ? acts[i] : nullptr;
+        if (save_mask && !a.acts[i]) return NAV_EINVAL;
+        a.masks[i] = masks[i];
+    }
+    a.B = B;
+    a.rows = replay->rows;
+    a.rsize = size;
+    a.idx = idx;
+    a.seed_lo = seed_lo;
+    a.seed_hi = seed_hi;
+    a.sample_ctr = 2u * counter;  // the actor's batch of the same epoch uses 2*counter + 1
+    a.noise_ctr = counter;
+    a.eps = eps;
+    a.policy_noise = policy_noise;
+    a.noise_clip = noise_clip;
+    a.max_action = max_action;
+    a.gamma = gamma;
+    a.norm = (float)(2.0 / (double)B);
+    a.batch = batch;
+    a.ecount = edge_count(a.critic[0]);
+    a.save_mask = save_mask;
+    NAV_ROWS_SWITCH(a.actor_t.hp, launch_critic_rows_k, a, S(stream))
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_td3_actor_rows(const nav_mlp* actor, const nav_mlp* critic, const nav_replay* replay,
+                       int64_t size, int64_t B, const int64_t* idx, uint32_t seed_lo,
+                       uint32_t seed_hi, uint32_t counter, float* batch, float* q, float* da,
+                       float* acts, uint32_t save_mask, float* dz, uint32_t dz_save_mask,
+                       uint16_t* masks_actor, uint16_t* masks_critic, float* edge_slabs,
+                       void* stream) {
+    ActorRowsArgs a{};
+    if (!actor || !critic || !replay || !replay->rows || B < 1 || size < 1 ||
+        size > replay->capacity || size > ((int64_t)1 << 32) || !batch || !da || !acts ||
+        !masks_actor || !masks_critic || !edge_slabs || !make_dev(actor, &a.actor) ||
+        !make_dev(critic, &a.critic) || actor->d_in != 2 || actor->d_out != 2 ||
+        critic->d_in != 4 || critic->d_out != 1 || a.actor.hp != a.critic.hp ||
+        !((save_mask >> (actor->n_hidden - 1)) & 1u) || (save_mask >> actor->n_hidden) ||
+        (dz_save_mask && !dz) || (dz_save_mask >> actor->n_hidden))
+        return NAV_EINVAL;
+    a.B = B;
+    a.rows = replay->rows;
+    a.rsize = size;
+    a.idx = idx;
+    a.seed_lo = seed_lo;
+    a.seed_hi = seed_hi;
+    a.sample_ctr = 2u * counter + 1u;
+    a.dq = (float)(-1.0 / (double)B);
+    a.batch = batch;
+    a.q = q;
+    a.da = da;
+    a.acts = acts;
+    a.save_mask = save_mask;
+    a.dz = dz;
+    a.dz_save_mask = dz_save_mask;
+    a.masks_a = masks_actor;
+    a.masks_c = masks_critic;
+    a.eslab = edge_slabs;
+    a.ecount = edge_count(a.actor);
+    NAV_ROWS_SWITCH(a.actor.hp, launch_actor_rows_k, a, S(stream))
+    NAV_CHECK_LAUNCH();
+    return 0;
 }
 
 int64_t nav_mlp_mask_count(int32_t hidden_pad, int32_t n_hidden, int64_t M) {

@@ -89,6 +89,15 @@ SIGNATURES = [
                                   _P(_vp), C.c_int32, C.c_int32, C.c_int32, _vp, C.c_float,
                                   C.c_float, C.c_float, C.c_uint32, C.c_uint32, C.c_uint32,
                                   _P(_vp), C.c_uint32, _P(_vp), _vp]),
+    ("nav_td3_critic_rows", C.c_int, [_P(NavMlp), _P(NavMlp), _P(NavMlp), _P(NavReplay),
+                                      C.c_int64, C.c_int64, _vp, C.c_uint32, C.c_uint32,
+                                      C.c_uint32, _vp, C.c_float, C.c_float, C.c_float, C.c_float,
+                                      _vp, _P(_vp), _P(_vp), _P(_vp), _P(_vp), C.c_uint32,
+                                      _P(_vp), _vp]),
+    ("nav_td3_actor_rows", C.c_int, [_P(NavMlp), _P(NavMlp), _P(NavReplay), C.c_int64,
+                                     C.c_int64, _vp, C.c_uint32, C.c_uint32, C.c_uint32, _vp,
+                                     _vp, _vp, _vp, C.c_uint32, _vp, C.c_uint32, _vp, _vp, _vp,
+                                     _vp]),
     ("nav_mlp_mask_count", C.c_int64, [C.c_int32, C.c_int32, C.c_int64]),
     ("nav_mlp_row_blocks", C.c_int64, [C.c_int64]),
     ("nav_mlp_edge_count", C.c_int64, [C.c_int32] * 4),

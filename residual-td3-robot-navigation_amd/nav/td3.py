@@ -14,7 +14,7 @@ import torch
 from . import config as K
 from . import prof
 from ._lib import descs, lib, parr, ptr, stream_handle
-from .mlp import DeviceMLP, forward
+from .mlp import DeviceMLP
 
 
 class _Adam:
@@ -80,11 +80,8 @@ class TD3:
         L = lib()
         self.batch = f(B, 8)
         self.batch2 = f(B, 8)
-        self.tgt_in = f(B, 4)
-        self.q1t, self.q2t, self.q1 = f(B), f(B), f(B)
+        self.q1 = f(B)
         self.dq1, self.dq2 = f(B), f(B)
-        # train_actor: d(-mean Q)/dQ = -1/B for every row, one broadcast row (ld_dy = 0)
-        self.dq_actor = torch.full((1,), -1.0 / B, dtype=torch.float32, device=d)
         # saved rows: only hidden layers 1 .. nh-2 (+ the actor's top layer for dWo); h_0 and the
         # top dz are recomputed by the weight-gradient kernel
         self.acts1, self.acts2, self.acts_a = f(nh, B, hp), f(nh, B, hp), f(nh, B, hp)
@@ -92,7 +89,7 @@ class TD3:
         self.mask1 = self.critic_network_1.mask_buffer(B)
         self.mask2 = self.critic_network_1.mask_buffer(B)
         self.mask_a = self.actor_network.mask_buffer(B)
-        self.dx = f(B, 4)
+        self.da = f(B, 2)
         self.nblk = L.nav_mlp_row_blocks(B)
         self.loss_part = f(2, self.nblk)
         ec = L.nav_mlp_edge_count(4, 1, hp, nh)
@@ -151,41 +148,30 @@ class TD3:
                                    ld_in, in_col, parr(*(h_top or nil)), parr(*(dz or nil)),
                                    save_mask, parr(*(dx or nil)), parr(*(eslab or nil)), s)
 
-    def _sample(self, replay, B, out, idx=None, stream=None):
-        """ReplayBuffer.sample (robot.py:98-115) into a [B][8] batch."""
-        rd = replay.desc()
-        ctr = self.update_counter * 2 + (0 if out is self.batch else 1)
-        lib().nav_replay_sample(C.byref(rd), len(replay), B, ptr(idx),
-                                self.seed & 0xFFFFFFFF, (self.seed >> 32) & 0xFFFFFFFF, ctr,
-                                ptr(out), stream_handle(stream))
-
     # robot.py:312-366
     def train_critic(self, replay, idx=None, eps=None, stream=None):
         c = self.cfg
         B = c.batch_size
         self._workspace(B)
         s = stream_handle(stream)
-        self._sample(replay, B, self.batch, idx, stream)
-        bt = self.batch
-        # target action with smoothing noise: tgt_in = (s', clamp(pi'(s') + clip(eps*.2), +-5))
-        lib().nav_strided_copy(ptr(bt), 8, 5, ptr(self.tgt_in), 4, 0, B, 2, s)
-        forward([self.target_actor], bt, 8, 5, [self.tgt_in], 4, 2, B, out_mode=1, eps=eps,
-                policy_noise=c.policy_noise, noise_clip=c.noise_clip, max_action=c.max_action,
-                seed=(self.seed & 0xFFFFFFFF, (self.seed >> 32) & 0xFFFFFFFF),
-                counter=self.update_counter, stream=stream)
-        forward([self.target_critic_network_1, self.target_critic_network_2], self.tgt_in, 4, 0,
-                [self.q1t, self.q2t], 1, 0, B, stream=stream)
-        # online twin forward on (s, a) = batch columns 0..3, fused with the TD target, the MSE
-        # gradient and the output layer's gradient partials
         c1, c2 = self.critic_network_1, self.critic_network_2
         mid = c1.middle_layers()
-        with prof.region("mlp_fwd", 2 * prof.mlp_fwd_flops(4, 1, c1.hidden, c1.n_hidden, B)):
-            lib().nav_td3_critic_forward(descs(c1, c2), B, ptr(bt), 8, 0, ptr(bt), ptr(self.q1t),
-                                         ptr(self.q2t), c.gamma, parr(self.dq1, self.dq2),
-                                         parr(self.loss_part[0], self.loss_part[1]),
-                                         parr(self.eslab1, self.eslab2),
-                                         parr(self.acts1, self.acts2), mid,
-                                         parr(self.mask1, self.mask2), s)
+        rd = replay.desc()
+        # sample + target actor with smoothing noise + twin target critics + TD target + online
+        # twin forward with the MSE gradient: one launch, rows in LDS throughout
+        h, nh = c1.hidden, c1.n_hidden
+        work = (prof.mlp_fwd_flops(2, 2, h, nh, B) + 4 * prof.mlp_fwd_flops(4, 1, h, nh, B))
+        with prof.region("critic_rows", work):
+            lib().nav_td3_critic_rows(
+                C.byref(self.target_actor.desc()),
+                descs(self.target_critic_network_1, self.target_critic_network_2),
+                descs(c1, c2), C.byref(rd), len(replay), B, ptr(idx),
+                self.seed & 0xFFFFFFFF, (self.seed >> 32) & 0xFFFFFFFF, self.update_counter,
+                ptr(eps), c.policy_noise, c.noise_clip, c.max_action, c.gamma, ptr(self.batch),
+                parr(self.dq1, self.dq2), parr(self.loss_part[0], self.loss_part[1]),
+                parr(self.eslab1, self.eslab2), parr(self.acts1, self.acts2), mid,
+                parr(self.mask1, self.mask2), s)
+        bt = self.batch
         # both critics' backward, weight gradients and reduce + Adam: one launch each
         crit, opts = [c1, c2], [self.critic_optimizer_1, self.critic_optimizer_2]
         self._bwd(crit, B, [self.dq1, self.dq2], 1, [self.mask1, self.mask2], s, inp=bt, ld_in=8,
@@ -207,25 +193,25 @@ class TD3:
         B = c.batch_size
         self._workspace(B)
         s = stream_handle(stream)
-        self._sample(replay, B, self.batch2, idx, stream)
-        bt = self.batch2
         net = self.actor_network
         c1 = self.critic_network_1
-        # actor(s) overwrites the stored action (columns 2..3): the critic then reads (s, pi(s))
-        # straight from the batch rows
-        forward([net], bt, 8, 0, [bt], 8, 2, B, acts=[self.acts_a],
-                save_mask=net.middle_layers() | net.top_layer(), masks=[self.mask_a],
-                stream=stream)
-        forward([c1], bt, 8, 0, [self.q1], 1, 0, B, masks=[self.mask1], stream=stream)
-        # backprop -mean(Q) through critic 1 to its action input (its own grads are discarded)
-        self._bwd([c1], B, [self.dq_actor], 0, [self.mask1], s, dx=[self.dx])
-        da = self.dx.view(-1)[2:]  # dL/da = columns 2..3 of dL/dx, row stride 4
-        self._bwd([net], B, [da], 4, [self.mask_a], s, inp=bt, ld_in=8, in_col=0,
-                  h_top=[self.acts_a[net.n_hidden - 1]], dz=[self.dz_a],
-                  save_mask=net.middle_layers(), eslab=[self.eslab_a])
-        self._grads_and_step([net], [self.actor_optimizer], B, bt, 8, 0, [self.acts_a],
-                             [self.dz_a], [da], 4, [self.mask_a], [self.eslab_a], [self.grad_a],
-                             [self.hslab], s, stream)
+        rd = replay.desc()
+        h, nh = net.hidden, net.n_hidden
+        # sample + actor forward + critic-1 forward + backward of -mean(Q) to the action + the
+        # actor's row backward with its edge partials: one launch
+        work = (prof.mlp_fwd_flops(2, 2, h, nh, B) + prof.mlp_fwd_flops(4, 1, h, nh, B) +
+                prof.mlp_bwd_flops(4, 1, h, nh, B, True) +
+                prof.mlp_bwd_flops(2, 2, h, nh, B, False, True, True))
+        with prof.region("actor_rows", work):
+            lib().nav_td3_actor_rows(
+                C.byref(net.desc()), C.byref(c1.desc()), C.byref(rd), len(replay), B, ptr(idx),
+                self.seed & 0xFFFFFFFF, (self.seed >> 32) & 0xFFFFFFFF, self.update_counter,
+                ptr(self.batch2), ptr(self.q1), ptr(self.da), ptr(self.acts_a),
+                net.middle_layers() | net.top_layer(), ptr(self.dz_a), net.middle_layers(),
+                ptr(self.mask_a), ptr(self.mask1), ptr(self.eslab_a), s)
+        self._grads_and_step([net], [self.actor_optimizer], B, self.batch2, 8, 0, [self.acts_a],
+                             [self.dz_a], [self.da], 2, [self.mask_a], [self.eslab_a],
+                             [self.grad_a], [self.hslab], s, stream)
 
     def actor_loss_value(self):
         return -(self.q1.sum() / self._B).item()

@@ -376,3 +376,93 @@ def test_td3_update_vs_oracle_and_reference(nav):
         for k, (_, _, ix, v) in enumerate(dig):
             assert (ix == g[name + "_idx"][k]).all()
             np.testing.assert_allclose(v, g[name + "_val"][k], rtol=0, atol=3e-7)
+
+
+@pytest.mark.parametrize("hidden,nh,B", [(200, 3, 333), (256, 2, 2048)])
+def test_fused_row_kernels_match_unfused(nav, hidden, nh, B):
+    """nav_td3_critic_rows / nav_td3_actor_rows (one launch each) produce bit-identical batches,
+    targets, dq, losses, ReLU bits, dL/da and edge partials to the per-network kernels they
+    fuse (same device code, same order)."""
+    from nav._lib import NavReplay, descs, lib, parr, ptr, stream_handle
+    from nav.mlp import forward
+    L = lib()
+    s = stream_handle()
+    ta, _ = make_net(2, 2, hidden, nh, 61)
+    tc = [make_net(4, 1, hidden, nh, 62 + k)[0] for k in range(2)]
+    cr = [make_net(4, 1, hidden, nh, 64 + k)[0] for k in range(2)]
+    actor, _ = make_net(2, 2, hidden, nh, 66)
+    hp = ta.hp
+    cap = 5000
+    g = torch.Generator().manual_seed(9)
+    rows = torch.randn(cap, 8, generator=g) * 10
+    rows[:, 7] = (torch.rand(cap, generator=g) < 0.1).float()
+    rows = rows.to(DEV)
+    rd = NavReplay(rows.data_ptr(), cap)
+    seed, counter = 1707366464, 3
+    slo, shi = seed & 0xFFFFFFFF, seed >> 32
+    mid = cr[0].middle_layers()
+    nblk = L.nav_mlp_row_blocks(B)
+    f = lambda *sh: torch.zeros(*sh, device=DEV)  # noqa: E731
+    ec = L.nav_mlp_edge_count(4, 1, hp, nh)
+
+    def critic_bufs():
+        return dict(batch=f(B, 8), dq=[f(B), f(B)], lp=f(2, nblk), es=[f(nblk, ec), f(nblk, ec)],
+                    acts=[f(nh, B, hp), f(nh, B, hp)], masks=[cr[0].mask_buffer(B) for _ in range(2)])
+    u, v = critic_bufs(), critic_bufs()
+    # unfused: sample, target actor with smoothing, twin targets, online twin with the TD loss
+    L.nav_replay_sample(C.byref(rd), cap, B, None, slo, shi, 2 * counter, ptr(u["batch"]), s)
+    tgt_in, q1t, q2t = f(B, 4), f(B), f(B)
+    L.nav_strided_copy(ptr(u["batch"]), 8, 5, ptr(tgt_in), 4, 0, B, 2, s)
+    forward([ta], u["batch"], 8, 5, [tgt_in], 4, 2, B, out_mode=1, seed=(slo, shi),
+            counter=counter)
+    forward(tc, tgt_in, 4, 0, [q1t, q2t], 1, 0, B)
+    L.nav_td3_critic_forward(descs(*cr), B, ptr(u["batch"]), 8, 0, ptr(u["batch"]), ptr(q1t),
+                             ptr(q2t), 0.99, parr(*u["dq"]), parr(u["lp"][0], u["lp"][1]),
+                             parr(*u["es"]), parr(*u["acts"]), mid, parr(*u["masks"]), s)
+    L.nav_td3_critic_rows(C.byref(ta.desc()), descs(*tc), descs(*cr), C.byref(rd), cap, B, None,
+                          slo, shi, counter, None, 0.2, 0.5, 5.0, 0.99, ptr(v["batch"]),
+                          parr(*v["dq"]), parr(v["lp"][0], v["lp"][1]), parr(*v["es"]),
+                          parr(*v["acts"]), mid, parr(*v["masks"]), s)
+    torch.cuda.synchronize()
+    assert torch.equal(u["batch"], v["batch"])
+    assert torch.equal(u["lp"], v["lp"])
+    for k in range(2):
+        assert torch.equal(u["dq"][k], v["dq"][k])
+        assert torch.equal(u["es"][k], v["es"][k])
+        assert torch.equal(u["masks"][k], v["masks"][k])
+        if mid:
+            assert torch.equal(u["acts"][k], v["acts"][k])
+    # actor rows: sample, actor fwd, critic fwd, backward of -mean Q to the action, actor bwd
+    eca = L.nav_mlp_edge_count(2, 2, hp, nh)
+    save = actor.middle_layers() | actor.top_layer()
+
+    def actor_bufs():
+        return dict(batch=f(B, 8), q=f(B), da=f(B, 2), acts=f(nh, B, hp), dz=f(nh, B, hp),
+                    ma=actor.mask_buffer(B), mc=cr[0].mask_buffer(B), es=f(nblk, eca))
+    u, v = actor_bufs(), actor_bufs()
+    L.nav_replay_sample(C.byref(rd), cap, B, None, slo, shi, 2 * counter + 1, ptr(u["batch"]), s)
+    forward([actor], u["batch"], 8, 0, [u["batch"]], 8, 2, B, acts=[u["acts"]], save_mask=save,
+            masks=[u["ma"]])
+    forward([cr[0]], u["batch"], 8, 0, [u["q"]], 1, 0, B, masks=[u["mc"]])
+    dqc = torch.full((1,), -1.0 / B, device=DEV)
+    dx = f(B, 4)
+    L.nav_mlp_backward(descs(cr[0]), 1, B, parr(dqc), 0, parr(u["mc"]), None, 0, 0, None, None, 0,
+                       parr(dx), None, s)
+    da = dx.view(-1)[2:]
+    L.nav_mlp_backward(descs(actor), 1, B, parr(da), 4, parr(u["ma"]), ptr(u["batch"]), 8, 0,
+                       parr(u["acts"][nh - 1]), parr(u["dz"]), actor.middle_layers(), None,
+                       parr(u["es"]), s)
+    L.nav_td3_actor_rows(C.byref(actor.desc()), C.byref(cr[0].desc()), C.byref(rd), cap, B, None,
+                         slo, shi, counter, ptr(v["batch"]), ptr(v["q"]), ptr(v["da"]),
+                         ptr(v["acts"]), save, ptr(v["dz"]), actor.middle_layers(), ptr(v["ma"]),
+                         ptr(v["mc"]), ptr(v["es"]), s)
+    torch.cuda.synchronize()
+    assert torch.equal(u["batch"][:, :2], v["batch"][:, :2])
+    assert torch.equal(u["batch"][:, 4:], v["batch"][:, 4:])
+    assert torch.equal(u["q"], v["q"])
+    assert torch.equal(dx[:, 2:], v["da"])
+    assert torch.equal(u["ma"], v["ma"]) and torch.equal(u["mc"], v["mc"])
+    assert torch.equal(u["acts"], v["acts"])
+    assert torch.equal(u["es"], v["es"])
+    if actor.middle_layers():
+        assert torch.equal(u["dz"][1:nh - 1], v["dz"][1:nh - 1])
