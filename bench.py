@@ -31,6 +31,27 @@ import torch  # noqa: E402
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP32_MFMA_PEAK_TFS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
 FP64_VALU_PEAK_TFS = 78.6    # MI355X spec FP64 vector
+# HBM bytes per launch from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this same
+# command (tools/pmc_traffic.py, gfx950 correction applied); bench regions -> kernel names
+PMC_TRAFFIC = os.path.join(HERE, "profiles", "pmc_traffic.json")
+REGION_KERNEL = {"critic_rows": "k_td3_critic_rows", "actor_rows": "k_td3_actor_rows",
+                 "mlp_bwd": "k_mlp_bwd", "mlp_wgrad": "k_wgrad", "act": "k_mlp_fwd",
+                 "agent_step": "k_agent_step", "env_step": "k_env_step",
+                 "grad_reduce": "k_grad_reduce", "demo_reward": "k_demo_reward_idx"}
+
+
+def pmc_traffic(region):
+    """(bytes per launch, source) of the region's kernel from the committed PMC summary, else
+    (None, None)."""
+    try:
+        with open(PMC_TRAFFIC) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    k = t.get(REGION_KERNEL.get(region, ""))
+    if not k:
+        return None, None
+    return k["bytes_per_launch"], "profiles/pmc_traffic.json (%s)" % t["_meta"].get("command", "")
 
 
 def parse():
@@ -50,6 +71,11 @@ def parse():
     ap.add_argument("--no-sweep", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--breakdown", action="store_true", help="print the per-kernel table")
+    ap.add_argument("--presleep", type=int, default=0,
+                    help="diagnostic: a GPU sleep of this many cycles before the timed loop, so "
+                         "the host queues ahead (launch-gap check under rocprofv3)")
+    ap.add_argument("--no-timed-events", action="store_true",
+                    help="no HIP events inside the timed region (overhead check; no roofline)")
     ap.add_argument("--sweep-only", type=int, default=0,
                     help="only run the step-kernel sweep at this N (profiling helper)")
     return ap.parse_args()
@@ -160,10 +186,12 @@ def main():
     dominant = max(breakdown, key=lambda k: breakdown[k]["total_ms"])
 
     # ---- timed region
-    timer = prof.KernelTimer([dominant, "agent_step"])
+    timer = prof.KernelTimer([] if args.no_timed_events else [dominant, "agent_step"])
     barrier(ws)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    if args.presleep:
+        torch.cuda._sleep(args.presleep)
     with prof.timing(timer):
         for _ in range(args.steps):
             tr.step()
@@ -176,20 +204,26 @@ def main():
     env_steps = args.envs * args.steps * ws
     value = env_steps / dt
 
-    if rank == 0:
+    if rank == 0 and args.no_timed_events:
+        print(json.dumps({"value": value, "ms_per_step": 1e3 * dt / args.steps,
+                          "no_timed_events": True}), flush=True)
+    elif rank == 0:
         d = ksum[dominant]
+        traffic, traffic_src = pmc_traffic(dominant)
         is_bytes = dominant in ("agent_step", "env_step", "grad_reduce")
         ach = d["work_per_launch"] / (d["avg_us"] * 1e-6)
         if is_bytes:
             roof = {"bound": "hbm", "kernel": dominant, "achieved": round(ach / 1e9, 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(ach / 1e9 / HBM_PEAK_GBS, 4), "traffic": None}
+                    "frac": round(ach / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "traffic_source": traffic_src}
         else:
             tf = ach / 1e12
             peak = FP64_VALU_PEAK_TFS if dominant == "demo_reward" else FP32_MFMA_PEAK_TFS
             roof = {"bound": "valu" if dominant == "demo_reward" else "mfma",
                     "kernel": dominant, "achieved": round(tf, 2), "peak": peak,
-                    "unit": "TFLOP/s", "frac": round(tf / peak, 4), "traffic": None,
+                    "unit": "TFLOP/s", "frac": round(tf / peak, 4), "traffic": traffic,
+                    "traffic_source": traffic_src,
                     "flop_per_launch": d["work_per_launch"], "avg_us": round(d["avg_us"], 2),
                     "launches": d["launches"]}
         a = ksum.get("agent_step")
@@ -199,9 +233,10 @@ def main():
             step_k = {"kernel": "nav_agent_step", "n_envs": args.envs,
                       "avg_us": round(a["avg_us"], 2), "bytes_per_env": prof.AGENT_STEP_BYTES,
                       "GBps": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
-        sweep = None if args.no_sweep else step_kernel_sweep(
+        sweep = None if (args.no_sweep or ws > 1) else step_kernel_sweep(
             tr.field, [65536, 1 << 20, 1 << 22, 1 << 24])
-        cpu = None if args.no_cpu_baseline else cpu_baseline(args, tr)
+        # CPU baseline: rank 0 at N = 1 only (a reported baseline, not part of the scaling runs)
+        cpu = None if (args.no_cpu_baseline or ws > 1) else cpu_baseline(args, tr)
         line = {
             "metric": "env-steps/sec at 65 536 parallel envs (full residual-TD3 update)",
             "value": value, "unit": "env-steps/s", "n_gpus": ws, "steps": args.steps,

@@ -327,6 +327,16 @@ int nav_fill(float* x, int64_t n, float value, void* stream);
 int nav_strided_copy(const float* src, int32_t ld_src, int32_t col_src, float* dst, int32_t ld_dst,
                      int32_t col_dst, int64_t rows, int32_t cols, void* stream);
 
+/* ---- kernel timing (measurement only, not on the reference's interface) ----
+ * Timing events recorded with a device-scope release (hipEventReleaseToDevice): bracketing a
+ * launch costs no system-scope L2 writeback, so timing the bench's timed region does not stretch
+ * it (a default torch/HIP event costs ~6 us of GPU time per record on MI355X). */
+int nav_event_create(void** event);
+int nav_event_destroy(void* event);
+int nav_event_record(void* event, void* stream);
+/* waits for `end`, then *ms = end - start */
+int nav_event_elapsed_ms(void* start, void* end, float* ms);
+
 #ifdef __cplusplus
 }
 #endif

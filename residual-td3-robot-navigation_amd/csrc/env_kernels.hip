@@ -652,6 +652,34 @@ extern "C" {
 
 int nav_abi_version(void) { return NAV_ABI_VERSION; }
 
+int nav_event_create(void** event) {
+    if (!event) return NAV_EINVAL;
+    const hipError_t e = hipEventCreateWithFlags(reinterpret_cast<hipEvent_t*>(event),
+                                                 hipEventReleaseToDevice);
+    return e == hipSuccess ? 0 : -(int)e;
+}
+
+int nav_event_destroy(void* event) {
+    if (!event) return NAV_EINVAL;
+    const hipError_t e = hipEventDestroy(reinterpret_cast<hipEvent_t>(event));
+    return e == hipSuccess ? 0 : -(int)e;
+}
+
+int nav_event_record(void* event, void* stream) {
+    if (!event) return NAV_EINVAL;
+    const hipError_t e = hipEventRecord(reinterpret_cast<hipEvent_t>(event), S(stream));
+    return e == hipSuccess ? 0 : -(int)e;
+}
+
+int nav_event_elapsed_ms(void* start, void* end, float* ms) {
+    if (!start || !end || !ms) return NAV_EINVAL;
+    hipError_t e = hipEventSynchronize(reinterpret_cast<hipEvent_t>(end));
+    if (e == hipSuccess)
+        e = hipEventElapsedTime(ms, reinterpret_cast<hipEvent_t>(start),
+                                reinterpret_cast<hipEvent_t>(end));
+    return e == hipSuccess ? 0 : -(int)e;
+}
+
 void nav_default_params(nav_params* p) {
     if (!p) return;
     p->world_size = 100.0;

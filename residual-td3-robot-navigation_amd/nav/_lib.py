@@ -125,6 +125,10 @@ SIGNATURES = [
     ("nav_fill", C.c_int, [_vp, C.c_int64, C.c_float, _vp]),
     ("nav_strided_copy", C.c_int, [_vp, C.c_int32, C.c_int32, _vp, C.c_int32, C.c_int32,
                                    C.c_int64, C.c_int32, _vp]),
+    ("nav_event_create", C.c_int, [_P(_vp)]),
+    ("nav_event_destroy", C.c_int, [_vp]),
+    ("nav_event_record", C.c_int, [_vp, _vp]),
+    ("nav_event_elapsed_ms", C.c_int, [_vp, _vp, _P(C.c_float)]),
 ]
 
 # Entry points that return int64 counts (negative = error) rather than a status code.

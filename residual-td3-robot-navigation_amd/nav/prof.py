@@ -4,8 +4,11 @@ roofline figures use.
 `with timing(KernelTimer(...)):` activates a timer; every libnavenv launch site in nav/ wraps its
 launch in `region(name, work)`, which records a start/stop event pair on the current stream (the
 stream the kernel is launched on) when the timer tracks that name. Nothing is recorded otherwise.
+The events are libnavenv's device-scope-release HIP events (nav_event_*): a default HIP event
+record costs ~6 us of GPU time (system-scope L2 writeback), which would stretch the timed region.
 """
 import contextlib
+import ctypes as C
 from collections import defaultdict
 
 import torch
@@ -54,12 +57,41 @@ class KernelTimer:
         torch.cuda.synchronize()
         out = {}
         for name, lst in self.rec.items():
-            ms = [s.elapsed_time(e) for s, e, _ in lst]
+            ms = [s.elapsed_ms(e) for s, e, _ in lst]
             work = sum(w for _, _, w in lst)
             out[name] = {"launches": len(ms), "total_ms": sum(ms),
                          "avg_us": 1e3 * sum(ms) / len(ms), "work": work,
                          "work_per_launch": work / len(ms)}
         return out
+
+
+class _Event:
+    """A pooled nav_event (hipEventReleaseToDevice), returned to the pool when collected."""
+    _pool = []
+
+    def __init__(self):
+        from ._lib import lib
+        if _Event._pool:
+            self.h = _Event._pool.pop()
+        else:
+            h = C.c_void_p()
+            lib().nav_event_create(C.byref(h))
+            self.h = h
+
+    def record(self):
+        from ._lib import lib, stream_handle
+        lib().nav_event_record(self.h, stream_handle())
+
+    def elapsed_ms(self, end):
+        from ._lib import lib
+        ms = C.c_float()
+        lib().nav_event_elapsed_ms(self.h, end.h, C.byref(ms))
+        return ms.value
+
+    def __del__(self):
+        if getattr(self, "h", None) is not None:
+            _Event._pool.append(self.h)
+            self.h = None
 
 
 _active = None
@@ -81,8 +113,7 @@ def region(name, work=0.0):
     if t is None or not t.wants(name):
         yield
         return
-    s = torch.cuda.Event(enable_timing=True)
-    e = torch.cuda.Event(enable_timing=True)
+    s, e = _Event(), _Event()
     s.record()
     try:
         yield

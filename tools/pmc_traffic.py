@@ -1,0 +1,49 @@
+"""HBM traffic per launch from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) of the same
+bench command, corrected as MI355X_MICROARCH.md §HBM prescribes: on gfx950 FETCH_SIZE tallies
+exactly half the bytes of a wide (16 B/lane) coalesced read, so it is doubled; WRITE_SIZE is exact
+for 16-B-per-lane stores. Both counters are in KB.
+
+python tools/pmc_traffic.py FETCH.csv WRITE.csv OUT.json [command description]
+
+OUT.json: {kernel short name: {"launches", "fetch_kb_raw", "write_kb", "bytes_per_launch"}} plus a
+"_meta" entry. bench.py reads it to fill roofline.traffic for the dominant kernel.
+"""
+import csv
+import json
+import sys
+from collections import defaultdict
+
+from pmc_summary import short
+
+
+def per_kernel(path, counter):
+    acc = defaultdict(list)
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if r["Counter_Name"] != counter:
+                continue
+            acc[short(r["Kernel_Name"]).split("<")[0]].append(float(r["Counter_Value"]))
+    return acc
+
+
+def main():
+    fetch_csv, write_csv, out = sys.argv[1:4]
+    cmd = sys.argv[4] if len(sys.argv) > 4 else ""
+    fe, wr = per_kernel(fetch_csv, "FETCH_SIZE"), per_kernel(write_csv, "WRITE_SIZE")
+    res = {"_meta": {"command": cmd, "fetch_correction": 2.0, "write_correction": 1.0,
+                     "rule": "MI355X_MICROARCH.md HBM: FETCH_SIZE = 1/2 of wide streaming reads"}}
+    for k in sorted(set(fe) & set(wr)):
+        f = sum(fe[k]) / len(fe[k])
+        w = sum(wr[k]) / len(wr[k])
+        res[k] = {"launches": len(fe[k]), "fetch_kb_raw": round(f, 2), "write_kb": round(w, 2),
+                  "bytes_per_launch": round((2.0 * f + w) * 1024.0)}
+    with open(out, "w") as fh:
+        json.dump(res, fh, indent=1)
+    for k, v in res.items():
+        if k != "_meta":
+            print("%-24s n=%-4d fetch(raw)=%10.1f KB write=%10.1f KB -> %.3f MB/launch" %
+                  (k, v["launches"], v["fetch_kb_raw"], v["write_kb"], v["bytes_per_launch"] / 1e6))
+
+
+if __name__ == "__main__":
+    main()
