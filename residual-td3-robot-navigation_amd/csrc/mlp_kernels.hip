@@ -223,9 +223,13 @@ struct FwdArgs {
     double* action_out;
 };
 
-// rows [tm][hp+4] + input/dy staging [tm][4] + output-layer partial sums [2][kBlock]
+// Output-layer partial sums: [d_out <= 2][4 waves][TM rows] (red_floats per block).
+constexpr int kWaves = kBlock / 64;
+__host__ __device__ constexpr int red_floats(int tm) { return 2 * kWaves * tm; }
+
+// rows [tm][hp+4] + input/dy staging [tm][4] + output-layer partial sums
 inline size_t lds_bytes(int hp, int tm) {
-    return ((size_t)tm * (hp + 4) + tm * 4 + 2 * kBlock) * 4;
+    return ((size_t)tm * (hp + 4) + tm * 4 + red_floats(tm)) * 4;
 }
 
 // Mask image row-tile count: independent of the workgroup height, so any RT reads what any RT
@@ -301,14 +305,82 @@ NAV_DEV void edge_w0(const float* act, int S_, int hp, const float* xin, int d_i
     if (d_in > 3) out[n * d_in + 3] = s3;
 }
 
-// output j of block row rloc from fwd_net's partial sums
+// output j of block row rloc from fwd_net's per-wave partial sums, added in wave order
 template <int RT>
 NAV_DEV float out_y(const MlpDev& net, const float* red, int rloc, int j) {
-    constexpr int TM = RT * 32, PARTS = kBlock / TM;
+    constexpr int TM = RT * 32;
     float y = 0.f;
 #pragma unroll
-    for (int p = 0; p < PARTS; ++p) y += red[(j * PARTS + p) * TM + rloc];
+    for (int p = 0; p < kWaves; ++p) y += red[(j * kWaves + p) * TM + rloc];
     return y + net.params[net.b_off[net.n_hidden] + j];
+}
+
+// Block row of C-layout element i of row tile rt in lane half h.
+NAV_DEV int c_row(int rt, int i, int h) { return rt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h; }
+
+// ReLU mask words of a layer from its C-layout registers (store_layer's bits without the rows).
+template <int NT, int RT>
+NAV_DEV void store_mask(const f32x16 (&acc)[RT][2], uint16_t* mask, int64_t rt0) {
+    const int lane = threadIdx.x & 63;
+    const WaveCols<NT> wc(wave_id());
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        if (!(j == 0 ? wc.has0 : wc.has1)) continue;
+        const int t = j == 0 ? wc.t0 : wc.t1;
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+            uint32_t bits = 0;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) bits |= (acc[rt][j][i] > 0.f ? 1u : 0u) << i;
+            mask[mask_idx(rt0 + rt, NT, t, lane)] = (uint16_t)bits;
+        }
+    }
+}
+
+// Output layer (N = d_out <= 2) straight from the top hidden layer's C-layout registers: every
+// lane forms, per block row it holds, the dot product of its (up to) 2 columns with Wo; a
+// transpose-reduce across the 32 lanes of each lane half (5 xor exchanges that each halve the
+// list a lane carries: 31 exchanges for RT = 2) sums the columns of the wave; the 4 waves'
+// partials meet in LDS (red [d_out][4][TM]) and out_y adds them in wave order. No LDS copy of the
+// top layer, no barrier between the last GEMM and the output layer.
+template <int NT, int RT>
+NAV_DEV void out_partials(const MlpDev& net, const f32x16 (&top)[RT][2], float* red) {
+    constexpr int hp = NT * 32, TM = RT * 32, V = RT * 16, KEEP = V / 32;
+    const int lane = threadIdx.x & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
+    const WaveCols<NT> wc(wv);
+    const float* Wo = net.params + net.w_off[net.n_hidden];
+    const int c0 = wc.t0 * 32 + l32, c1 = (wc.has1 ? wc.t1 : wc.t0) * 32 + l32;
+#pragma unroll
+    for (int jo = 0; jo < 2; ++jo) {
+        if (jo >= net.d_out) break;
+        const float w0 = wc.has0 ? Wo[jo * hp + c0] : 0.f;
+        const float w1 = wc.has1 ? Wo[jo * hp + c1] : 0.f;
+        float v[V];
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) v[rt * 16 + i] = fmaf(top[rt][1][i], w1, top[rt][0][i] * w0);
+        // lane bit b (mask 16 .. 1) picks which half of the list the lane keeps: the survivor k
+        // of lane l32 is list element (l32 * KEEP + k)
+#pragma unroll
+        for (int st = 0; st < 5; ++st) {
+            const int m = 16 >> st, n = V >> st;  // compile-time after unrolling
+            // bitwise selects: a ?: over the list would be turned into a dynamic array index
+            const uint32_t um = (l32 & m) ? 0xffffffffu : 0u;
+#pragma unroll
+            for (int k = 0; k < n / 2; ++k) {
+                const uint32_t lo = __float_as_uint(v[k]), hi = __float_as_uint(v[k + n / 2]);
+                const float send = __uint_as_float((lo & um) | (hi & ~um));
+                const float keep = __uint_as_float((hi & um) | (lo & ~um));
+                v[k] = keep + __shfl_xor(send, m, 64);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < KEEP; ++k) {
+            const int e = l32 * KEEP + k;
+            red[(jo * kWaves + wv) * TM + c_row(e >> 4, e & 15, h)] = v[k];
+        }
+    }
 }
 
 // OUT_LOSS (d_out = 1): q from the output-layer partials against the TD target yt of the thread's
@@ -316,10 +388,10 @@ NAV_DEV float out_y(const MlpDev& net, const float* red, int rloc, int j) {
 // sum of (q - y)^2, and the output layer's gradient partials dWo = dq^T h_top, dbo = sum dq while
 // h_top is still in LDS. `red` = the [2][PARTS][TM] partial-sum scratch (second half reused).
 template <int NT, int RT>
-NAV_DEV void loss_epilogue(const MlpDev& net, const float* act, float* red, int64_t row0,
-                           int64_t M, float yt, float norm, float* dq, float* loss_slot,
-                           float* es) {
-    constexpr int hp = NT * 32, SS = hp + 4, TM = RT * 32;
+NAV_DEV void loss_epilogue(const MlpDev& net, const f32x16 (&top)[RT][2], float* red,
+                           int64_t row0, int64_t M, float yt, float norm, float* dq,
+                           float* loss_slot, float* es) {
+    constexpr int TM = RT * 32;
     const int tid = threadIdx.x;
     const int64_t r = row0 + tid;
     float dqv = 0.f, e2 = 0.f;
@@ -330,7 +402,7 @@ NAV_DEV void loss_epilogue(const MlpDev& net, const float* act, float* red, int6
         e2 = e * e;
         dq[r] = dqv;
     }
-    float* dqs = red + kBlock;  // [TM] dq, then [kBlock/64] wave sums
+    float* dqs = red + kWaves * TM;  // [TM] dq (past output 0's partials), then the wave sums
     float* ws = dqs + TM;
     if (tid < TM) dqs[tid] = dqv;
     const float w = wave_sum(e2);
@@ -343,11 +415,26 @@ NAV_DEV void loss_epilogue(const MlpDev& net, const float* act, float* red, int6
         *loss_slot = sum;
     }
     if (!es) return;
-    if (tid < hp) {
-        float sum = 0.f;
-#pragma unroll 8
-        for (int rr = 0; rr < TM; ++rr) sum = fmaf(dqs[rr], act[rr * SS + tid], sum);
-        es[e_wo(net) + tid] = sum;
+    // dWo partial from the top layer's registers: each lane sums its rows of its columns, the two
+    // lane halves (rows +0 / +4) meet by one exchange
+    {
+        const int lane = tid & 63, h = lane >> 5, l32 = lane & 31;
+        const WaveCols<NT> wc(wave_id());
+        float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const float g = dqs[c_row(rt, i, h)];
+                s0 = fmaf(g, top[rt][0][i], s0);
+                s1 = fmaf(g, top[rt][1][i], s1);
+            }
+        s0 += __shfl_xor(s0, 32, 64);
+        s1 += __shfl_xor(s1, 32, 64);
+        if (h == 0) {
+            if (wc.has0) es[e_wo(net) + wc.t0 * 32 + l32] = s0;
+            if (wc.has1) es[e_wo(net) + wc.t1 * 32 + l32] = s1;
+        }
     }
     if (tid < 4) {  // bo and its 3 padding floats
         float sum = 0.f;
@@ -357,14 +444,19 @@ NAV_DEV void loss_epilogue(const MlpDev& net, const float* act, float* red, int6
     }
 }
 
+// One network's forward over the block's TM rows (input rows xin [TM][4] in LDS). The top hidden
+// layer stays in registers (`top`, C layout) — its LDS rows are written only when save_mask asks
+// for its global copy — and the output layer's per-wave partials land in `red` (ready for out_y
+// after the trailing barrier).
 template <int NT, int RT>
 NAV_DEV void fwd_net(const MlpDev& net, float* act, const float* xin, float* red,
                      uint16_t* masks, int64_t n_rt, float* act_save, uint32_t save_mask,
-                     int64_t row0, int64_t M, int64_t rt0) {
-    constexpr int hp = NT * 32, SS = hp + 4, TM = RT * 32;
+                     int64_t row0, int64_t M, int64_t rt0, f32x16 (&top)[RT][2]) {
+    constexpr int hp = NT * 32, SS = hp + 4;
     const int tid = threadIdx.x, lane = tid & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
-    const int d_in = net.d_in, d_out = net.d_out, nh = net.n_hidden;
+    const int d_in = net.d_in, nh = net.n_hidden;
     const WaveCols<NT> wc(wv);
+    (void)tid;
     // ---- layer 0 (K = d_in) on the VALU, written in the C layout of the wave's column tiles
     {
         const float* W0 = net.params + net.w_off[0];
@@ -403,10 +495,8 @@ NAV_DEV void fwd_net(const MlpDev& net, float* act, const float* xin, float* red
     }
     __syncthreads();
     if (act_save && (save_mask & 1u)) copy_rows<NT, RT>(act, SS, act_save, row0, M);
-
-    // ---- hidden x hidden layers on MFMA
-    for (int L = 1; L < nh; ++L) {
-        f32x16 acc[RT][2];
+    // one hidden x hidden layer on MFMA: acc = relu(rows . W_L + b_L), C layout
+    auto hidden_layer = [&](int L, f32x16 (&acc)[RT][2]) {
         gemm_cols<NT, RT>(act, SS, net.packed + (int64_t)(L - 1) * 2 * hp * hp, acc);
         const float* bL = net.params + net.b_off[L];
 #pragma unroll
@@ -418,37 +508,45 @@ NAV_DEV void fwd_net(const MlpDev& net, float* act, const float* xin, float* red
 #pragma unroll
                 for (int i = 0; i < 16; ++i) acc[rt][j][i] = fmaxf(acc[rt][j][i] + b, 0.f);
         }
+    };
+    auto mask_of = [&](int L) { return masks ? masks + (size_t)L * n_rt * NT * 64 : nullptr; };
+    // ---- layers 1 .. nh-2: rows back into LDS for the next layer
+    for (int L = 1; L + 1 < nh; ++L) {
+        f32x16 acc[RT][2];
+        hidden_layer(L, acc);
         __syncthreads();  // every wave has finished reading the layer's input rows
-        store_layer<NT, RT>(acc, act, SS, masks ? masks + (size_t)L * n_rt * NT * 64 : nullptr,
-                            rt0);
+        store_layer<NT, RT>(acc, act, SS, mask_of(L), rt0);
         __syncthreads();
         if (act_save && ((save_mask >> L) & 1u))
             copy_rows<NT, RT>(act, SS, act_save + (int64_t)L * M * hp, row0, M);
     }
-
-    // ---- output layer (N = d_out <= 2) on the VALU: every thread takes one row and one K slice
-    // of hp / PARTS; the slices' partial sums meet in LDS and add up in a fixed order
-    {
-        constexpr int PARTS = kBlock / TM, KP = hp / PARTS;
-        const int rl = tid % TM, part = tid / TM;
-        const float* ar = act + rl * SS + part * KP;
-        const float* Wo = net.params + net.w_off[nh] + part * KP;
-        float s0 = 0.f, s1 = 0.f;
-#pragma unroll 4
-        for (int k = 0; k < KP; k += 4) {
-            const float4 x = *reinterpret_cast<const float4*>(ar + k);
-            const float4 w0 = *reinterpret_cast<const float4*>(Wo + k);
-            s0 = fmaf(x.x, w0.x, s0); s0 = fmaf(x.y, w0.y, s0);
-            s0 = fmaf(x.z, w0.z, s0); s0 = fmaf(x.w, w0.w, s0);
-            if (d_out > 1) {
-                const float4 w1 = *reinterpret_cast<const float4*>(Wo + hp + k);
-                s1 = fmaf(x.x, w1.x, s1); s1 = fmaf(x.y, w1.y, s1);
-                s1 = fmaf(x.z, w1.z, s1); s1 = fmaf(x.w, w1.w, s1);
-            }
+    // ---- the top hidden layer: registers (defined here only, so they are not live above)
+    if (nh >= 2) {
+        const int L = nh - 1;
+        hidden_layer(L, top);
+        if (act_save && ((save_mask >> L) & 1u)) {
+            __syncthreads();
+            store_layer<NT, RT>(top, act, SS, mask_of(L), rt0);
+            __syncthreads();
+            copy_rows<NT, RT>(act, SS, act_save + (int64_t)L * M * hp, row0, M);
+        } else if (masks) {
+            store_mask<NT, RT>(top, mask_of(L), rt0);
         }
-        red[part * TM + rl] = s0;
-        red[(PARTS + part) * TM + rl] = s1;
+    } else {
+        // the top layer is layer 0: its C-layout registers from the LDS rows just written
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const bool has = j == 0 ? wc.has0 : wc.has1;
+            const float* col = act + (j == 0 ? wc.t0 : wc.t1) * 32 + l32;
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) top[rt][j][i] = has ? col[c_row(rt, i, h) * SS] : 0.f;
+        }
     }
+
+    // ---- output layer (N = d_out <= 2) from the registers; a barrier publishes the partials
+    out_partials<NT, RT>(net, top, red);
     __syncthreads();
 }
 
@@ -491,7 +589,8 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
     __syncthreads();
 
     float* red = xin + TM * 4;  // [2][PARTS][TM]
-    fwd_net<NT, RT>(net, act, xin, red, masks, n_rt, act_save, a.save_mask, row0, M, rt0);
+    f32x16 top[RT][2];
+    fwd_net<NT, RT>(net, act, xin, red, masks, n_rt, act_save, a.save_mask, row0, M, rt0, top);
     const int rloc = tid % TM;
     const int j = tid / TM;
     const int64_t r = row0 + rloc;
@@ -504,7 +603,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
             yt = rw + (a.gamma * mn) * (1.0f - dn);
         }
         const int q = blockIdx.y;
-        loss_epilogue<NT, RT>(net, act, red, row0, M, yt, a.norm, a.dq[q],
+        loss_epilogue<NT, RT>(net, top, red, row0, M, yt, a.norm, a.dq[q],
                               a.loss_part[q] + blockIdx.x,
                               a.eslab[q] ? a.eslab[q] + (int64_t)blockIdx.x * a.ecount : nullptr);
         return;
@@ -705,7 +804,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_bwd(BwdArgs a) {
     const int64_t n_rt = mask_rowtiles(M);
     float* act = smem;
     float* dys = smem + TM * SS;  // [TM][4] dy rows
-    float* xin = dys + TM * 4;    // [TM][4] forward input rows (dW0), inside the 2*kBlock scratch
+    float* xin = dys + TM * 4;    // [TM][4] forward input rows (dW0), inside the red scratch
     const int d_in = net.d_in, d_out = net.d_out;
     static_assert(hp <= kBlock, "one thread per hidden column");
     float* es = a.eslab[y] ? a.eslab[y] + (int64_t)blockIdx.x * a.ecount : nullptr;
@@ -789,7 +888,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
     float* act = smem;
     float* xin = act + TM * SS;    // [TM][4] network input rows
     float* red = xin + TM * 4;     // [2][PARTS][TM] output partial sums
-    float* brow = red + 2 * kBlock;  // [TM][8] the sampled replay rows
+    float* brow = red + red_floats(TM);  // [TM][8] the sampled replay rows
     float* qv = brow + TM * 8;     // [TM] q1'
     if (tid < TM) {
         const int64_t b = row0 + tid;
@@ -806,7 +905,8 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
     }
     __syncthreads();
     // target actor; a' = clamp(pi'(s') + clamp(policy_noise * eps, +-noise_clip), +-max_action)
-    fwd_net<NT, RT>(a.actor_t, act, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0);
+    f32x16 top[RT][2];
+    fwd_net<NT, RT>(a.actor_t, act, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0, top);
     if (tid < 2 * TM) {
         const int rloc = tid % TM, j = tid / TM;
         const int64_t r = row0 + rloc;
@@ -831,9 +931,9 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
     __syncthreads();
     // twin target critics on (s', a'), then y = r + gamma * min(q1', q2') * (1 - done), kept in
     // the row's thread
-    fwd_net<NT, RT>(a.critic_t[0], act, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0);
+    fwd_net<NT, RT>(a.critic_t[0], act, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0, top);
     if (tid < TM) qv[tid] = out_y<RT>(a.critic_t[0], red, tid, 0);
-    fwd_net<NT, RT>(a.critic_t[1], act, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0);
+    fwd_net<NT, RT>(a.critic_t[1], act, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0, top);
     float yt = 0.f;
     if (tid < TM) {
         const float q2 = out_y<RT>(a.critic_t[1], red, tid, 0);
@@ -846,8 +946,8 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
 #pragma unroll 1
     for (int q = 0; q < 2; ++q) {
         fwd_net<NT, RT>(a.critic[q], act, xin, red, a.masks[q], n_rt, a.acts[q], a.save_mask, row0,
-                        B, rt0);
-        loss_epilogue<NT, RT>(a.critic[q], act, red, row0, B, yt, a.norm, a.dq[q],
+                        B, rt0, top);
+        loss_epilogue<NT, RT>(a.critic[q], top, red, row0, B, yt, a.norm, a.dq[q],
                               a.loss_part[q] + blockIdx.x,
                               a.eslab[q] ? a.eslab[q] + (int64_t)blockIdx.x * a.ecount : nullptr);
         __syncthreads();
@@ -889,7 +989,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_actor_rows(ActorRowsArgs a) {
     float* act = smem;
     float* xin = act + TM * SS;      // [TM][4] (s, pi(s))
     float* red = xin + TM * 4;       // [2][PARTS][TM]
-    float* dys = red + 2 * kBlock;   // [TM][4] critic dy
+    float* dys = red + red_floats(TM);  // [TM][4] critic dy
     float* dys2 = dys + TM * 4;      // [TM][4] actor dy = dL/da
     if (tid < TM) {
         const int64_t b = row0 + tid;
@@ -905,13 +1005,14 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_actor_rows(ActorRowsArgs a) {
             make_float4(b < B ? a.dq : 0.f, 0.f, 0.f, 0.f);
     }
     __syncthreads();
-    fwd_net<NT, RT>(a.actor, act, xin, red, a.masks_a, n_rt, a.acts, a.save_mask, row0, B, rt0);
+    f32x16 top[RT][2];
+    fwd_net<NT, RT>(a.actor, act, xin, red, a.masks_a, n_rt, a.acts, a.save_mask, row0, B, rt0, top);
     if (tid < 2 * TM) {
         const int rloc = tid % TM, j = tid / TM;
         xin[rloc * 4 + 2 + j] = row0 + rloc < B ? out_y<RT>(a.actor, red, rloc, j) : 0.f;
     }
     __syncthreads();
-    fwd_net<NT, RT>(a.critic, act, xin, red, a.masks_c, n_rt, nullptr, 0u, row0, B, rt0);
+    fwd_net<NT, RT>(a.critic, act, xin, red, a.masks_c, n_rt, nullptr, 0u, row0, B, rt0, top);
     if (tid < TM && a.q && row0 + tid < B) a.q[row0 + tid] = out_y<RT>(a.critic, red, tid, 0);
     bwd_net<NT, RT>(a.critic, act, dys, xin, a.masks_c, n_rt, nullptr, nullptr, nullptr, 0u, row0,
                     B, rt0);
@@ -1537,7 +1638,7 @@ int launch_bwd(const BwdArgs& a, int n_nets, hipStream_t st) {
 template <int NT, int RT>
 void launch_critic_rows_k(const CriticRowsArgs& a, hipStream_t st) {
     constexpr int TM = RT * 32;
-    const size_t lds = ((size_t)TM * (NT * 32 + 4) + TM * 4 + 2 * kBlock + TM * 8 + TM) * 4;
+    const size_t lds = ((size_t)TM * (NT * 32 + 4) + TM * 4 + red_floats(TM) + TM * 8 + TM) * 4;
     auto k = k_td3_critic_rows<NT, RT>;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
@@ -1547,7 +1648,7 @@ void launch_critic_rows_k(const CriticRowsArgs& a, hipStream_t st) {
 template <int NT, int RT>
 void launch_actor_rows_k(const ActorRowsArgs& a, hipStream_t st) {
     constexpr int TM = RT * 32;
-    const size_t lds = ((size_t)TM * (NT * 32 + 4) + TM * 4 + 2 * kBlock + TM * 8) * 4;
+    const size_t lds = ((size_t)TM * (NT * 32 + 4) + TM * 4 + red_floats(TM) + TM * 8) * 4;
     auto k = k_td3_actor_rows<NT, RT>;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
