@@ -239,7 +239,8 @@ int nav_td3_critic_rows(const nav_mlp* target_actor, const nav_mlp* target_criti
                         void* stream);
 /* train_actor's row-local part (robot.py:382-390) in one launch: sample rows (Philox
  * NAV_TAG_SAMPLE at 2*counter + 1, or idx) into batch [B][8]; actor forward on s (ReLU bits to
- * masks_actor, activations to acts for save_mask bits, which must include the top layer);
+ * masks_actor, activations to acts for save_mask bits; the top layer's dWo partials come
+ * from registers, so it need not be saved);
  * q [B] (nullable) = critic(s, actor(s)); dL/da of L = -mean(q) through the critic (masks_critic)
  * into da [B][2]; the actor's row backward with dz_save_mask rows to dz and its edge partials. */
 int nav_td3_actor_rows(const nav_mlp* actor, const nav_mlp* critic, const nav_replay* replay,

@@ -20,6 +20,11 @@ namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kMaxLayers = 9;
+// train_actor keeps the actor's top hidden layer in registers for its dWo partials (1) or writes
+// it to `acts` and reads it back (0; A/B builds)
+#ifndef NAV_ACTOR_TOP_REGS
+#define NAV_ACTOR_TOP_REGS 1
+#endif
 // workgroups hold RT row tiles of 32 rows (RT = 2 or 4; NAV_MLP_RT)
 
 struct MlpDev {
@@ -343,18 +348,36 @@ NAV_DEV void store_mask(const f32x16 (&acc)[RT][2], uint16_t* mask, int64_t rt0)
 // list a lane carries: 31 exchanges for RT = 2) sums the columns of the wave; the 4 waves'
 // partials meet in LDS (red [d_out][4][TM]) and out_y adds them in wave order. No LDS copy of the
 // top layer, no barrier between the last GEMM and the output layer.
-template <int NT, int RT>
-NAV_DEV void out_partials(const MlpDev& net, const f32x16 (&top)[RT][2], float* red) {
-    constexpr int hp = NT * 32, TM = RT * 32, V = RT * 16, KEEP = V / 32;
-    const int lane = threadIdx.x & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
-    const WaveCols<NT> wc(wv);
+// Wo entries of the lane's columns (0 for absent tiles): wo[output][tile]
+struct WoCols {
+    float w[2][2];
+};
+template <int NT>
+NAV_DEV WoCols load_wo(const MlpDev& net) {
+    constexpr int hp = NT * 32;
+    const int l32 = threadIdx.x & 31;
+    const WaveCols<NT> wc(wave_id());
     const float* Wo = net.params + net.w_off[net.n_hidden];
     const int c0 = wc.t0 * 32 + l32, c1 = (wc.has1 ? wc.t1 : wc.t0) * 32 + l32;
+    WoCols r;
+#pragma unroll
+    for (int jo = 0; jo < 2; ++jo) {
+        const bool on = jo < net.d_out;
+        r.w[jo][0] = on && wc.has0 ? Wo[jo * hp + c0] : 0.f;
+        r.w[jo][1] = on && wc.has1 ? Wo[jo * hp + c1] : 0.f;
+    }
+    return r;
+}
+
+template <int NT, int RT>
+NAV_DEV void out_partials(const MlpDev& net, const f32x16 (&top)[RT][2], const WoCols& wo,
+                          float* red) {
+    constexpr int TM = RT * 32, V = RT * 16, KEEP = V / 32;
+    const int lane = threadIdx.x & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
 #pragma unroll
     for (int jo = 0; jo < 2; ++jo) {
         if (jo >= net.d_out) break;
-        const float w0 = wc.has0 ? Wo[jo * hp + c0] : 0.f;
-        const float w1 = wc.has1 ? Wo[jo * hp + c1] : 0.f;
+        const float w0 = wo.w[jo][0], w1 = wo.w[jo][1];
         float v[V];
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt)
@@ -379,6 +402,38 @@ NAV_DEV void out_partials(const MlpDev& net, const f32x16 (&top)[RT][2], float* 
         for (int k = 0; k < KEEP; ++k) {
             const int e = l32 * KEEP + k;
             red[(jo * kWaves + wv) * TM + c_row(e >> 4, e & 15, h)] = v[k];
+        }
+    }
+}
+
+// Output-layer weight-gradient partials dWo[jo][c] = sum_rows g[row][jo] * h_top[row][c] of the
+// block, straight from the top layer's C-layout registers (g = dL/dy rows in LDS, row stride
+// gstride): each lane sums its 16 * RT rows of its columns in (row tile, element) order, then
+// the two lane halves (rows +0 / +4) meet by one exchange. bwd_net's h_top path (rows from
+// global memory) adds in the same order, so both give the same bits.
+template <int NT, int RT>
+NAV_DEV void wo_grad_regs(const MlpDev& net, const f32x16 (&top)[RT][2], const float* g,
+                          int gstride, float* es) {
+    const int lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
+    const WaveCols<NT> wc(wave_id());
+#pragma unroll
+    for (int jo = 0; jo < 2; ++jo) {
+        if (jo >= net.d_out) break;
+        float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const float gv = g[c_row(rt, i, h) * gstride + jo];
+                s0 = fmaf(gv, top[rt][0][i], s0);
+                s1 = fmaf(gv, top[rt][1][i], s1);
+            }
+        s0 += __shfl_xor(s0, 32, 64);
+        s1 += __shfl_xor(s1, 32, 64);
+        if (h == 0) {
+            float* o = es + e_wo(net) + jo * net.hp;
+            if (wc.has0) o[wc.t0 * 32 + l32] = s0;
+            if (wc.has1) o[wc.t1 * 32 + l32] = s1;
         }
     }
 }
@@ -415,27 +470,7 @@ NAV_DEV void loss_epilogue(const MlpDev& net, const f32x16 (&top)[RT][2], float*
         *loss_slot = sum;
     }
     if (!es) return;
-    // dWo partial from the top layer's registers: each lane sums its rows of its columns, the two
-    // lane halves (rows +0 / +4) meet by one exchange
-    {
-        const int lane = tid & 63, h = lane >> 5, l32 = lane & 31;
-        const WaveCols<NT> wc(wave_id());
-        float s0 = 0.f, s1 = 0.f;
-#pragma unroll
-        for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const float g = dqs[c_row(rt, i, h)];
-                s0 = fmaf(g, top[rt][0][i], s0);
-                s1 = fmaf(g, top[rt][1][i], s1);
-            }
-        s0 += __shfl_xor(s0, 32, 64);
-        s1 += __shfl_xor(s1, 32, 64);
-        if (h == 0) {
-            if (wc.has0) es[e_wo(net) + wc.t0 * 32 + l32] = s0;
-            if (wc.has1) es[e_wo(net) + wc.t1 * 32 + l32] = s1;
-        }
-    }
+    wo_grad_regs<NT, RT>(net, top, dqs, 1, es);
     if (tid < 4) {  // bo and its 3 padding floats
         float sum = 0.f;
         if (tid == 0)
@@ -457,6 +492,8 @@ NAV_DEV void fwd_net(const MlpDev& net, float* act, const float* xin, float* red
     const int d_in = net.d_in, nh = net.n_hidden;
     const WaveCols<NT> wc(wv);
     (void)tid;
+    // the output layer's Wo columns: issued now, in flight under layer 0 and the GEMMs
+    const WoCols wo = load_wo<NT>(net);
     // ---- layer 0 (K = d_in) on the VALU, written in the C layout of the wave's column tiles
     {
         const float* W0 = net.params + net.w_off[0];
@@ -497,12 +534,15 @@ NAV_DEV void fwd_net(const MlpDev& net, float* act, const float* xin, float* red
     if (act_save && (save_mask & 1u)) copy_rows<NT, RT>(act, SS, act_save, row0, M);
     // one hidden x hidden layer on MFMA: acc = relu(rows . W_L + b_L), C layout
     auto hidden_layer = [&](int L, f32x16 (&acc)[RT][2]) {
-        gemm_cols<NT, RT>(act, SS, net.packed + (int64_t)(L - 1) * 2 * hp * hp, acc);
+        // the bias is loaded before the product so its latency hides under the MFMAs
         const float* bL = net.params + net.b_off[L];
+        const float bb0 = wc.has0 ? bL[wc.t0 * 32 + l32] : 0.f;
+        const float bb1 = wc.has1 ? bL[wc.t1 * 32 + l32] : 0.f;
+        gemm_cols<NT, RT>(act, SS, net.packed + (int64_t)(L - 1) * 2 * hp * hp, acc);
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             if (!(j == 0 ? wc.has0 : wc.has1)) continue;
-            const float b = bL[(j == 0 ? wc.t0 : wc.t1) * 32 + l32];
+            const float b = j == 0 ? bb0 : bb1;
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
@@ -546,7 +586,7 @@ NAV_DEV void fwd_net(const MlpDev& net, float* act, const float* xin, float* red
     }
 
     // ---- output layer (N = d_out <= 2) from the registers; a barrier publishes the partials
-    out_partials<NT, RT>(net, top, red);
+    out_partials<NT, RT>(net, top, wo, red);
     __syncthreads();
 }
 
@@ -664,9 +704,23 @@ struct BwdArgs {
     int64_t ecount;
 };
 
+// The lane's ReLU mask words of one layer (issued ahead of the product that needs them).
 template <int NT, int RT>
-NAV_DEV void mask_and_store(f32x16 (&acc)[RT][2], const uint16_t* mask, float* act, int S_,
-                            int64_t rt0) {
+NAV_DEV void load_mask_bits(const uint16_t* mask, int64_t rt0, uint32_t (&bits)[RT][2]) {
+    const int lane = threadIdx.x & 63;
+    const WaveCols<NT> wc(wave_id());
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const bool has = j == 0 ? wc.has0 : wc.has1;
+        const int t = j == 0 ? wc.t0 : wc.t1;
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) bits[rt][j] = has ? mask[mask_idx(rt0 + rt, NT, t, lane)] : 0u;
+    }
+}
+
+template <int NT, int RT>
+NAV_DEV void mask_and_store(f32x16 (&acc)[RT][2], const uint32_t (&mbits)[RT][2], float* act,
+                            int S_) {
     const int lane = threadIdx.x & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
     const WaveCols<NT> wc(wv);
 #pragma unroll
@@ -676,7 +730,7 @@ NAV_DEV void mask_and_store(f32x16 (&acc)[RT][2], const uint16_t* mask, float* a
         float* col = act + t * 32 + l32 + 4 * h * S_;
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) {
-            const uint32_t bits = mask[mask_idx(rt0 + rt, NT, t, lane)];
+            const uint32_t bits = mbits[rt][j];
 #pragma unroll
             for (int i = 0; i < 16; ++i)
                 col[(rt * 32 + (i & 3) + 8 * (i >> 2)) * S_] =
@@ -703,18 +757,24 @@ NAV_DEV void bwd_net(const MlpDev& net, float* act, const float* dys, const floa
         // output layer (robot.py:361 / 392 backward): dWo = dy^T h_top, dbo = sum dy, when the
         // forward did not produce them (it does for the critic's TD loss)
         if (h_top) {
+            // rows in wo_grad_regs' order: per lane half, (row tile, C element); halves added last
             const int n = tid;
             if (n < hp) {
-                float s0 = 0.f, s1 = 0.f;
-                const int rows = (int)(M - row0 < TM ? M - row0 : TM);
+                float s0[2] = {0.f, 0.f}, s1[2] = {0.f, 0.f};
+#pragma unroll
+                for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+                    for (int rt = 0; rt < RT; ++rt)
 #pragma unroll 4
-                for (int rr = 0; rr < rows; ++rr) {
-                    const float h = h_top[(row0 + rr) * hp + n];
-                    s0 = fmaf(dys[rr * 4], h, s0);
-                    s1 = fmaf(dys[rr * 4 + 1], h, s1);
-                }
-                es[e_wo(net) + n] = s0;
-                if (d_out > 1) es[e_wo(net) + hp + n] = s1;
+                        for (int i = 0; i < 16; ++i) {
+                            const int rr = c_row(rt, i, hh);
+                            if (row0 + rr >= M) continue;
+                            const float hv = h_top[(row0 + rr) * hp + n];
+                            s0[hh] = fmaf(dys[rr * 4], hv, s0[hh]);
+                            s1[hh] = fmaf(dys[rr * 4 + 1], hv, s1[hh]);
+                        }
+                es[e_wo(net) + n] = s0[0] + s0[1];
+                if (d_out > 1) es[e_wo(net) + hp + n] = s1[0] + s1[1];
             }
             if (tid < 4) {
                 float s = 0.f;
@@ -770,10 +830,12 @@ NAV_DEV void bwd_net(const MlpDev& net, float* act, const float* dys, const floa
     // hidden layers, top-down: dz_{L-1} = (dz_L . W_L) * relu'(act_{L-1}), B = packed Wb_L
     for (int L = nh - 1; L >= 1; --L) {
         f32x16 acc[RT][2];
+        uint32_t mbits[RT][2];
+        load_mask_bits<NT, RT>(masks + (size_t)(L - 1) * mstride, rt0, mbits);
         gemm_cols<NT, RT>(act, SS,
                           net.packed + (int64_t)(L - 1) * 2 * hp * hp + (int64_t)hp * hp, acc);
         __syncthreads();
-        mask_and_store<NT, RT>(acc, masks + (size_t)(L - 1) * mstride, act, SS, rt0);
+        mask_and_store<NT, RT>(acc, mbits, act, SS);
         __syncthreads();
         finish_layer(L - 1);
     }
@@ -1005,13 +1067,21 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_actor_rows(ActorRowsArgs a) {
             make_float4(b < B ? a.dq : 0.f, 0.f, 0.f, 0.f);
     }
     __syncthreads();
-    f32x16 top[RT][2];
-    fwd_net<NT, RT>(a.actor, act, xin, red, a.masks_a, n_rt, a.acts, a.save_mask, row0, B, rt0, top);
+    // the actor's top hidden layer stays in registers until dL/da is known (its dWo partials)
+    f32x16 topa[RT][2];
+#if NAV_ACTOR_TOP_REGS
+    fwd_net<NT, RT>(a.actor, act, xin, red, a.masks_a, n_rt, a.acts, a.save_mask, row0, B, rt0,
+                    topa);
+#else
+    fwd_net<NT, RT>(a.actor, act, xin, red, a.masks_a, n_rt, a.acts,
+                    a.save_mask | (1u << (a.actor.n_hidden - 1)), row0, B, rt0, topa);
+#endif
     if (tid < 2 * TM) {
         const int rloc = tid % TM, j = tid / TM;
         xin[rloc * 4 + 2 + j] = row0 + rloc < B ? out_y<RT>(a.actor, red, rloc, j) : 0.f;
     }
     __syncthreads();
+    f32x16 top[RT][2];
     fwd_net<NT, RT>(a.critic, act, xin, red, a.masks_c, n_rt, nullptr, 0u, row0, B, rt0, top);
     if (tid < TM && a.q && row0 + tid < B) a.q[row0 + tid] = out_y<RT>(a.critic, red, tid, 0);
     bwd_net<NT, RT>(a.critic, act, dys, xin, a.masks_c, n_rt, nullptr, nullptr, nullptr, 0u, row0,
@@ -1028,10 +1098,24 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_actor_rows(ActorRowsArgs a) {
         dys2[tid * 4 + 3] = 0.f;
     }
     __syncthreads();
-    bwd_net<NT, RT>(a.actor, act, dys2, xin, a.masks_a, n_rt,
-                    a.eslab + (int64_t)blockIdx.x * a.ecount,
-                    a.acts + (int64_t)(a.actor.n_hidden - 1) * B * hp, a.dz, a.dz_save_mask, row0, B,
-                    rt0);
+    // the actor's output layer gradient partials: dWo from its top-layer registers, dbo = column
+    // sums of dL/da (bwd_net's order)
+    float* es = a.eslab + (int64_t)blockIdx.x * a.ecount;
+#if NAV_ACTOR_TOP_REGS
+    wo_grad_regs<NT, RT>(a.actor, topa, dys2, 4, es);
+    if (tid < 4) {
+        float sb = 0.f;
+        if (tid < a.actor.d_out)
+            for (int rr = 0; rr < TM; ++rr) sb += dys2[rr * 4 + tid];
+        es[e_bo(a.actor) + tid] = sb;
+    }
+    bwd_net<NT, RT>(a.actor, act, dys2, xin, a.masks_a, n_rt, es, nullptr, a.dz, a.dz_save_mask,
+                    row0, B, rt0);
+#else
+    bwd_net<NT, RT>(a.actor, act, dys2, xin, a.masks_a, n_rt, es,
+                    a.acts + (int64_t)(a.actor.n_hidden - 1) * B * hp, a.dz, a.dz_save_mask,
+                    row0, B, rt0);
+#endif
 }
 
 // ---------------- hidden x hidden weight gradients (split-M partial slabs) ----------------
@@ -1881,11 +1965,11 @@ int nav_td3_actor_rows(const nav_mlp* actor, const nav_mlp* critic, const nav_re
                        void* stream) {
     ActorRowsArgs a{};
     if (!actor || !critic || !replay || !replay->rows || B < 1 || size < 1 ||
-        size > replay->capacity || size > ((int64_t)1 << 32) || !batch || !da || !acts ||
-        !masks_actor || !masks_critic || !edge_slabs || !make_dev(actor, &a.actor) ||
-        !make_dev(critic, &a.critic) || actor->d_in != 2 || actor->d_out != 2 ||
-        critic->d_in != 4 || critic->d_out != 1 || a.actor.hp != a.critic.hp ||
-        !((save_mask >> (actor->n_hidden - 1)) & 1u) || (save_mask >> actor->n_hidden) ||
+        size > replay->capacity || size > ((int64_t)1 << 32) || !batch || !da ||
+        (save_mask && !acts) || !masks_actor || !masks_critic || !edge_slabs ||
+        !make_dev(actor, &a.actor) || !make_dev(critic, &a.critic) || actor->d_in != 2 ||
+        actor->d_out != 2 || critic->d_in != 4 || critic->d_out != 1 ||
+        a.actor.hp != a.critic.hp || (save_mask >> actor->n_hidden) ||
         (dz_save_mask && !dz) || (dz_save_mask >> actor->n_hidden))
         return NAV_EINVAL;
     a.B = B;

@@ -10,7 +10,8 @@ import os
 import torch  # noqa: F401  (must be loaded first: provides the HIP runtime)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libnavenv.so")
+# NAV_LIB: load another build of the same ABI instead (A/B timing of kernel variants only)
+LIB_PATH = os.environ.get("NAV_LIB") or os.path.join(HERE, "libnavenv.so")
 NAV_EINVAL = -100000
 ABI_VERSION = 2
 

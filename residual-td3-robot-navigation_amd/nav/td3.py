@@ -82,8 +82,8 @@ class TD3:
         self.batch2 = f(B, 8)
         self.q1 = f(B)
         self.dq1, self.dq2 = f(B), f(B)
-        # saved rows: only hidden layers 1 .. nh-2 (+ the actor's top layer for dWo); h_0 and the
-        # top dz are recomputed by the weight-gradient kernel
+        # saved rows: only hidden layers 1 .. nh-2; h_0 and the top dz are recomputed by the
+        # weight-gradient kernel, the top layer's dWo partials come from registers
         self.acts1, self.acts2, self.acts_a = f(nh, B, hp), f(nh, B, hp), f(nh, B, hp)
         self.dz1, self.dz2, self.dz_a = f(nh, B, hp), f(nh, B, hp), f(nh, B, hp)
         self.mask1 = self.critic_network_1.mask_buffer(B)
@@ -207,7 +207,7 @@ class TD3:
                 C.byref(net.desc()), C.byref(c1.desc()), C.byref(rd), len(replay), B, ptr(idx),
                 self.seed & 0xFFFFFFFF, (self.seed >> 32) & 0xFFFFFFFF, self.update_counter,
                 ptr(self.batch2), ptr(self.q1), ptr(self.da), ptr(self.acts_a),
-                net.middle_layers() | net.top_layer(), ptr(self.dz_a), net.middle_layers(),
+                net.middle_layers(), ptr(self.dz_a), net.middle_layers(),
                 ptr(self.mask_a), ptr(self.mask1), ptr(self.eslab_a), s)
         self._grads_and_step([net], [self.actor_optimizer], B, self.batch2, 8, 0, [self.acts_a],
                              [self.dz_a], [self.da], 2, [self.mask_a], [self.eslab_a],
