@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define NAV_ABI_VERSION 2
+#define NAV_ABI_VERSION 3
 #define NAV_EINVAL (-100000)
 
 #define NAV_WORLD_CELLS 100 /* field = float32 [100][100][2] (speed, angle), x-major: cell cx*100+cy
@@ -228,7 +228,10 @@ int nav_mlp_forward(const nav_mlp* nets, int32_t n_nets, int64_t M, const float*
  * * eps, +-noise_clip), +-max_action) with eps from `eps` [B][2] if given else Philox
  * NAV_TAG_TNOISE at counter; y = r + gamma*min(target_critics[0](s', a'), target_critics[1](s',
  * a'))*(1 - done); then both online critics on (s, a) as nav_td3_critic_forward (dq, loss_part,
- * edge_slabs, acts/save_mask, masks). */
+ * edge_slabs, acts/save_mask, masks). With row_backward != 0 each online critic's row backward
+ * (robot.py:361) follows its forward in the same launch, as nav_mlp_backward of dq with the
+ * batch's (s, a) columns as input: W0 / bias partials into edge_slabs, dz rows of dz_save_mask
+ * layers into dz[i] — the caller then skips nav_mlp_backward. */
 int nav_td3_critic_rows(const nav_mlp* target_actor, const nav_mlp* target_critics,
                         const nav_mlp* critics, const nav_replay* replay, int64_t size,
                         int64_t B, const int64_t* idx, uint32_t seed_lo, uint32_t seed_hi,
@@ -236,6 +239,7 @@ int nav_td3_critic_rows(const nav_mlp* target_actor, const nav_mlp* target_criti
                         float noise_clip, float max_action, float gamma, float* batch,
                         float* const* dq, float* const* loss_part, float* const* edge_slabs,
                         float* const* acts, uint32_t save_mask, uint16_t* const* masks,
+                        int32_t row_backward, float* const* dz, uint32_t dz_save_mask,
                         void* stream);
 /* train_actor's row-local part (robot.py:382-390) in one launch: sample rows (Philox
  * NAV_TAG_SAMPLE at 2*counter + 1, or idx) into batch [B][8]; actor forward on s (ReLU bits to

@@ -935,11 +935,16 @@ struct CriticRowsArgs {
     float* acts[2];
     uint32_t save_mask;
     uint16_t* masks[2];
+    int row_backward;     // also each online critic's row backward (robot.py:361 .backward())
+    float* dz[2];         // [nh][B][hp] dz rows of dz_save_mask layers (row_backward)
+    uint32_t dz_save_mask;
 };
 
-// train_critic (robot.py:329-353) for one block of TM batch rows: sample, target policy
+// train_critic (robot.py:329-361) for one block of TM batch rows: sample, target policy
 // smoothing through the target actor, twin target critics, TD target, then the twin online
-// critics with mse_loss's gradient, the loss and the output layers' gradient partials.
+// critics with mse_loss's gradient, the loss and the output layers' gradient partials, and
+// (row_backward) each online critic's row backward with its W0 / bias partials right after its
+// forward, while its rows and ReLU bits are fresh.
 template <int NT, int RT>
 __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -952,6 +957,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
     float* red = xin + TM * 4;     // [2][PARTS][TM] output partial sums
     float* brow = red + red_floats(TM);  // [TM][8] the sampled replay rows
     float* qv = brow + TM * 8;     // [TM] q1'
+    float* dys = qv + TM;          // [TM][4] dL/dq rows of the row backward
     if (tid < TM) {
         const int64_t b = row0 + tid;
         float4 lo = make_float4(0.f, 0.f, 0.f, 0.f), hi = lo;
@@ -1009,10 +1015,19 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
     for (int q = 0; q < 2; ++q) {
         fwd_net<NT, RT>(a.critic[q], act, xin, red, a.masks[q], n_rt, a.acts[q], a.save_mask, row0,
                         B, rt0, top);
+        float* es = a.eslab[q] ? a.eslab[q] + (int64_t)blockIdx.x * a.ecount : nullptr;
         loss_epilogue<NT, RT>(a.critic[q], top, red, row0, B, yt, a.norm, a.dq[q],
-                              a.loss_part[q] + blockIdx.x,
-                              a.eslab[q] ? a.eslab[q] + (int64_t)blockIdx.x * a.ecount : nullptr);
+                              a.loss_part[q] + blockIdx.x, es);
         __syncthreads();
+        if (a.row_backward) {
+            if (tid < TM)
+                *reinterpret_cast<float4*>(dys + tid * 4) =
+                    make_float4(red[kWaves * TM + tid], 0.f, 0.f, 0.f);  // loss_epilogue's dq
+            __syncthreads();
+            bwd_net<NT, RT>(a.critic[q], act, dys, xin, a.masks[q], n_rt, es, nullptr, a.dz[q],
+                            a.dz_save_mask, row0, B, rt0);
+            __syncthreads();  // the next forward's layer 0 overwrites the rows
+        }
     }
 }
 
@@ -1722,7 +1737,8 @@ int launch_bwd(const BwdArgs& a, int n_nets, hipStream_t st) {
 template <int NT, int RT>
 void launch_critic_rows_k(const CriticRowsArgs& a, hipStream_t st) {
     constexpr int TM = RT * 32;
-    const size_t lds = ((size_t)TM * (NT * 32 + 4) + TM * 4 + red_floats(TM) + TM * 8 + TM) * 4;
+    const size_t lds =
+        ((size_t)TM * (NT * 32 + 4) + TM * 4 + red_floats(TM) + TM * 8 + TM + TM * 4) * 4;
     auto k = k_td3_critic_rows<NT, RT>;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
@@ -1913,8 +1929,10 @@ int nav_td3_critic_rows(const nav_mlp* target_actor, const nav_mlp* target_criti
                         float noise_clip, float max_action, float gamma, float* batch,
                         float* const* dq, float* const* loss_part, float* const* edge_slabs,
                         float* const* acts, uint32_t save_mask, uint16_t* const* masks,
+                        int32_t row_backward, float* const* dz, uint32_t dz_save_mask,
                         void* stream) {
     CriticRowsArgs a{};
+    if (row_backward && dz_save_mask && !dz) return NAV_EINVAL;
     if (!target_actor || !target_critics || !critics || !replay || !replay->rows || B < 1 ||
         size < 1 || size > replay->capacity || size > ((int64_t)1 << 32) || !batch || !dq ||
         !loss_part || !masks || !make_dev(target_actor, &a.actor_t) || target_actor->d_in != 2 ||
@@ -1934,7 +1952,13 @@ int nav_td3_critic_rows(const nav_mlp* target_actor, const nav_mlp* target_criti
         a.acts[i] = acts ? acts[i] : nullptr;
         if (save_mask && !a.acts[i]) return NAV_EINVAL;
         a.masks[i] = masks[i];
+        a.dz[i] = dz ? dz[i] : nullptr;
+        if (row_backward && ((dz_save_mask && !a.dz[i]) ||
+                             (dz_save_mask >> critics[i].n_hidden)))
+            return NAV_EINVAL;
     }
+    a.row_backward = row_backward ? 1 : 0;
+    a.dz_save_mask = row_backward ? dz_save_mask : 0u;
     a.B = B;
     a.rows = replay->rows;
     a.rsize = size;

@@ -7,6 +7,7 @@ provides the stream. Sampling: robot.py:98-115 draws `batch_size` rows without r
 device ring, or taken from an injected index tensor (parity tests, the N=1 drop-in).
 """
 import ctypes as C
+import os
 import math
 
 import torch
@@ -68,6 +69,9 @@ class TD3:
         self.seed = seed
         self.update_counter = 0  # Philox counter for sampling / smoothing noise
         self.grad_hook = grad_hook  # e.g. RCCL all-reduce of flat grads (shared policy)
+        # train_critic's row backward inside the critic_rows launch (NAV_CRITIC_ROW_BWD=0: its
+        # own launch; tuning / A/B only)
+        self.row_backward = os.environ.get("NAV_CRITIC_ROW_BWD", "1") != "0"
         self._B = 0
         self.actor_losses, self.critic_losses = [], []
 
@@ -158,9 +162,11 @@ class TD3:
         mid = c1.middle_layers()
         rd = replay.desc()
         # sample + target actor with smoothing noise + twin target critics + TD target + online
-        # twin forward with the MSE gradient: one launch, rows in LDS throughout
+        # twin forward with the MSE gradient + each online critic's row backward: one launch,
+        # rows in LDS throughout
         h, nh = c1.hidden, c1.n_hidden
-        work = (prof.mlp_fwd_flops(2, 2, h, nh, B) + 4 * prof.mlp_fwd_flops(4, 1, h, nh, B))
+        work = (prof.mlp_fwd_flops(2, 2, h, nh, B) + 4 * prof.mlp_fwd_flops(4, 1, h, nh, B) +
+                2 * prof.mlp_bwd_flops(4, 1, h, nh, B, False, True))
         with prof.region("critic_rows", work):
             lib().nav_td3_critic_rows(
                 C.byref(self.target_actor.desc()),
@@ -170,13 +176,15 @@ class TD3:
                 ptr(eps), c.policy_noise, c.noise_clip, c.max_action, c.gamma, ptr(self.batch),
                 parr(self.dq1, self.dq2), parr(self.loss_part[0], self.loss_part[1]),
                 parr(self.eslab1, self.eslab2), parr(self.acts1, self.acts2), mid,
-                parr(self.mask1, self.mask2), s)
+                parr(self.mask1, self.mask2), int(self.row_backward), parr(self.dz1, self.dz2),
+                mid, s)
         bt = self.batch
-        # both critics' backward, weight gradients and reduce + Adam: one launch each
         crit, opts = [c1, c2], [self.critic_optimizer_1, self.critic_optimizer_2]
-        self._bwd(crit, B, [self.dq1, self.dq2], 1, [self.mask1, self.mask2], s, inp=bt, ld_in=8,
-                  in_col=0, dz=[self.dz1, self.dz2], save_mask=mid,
-                  eslab=[self.eslab1, self.eslab2])
+        if not self.row_backward:  # separate backward launch (A/B of the fusion)
+            self._bwd(crit, B, [self.dq1, self.dq2], 1, [self.mask1, self.mask2], s, inp=bt,
+                      ld_in=8, in_col=0, dz=[self.dz1, self.dz2], save_mask=mid,
+                      eslab=[self.eslab1, self.eslab2])
+        # both critics' weight gradients and reduce + Adam: one launch each
         self._grads_and_step(crit, opts, B, bt, 8, 0, [self.acts1, self.acts2],
                              [self.dz1, self.dz2], [self.dq1, self.dq2], 1,
                              [self.mask1, self.mask2], [self.eslab1, self.eslab2],

@@ -422,7 +422,19 @@ def test_fused_row_kernels_match_unfused(nav, hidden, nh, B):
     L.nav_td3_critic_rows(C.byref(ta.desc()), descs(*tc), descs(*cr), C.byref(rd), cap, B, None,
                           slo, shi, counter, None, 0.2, 0.5, 5.0, 0.99, ptr(v["batch"]),
                           parr(*v["dq"]), parr(v["lp"][0], v["lp"][1]), parr(*v["es"]),
-                          parr(*v["acts"]), mid, parr(*v["masks"]), s)
+                          parr(*v["acts"]), mid, parr(*v["masks"]), 0, None, 0, s)
+    # the same launch with each online critic's row backward fused in, against the separate
+    # nav_mlp_backward of the unfused path (same device code, same order: same bits)
+    w = critic_bufs()
+    wdz = [f(nh, B, cr[0].hp), f(nh, B, cr[0].hp)]
+    L.nav_td3_critic_rows(C.byref(ta.desc()), descs(*tc), descs(*cr), C.byref(rd), cap, B, None,
+                          slo, shi, counter, None, 0.2, 0.5, 5.0, 0.99, ptr(w["batch"]),
+                          parr(*w["dq"]), parr(w["lp"][0], w["lp"][1]), parr(*w["es"]),
+                          parr(*w["acts"]), mid, parr(*w["masks"]), 1, parr(*wdz), mid, s)
+    udz = [f(nh, B, cr[0].hp), f(nh, B, cr[0].hp)]
+    ues = [u["es"][0].clone(), u["es"][1].clone()]
+    L.nav_mlp_backward(descs(*cr), 2, B, parr(*u["dq"]), 1, parr(*u["masks"]), ptr(u["batch"]),
+                       8, 0, None, parr(*udz), mid, None, parr(*ues), s)
     torch.cuda.synchronize()
     assert torch.equal(u["batch"], v["batch"])
     assert torch.equal(u["lp"], v["lp"])
@@ -432,6 +444,10 @@ def test_fused_row_kernels_match_unfused(nav, hidden, nh, B):
         assert torch.equal(u["masks"][k], v["masks"][k])
         if mid:
             assert torch.equal(u["acts"][k], v["acts"][k])
+        assert torch.equal(w["dq"][k], v["dq"][k])
+        assert torch.equal(ues[k], w["es"][k])
+        if mid:
+            assert torch.equal(udz[k][1:nh - 1], wdz[k][1:nh - 1])
     # actor rows: sample, actor fwd, critic fwd, backward of -mean Q to the action, actor bwd
     eca = L.nav_mlp_edge_count(2, 2, hp, nh)
     save = actor.middle_layers() | actor.top_layer()
