@@ -1133,6 +1133,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_actor_rows(ActorRowsArgs a) {
 #endif
 }
 
+#if NAV_MLP_PART == 0  // the rest of the learner: main object only
 // ---------------- hidden x hidden weight gradients (split-M partial slabs) ----------------
 // dW_L = dz_L^T h_{L-1} for L = 1 .. nh-1 over the rows of each split. The thin layers' gradients
 // (W0, every bias, Wo, bo) are edge partials of the forward / backward kernels instead.
@@ -1666,6 +1667,8 @@ bool red_net(const nav_mlp* net, const float* hs, int splits, const float* es, f
     return true;
 }
 
+#endif  // NAV_MLP_PART == 0
+
 // ---- launch helpers (template dispatch on NT = hp / 32 and RT = rows / 32) ----
 // Workgroup height: RT = 4 (128 rows, one workgroup per CU) or RT = 2 (64 rows, two per CU so one
 // workgroup's epilogue overlaps the other's MFMA loop). NAV_MLP_RT overrides (tuning only).
@@ -1678,6 +1681,23 @@ int row_tiles() {
     return rt;
 }
 
+// The row kernels (forward, row backward, critic_rows, actor_rows) are instantiated per NT in
+// their own objects (this file built with NAV_MLP_PART = NT, see the Makefile) so the heavy
+// template instantiations compile in parallel; the main object (NAV_MLP_PART = 0) dispatches to
+// them through nav_mlp_rows_<NT>(). Argument structs travel as const void* (same definitions).
+enum { FAM_FWD = 0, FAM_BWD = 1, FAM_CRITIC = 2, FAM_ACTOR = 3 };
+
+}  // namespace
+
+#define NAV_ROWS_DECL(NT_)                                                                   \
+    int nav_mlp_rows_##NT_(int fam, int rt, int in_mode, int out_mode, const void* args,      \
+                           int n_nets, hipStream_t st);
+NAV_ROWS_DECL(1) NAV_ROWS_DECL(2) NAV_ROWS_DECL(3) NAV_ROWS_DECL(4)
+NAV_ROWS_DECL(5) NAV_ROWS_DECL(6) NAV_ROWS_DECL(7) NAV_ROWS_DECL(8)
+#undef NAV_ROWS_DECL
+
+#if NAV_MLP_PART > 0
+namespace {
 template <int NT, int RT, int IN_MODE, int OUT_MODE>
 void launch_fwd_k(const FwdArgs& a, int n_nets, hipStream_t st) {
     const size_t lds = lds_bytes(NT * 32, RT * 32);
@@ -1686,24 +1706,6 @@ void launch_fwd_k(const FwdArgs& a, int n_nets, hipStream_t st) {
                               (int)lds);
     const dim3 grid((unsigned)((a.M + RT * 32 - 1) / (RT * 32)), (unsigned)n_nets);
     hipLaunchKernelGGL(k, grid, dim3(kBlock), lds, st, a);
-}
-
-template <int IN_MODE, int OUT_MODE>
-int launch_fwd(const FwdArgs& a, int n_nets, hipStream_t st) {
-    const int rt = row_tiles();
-#define NAV_FWD_CASE(NT_)                                                                    \
-    case NT_:                                                                                \
-        if (rt == 4) launch_fwd_k<NT_, 4, IN_MODE, OUT_MODE>(a, n_nets, st);                 \
-        else launch_fwd_k<NT_, 2, IN_MODE, OUT_MODE>(a, n_nets, st);                         \
-        break;
-    switch (a.net[0].hp / 32) {
-        NAV_FWD_CASE(1) NAV_FWD_CASE(2) NAV_FWD_CASE(3) NAV_FWD_CASE(4)
-        NAV_FWD_CASE(5) NAV_FWD_CASE(6) NAV_FWD_CASE(7) NAV_FWD_CASE(8)
-        default: return NAV_EINVAL;
-    }
-#undef NAV_FWD_CASE
-    NAV_CHECK_LAUNCH();
-    return 0;
 }
 
 template <int NT, int RT>
@@ -1715,24 +1717,6 @@ void launch_bwd_k(const BwdArgs& a, int n_nets, hipStream_t st) {
     const dim3 grid((unsigned)((a.M + RT * 32 - 1) / (RT * 32)), (unsigned)n_nets);
     hipLaunchKernelGGL(k, grid, dim3(kBlock), lds, st, a);
 }
-
-int launch_bwd(const BwdArgs& a, int n_nets, hipStream_t st) {
-    const int rt = row_tiles();
-#define NAV_BWD_CASE(NT_)                                                                    \
-    case NT_:                                                                                \
-        if (rt == 4) launch_bwd_k<NT_, 4>(a, n_nets, st);                                    \
-        else launch_bwd_k<NT_, 2>(a, n_nets, st);                                            \
-        break;
-    switch (a.net[0].hp / 32) {
-        NAV_BWD_CASE(1) NAV_BWD_CASE(2) NAV_BWD_CASE(3) NAV_BWD_CASE(4)
-        NAV_BWD_CASE(5) NAV_BWD_CASE(6) NAV_BWD_CASE(7) NAV_BWD_CASE(8)
-        default: return NAV_EINVAL;
-    }
-#undef NAV_BWD_CASE
-    NAV_CHECK_LAUNCH();
-    return 0;
-}
-
 
 template <int NT, int RT>
 void launch_critic_rows_k(const CriticRowsArgs& a, hipStream_t st) {
@@ -1755,23 +1739,83 @@ void launch_actor_rows_k(const ActorRowsArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(k, dim3((unsigned)((a.B + TM - 1) / TM)), dim3(kBlock), lds, st, a);
 }
 
-template <typename Args, void (*L2)(const Args&, hipStream_t), void (*L4)(const Args&, hipStream_t)>
-void pick_rt(const Args& a, hipStream_t st) {
-    if (row_tiles() == 4) L4(a, st);
-    else L2(a, st);
+template <int RT>
+int rows_rt(int fam, int in_mode, int out_mode, const void* args, int n_nets, hipStream_t st) {
+    constexpr int NT = NAV_MLP_PART;
+    switch (fam) {
+        case FAM_FWD: {
+            const FwdArgs& a = *static_cast<const FwdArgs*>(args);
+            if (in_mode == IN_BASELINE && out_mode == OUT_ACT)
+                launch_fwd_k<NT, RT, IN_BASELINE, OUT_ACT>(a, n_nets, st);
+            else if (in_mode == IN_F32 && out_mode == OUT_F32)
+                launch_fwd_k<NT, RT, IN_F32, OUT_F32>(a, n_nets, st);
+            else if (in_mode == IN_F32 && out_mode == OUT_TARGET)
+                launch_fwd_k<NT, RT, IN_F32, OUT_TARGET>(a, n_nets, st);
+            else if (in_mode == IN_F32 && out_mode == OUT_LOSS)
+                launch_fwd_k<NT, RT, IN_F32, OUT_LOSS>(a, n_nets, st);
+            else
+                return NAV_EINVAL;
+            return 0;
+        }
+        case FAM_BWD: launch_bwd_k<NT, RT>(*static_cast<const BwdArgs*>(args), n_nets, st); return 0;
+        case FAM_CRITIC:
+            launch_critic_rows_k<NT, RT>(*static_cast<const CriticRowsArgs*>(args), st);
+            return 0;
+        case FAM_ACTOR:
+            launch_actor_rows_k<NT, RT>(*static_cast<const ActorRowsArgs*>(args), st);
+            return 0;
+        default: return NAV_EINVAL;
+    }
 }
 
-#define NAV_ROWS_SWITCH(HP, FN, ARGS, ST)                                                   \
-    switch ((HP) / 32) {                                                                    \
-        case 1: pick_rt<decltype(ARGS), FN<1, 2>, FN<1, 4>>(ARGS, ST); break;               \
-        case 2: pick_rt<decltype(ARGS), FN<2, 2>, FN<2, 4>>(ARGS, ST); break;               \
-        case 3: pick_rt<decltype(ARGS), FN<3, 2>, FN<3, 4>>(ARGS, ST); break;               \
-        case 4: pick_rt<decltype(ARGS), FN<4, 2>, FN<4, 4>>(ARGS, ST); break;               \
-        case 5: pick_rt<decltype(ARGS), FN<5, 2>, FN<5, 4>>(ARGS, ST); break;               \
-        case 6: pick_rt<decltype(ARGS), FN<6, 2>, FN<6, 4>>(ARGS, ST); break;               \
-        case 7: pick_rt<decltype(ARGS), FN<7, 2>, FN<7, 4>>(ARGS, ST); break;               \
-        case 8: pick_rt<decltype(ARGS), FN<8, 2>, FN<8, 4>>(ARGS, ST); break;               \
-        default: return NAV_EINVAL;                                                         \
+}  // namespace
+
+#define NAV_CAT2(a, b) a##b
+#define NAV_CAT(a, b) NAV_CAT2(a, b)
+int NAV_CAT(nav_mlp_rows_, NAV_MLP_PART)(int fam, int rt, int in_mode, int out_mode,
+                                           const void* args, int n_nets, hipStream_t st) {
+    return rt == 4 ? rows_rt<4>(fam, in_mode, out_mode, args, n_nets, st)
+                   : rows_rt<2>(fam, in_mode, out_mode, args, n_nets, st);
+}
+
+#else  // NAV_MLP_PART == 0
+
+namespace {
+
+// hp / 32 -> the per-NT object
+int rows_dispatch(int hp, int fam, int in_mode, int out_mode, const void* args, int n_nets,
+                  hipStream_t st) {
+    const int rt = row_tiles();
+    int r;
+    switch (hp / 32) {
+        case 1: r = nav_mlp_rows_1(fam, rt, in_mode, out_mode, args, n_nets, st); break;
+        case 2: r = nav_mlp_rows_2(fam, rt, in_mode, out_mode, args, n_nets, st); break;
+        case 3: r = nav_mlp_rows_3(fam, rt, in_mode, out_mode, args, n_nets, st); break;
+        case 4: r = nav_mlp_rows_4(fam, rt, in_mode, out_mode, args, n_nets, st); break;
+        case 5: r = nav_mlp_rows_5(fam, rt, in_mode, out_mode, args, n_nets, st); break;
+        case 6: r = nav_mlp_rows_6(fam, rt, in_mode, out_mode, args, n_nets, st); break;
+        case 7: r = nav_mlp_rows_7(fam, rt, in_mode, out_mode, args, n_nets, st); break;
+        case 8: r = nav_mlp_rows_8(fam, rt, in_mode, out_mode, args, n_nets, st); break;
+        default: return NAV_EINVAL;
+    }
+    if (r) return r;
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+template <int IN_MODE, int OUT_MODE>
+int launch_fwd(const FwdArgs& a, int n_nets, hipStream_t st) {
+    return rows_dispatch(a.net[0].hp, FAM_FWD, IN_MODE, OUT_MODE, &a, n_nets, st);
+}
+
+int launch_bwd(const BwdArgs& a, int n_nets, hipStream_t st) {
+    return rows_dispatch(a.net[0].hp, FAM_BWD, 0, 0, &a, n_nets, st);
+}
+
+#define NAV_ROWS_SWITCH(HP, FAM, ARGS, ST)                                                  \
+    {                                                                                       \
+        const int r_ = rows_dispatch((HP), (FAM), 0, 0, &(ARGS), 1, (ST));                   \
+        if (r_) return r_;                                                                  \
     }
 
 }  // namespace
@@ -1976,7 +2020,7 @@ int nav_td3_critic_rows(const nav_mlp* target_actor, const nav_mlp* target_criti
     a.batch = batch;
     a.ecount = edge_count(a.critic[0]);
     a.save_mask = save_mask;
-    NAV_ROWS_SWITCH(a.actor_t.hp, launch_critic_rows_k, a, S(stream))
+    NAV_ROWS_SWITCH(a.actor_t.hp, FAM_CRITIC, a, S(stream))
     NAV_CHECK_LAUNCH();
     return 0;
 }
@@ -2015,7 +2059,7 @@ int nav_td3_actor_rows(const nav_mlp* actor, const nav_mlp* critic, const nav_re
     a.masks_c = masks_critic;
     a.eslab = edge_slabs;
     a.ecount = edge_count(a.actor);
-    NAV_ROWS_SWITCH(a.actor.hp, launch_actor_rows_k, a, S(stream))
+    NAV_ROWS_SWITCH(a.actor.hp, FAM_ACTOR, a, S(stream))
     NAV_CHECK_LAUNCH();
     return 0;
 }
@@ -2249,3 +2293,5 @@ int nav_strided_copy(const float* src, int32_t ld_src, int32_t col_src, float* d
 }
 
 }  // extern "C"
+
+#endif  // NAV_MLP_PART

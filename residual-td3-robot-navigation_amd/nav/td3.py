@@ -99,9 +99,15 @@ class TD3:
         ec = L.nav_mlp_edge_count(4, 1, hp, nh)
         self.eslab1, self.eslab2 = f(self.nblk, ec), f(self.nblk, ec)
         self.eslab_a = f(self.nblk, L.nav_mlp_edge_count(2, 2, hp, nh))
-        self.splits = max(1, min(64, B // 512))
+        # row splits of the weight-gradient launch (partial slabs): critic twins and actor
+        # separately (NAV_WGRAD_SPLITS="critic,actor" overrides; tuning only)
+        sc = sa = max(1, min(64, B // 512))
+        env = os.environ.get("NAV_WGRAD_SPLITS")
+        if env:
+            sc, sa = (max(1, min(int(v), max(1, B // 32))) for v in env.split(","))
+        self.splits_c, self.splits_a = sc, sa
         hc = max(4, L.nav_mlp_hidden_count(hp, nh))
-        self.hslab, self.hslab2 = f(self.splits, hc), f(self.splits, hc)
+        self.hslab, self.hslab2 = f(max(sc, sa), hc), f(sc, hc)
         self.grad_a = f(self.actor_network.count)
         self.grad_c1 = f(self.critic_network_1.count)
         self.grad_c2 = f(self.critic_network_1.count)
@@ -115,18 +121,19 @@ class TD3:
         writes the flat gradients, the hook runs, then Adam steps separately."""
         n = len(nets)
         net = nets[0]
+        splits = self.splits_a if net is self.actor_network else self.splits_c
         if net.n_hidden > 1:
             with prof.region("mlp_wgrad", n * prof.mlp_wgrad_flops(net.hidden, net.n_hidden, M)):
                 lib().nav_mlp_wgrad(descs(*nets), n, M, ptr(inp), ld_in, in_col, parr(*acts),
                                     parr(*dz), parr(*dy), ld_dy, parr(*masks), parr(*hslabs),
-                                    self.splits, s)
-        nbytes = sum(4.0 * (self.splits * (x.count - e.shape[1]) + e.numel() + 3 * x.count)
+                                    splits, s)
+        nbytes = sum(4.0 * (splits * (x.count - e.shape[1]) + e.numel() + 3 * x.count)
                      for x, e in zip(nets, eslabs))
         if self.grad_hook is None:
             coeffs = [o.advance() for o in opts]
             with prof.region("grad_reduce", nbytes):
                 lib().nav_grad_reduce_adam(
-                    descs(*nets), n, parr(*hslabs), self.splits, parr(*eslabs), self.nblk,
+                    descs(*nets), n, parr(*hslabs), splits, parr(*eslabs), self.nblk,
                     parr(*grads), parr(*[o.m for o in opts]), parr(*[o.v for o in opts]),
                     opts[0].b1, opts[0].b2, opts[0].eps,
                     (C.c_float * n)(*[c[0] for c in coeffs]), (C.c_float * n)(*[c[1] for c in coeffs]),
@@ -134,7 +141,7 @@ class TD3:
             return
         for x, o, h, e, g in zip(nets, opts, hslabs, eslabs, grads):
             with prof.region("grad_reduce", nbytes / n):
-                lib().nav_grad_reduce(C.byref(x.desc()), ptr(h), self.splits, ptr(e), self.nblk,
+                lib().nav_grad_reduce(C.byref(x.desc()), ptr(h), splits, ptr(e), self.nblk,
                                       ptr(g), s)
             self.grad_hook(g)
             o.step(g, stream)
