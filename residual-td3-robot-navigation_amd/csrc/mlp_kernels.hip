@@ -1190,9 +1190,13 @@ NAV_DEV void wgrad_hidden(const WgradArgs& a, int y, int job, int split, float* 
     // 32x32 sub-tiles inside hp (wave-uniform)
     const bool n0k = n0 + wn < hp, n1k = n0 + wn + 32 < hp;
     const bool k0k = k0 + wk < hp, k1k = k0 + wk + 32 < hp;
-    const int64_t per = (M + a.splits - 1) / a.splits;
-    const int64_t m_lo = (int64_t)split * per;
+    // 32-row aligned splits: a split's mask row tiles start at a tile boundary and every per-row
+    // offset inside the split is a 32-bit product (nav_mlp_wgrad checks the bound); the 64-bit
+    // address math happens once per split
+    const int64_t per = (((M + a.splits - 1) / a.splits) + 31) & ~(int64_t)31;
+    const int64_t m_lo = (int64_t)split * per < M ? (int64_t)split * per : M;
     const int64_t m_hi = m_lo + per < M ? m_lo + per : M;
+    const int cnt = (int)(m_hi - m_lo);
     f32x16 acc[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -1206,11 +1210,14 @@ NAV_DEV void wgrad_hidden(const WgradArgs& a, int y, int job, int split, float* 
     const int pn = n0 + 4 * c4, qk = k0 + 4 * c4;
     const bool pc_ok = pn < hp, qc_ok = qk < hp;
     const int pnc = pc_ok ? pn : 0, qkc = qc_ok ? qk : 0;
-    const float* Pc = a.dz[y] + (PR ? 0 : (int64_t)L * MH + pnc);
-    const float* Qc = a.acts[y] + (QR ? 0 : (int64_t)(L - 1) * MH + qkc);
+    const float* Pb = a.dz[y] + (PR ? 0 : (int64_t)L * MH + m_lo * hp + pnc);
+    const float* Qb = QR ? a.in + m_lo * a.ld_in + a.in_col
+                         : a.acts[y] + (int64_t)(L - 1) * MH + m_lo * hp + qkc;
+    const int ldp = PR ? a.ld_dy : hp, ldq = QR ? a.ld_in : hp;
     float wo0[4] = {0.f, 0.f, 0.f, 0.f}, wo1[4] = {0.f, 0.f, 0.f, 0.f};
     float w0[4][4] = {}, b0[4] = {0.f, 0.f, 0.f, 0.f};
     const uint16_t* mk = a.masks[y];
+    const int NTm = hp >> 5;
     if (PR) {
         const float* Wo = net.params + net.w_off[nh];
 #pragma unroll
@@ -1218,7 +1225,8 @@ NAV_DEV void wgrad_hidden(const WgradArgs& a, int y, int job, int split, float* 
             wo0[c] = Wo[pnc + c];
             wo1[c] = d_out > 1 ? Wo[hp + pnc + c] : 0.f;
         }
-        mk += (size_t)(nh - 1) * mask_rowtiles(M) * (hp >> 5) * 64;
+        mk += (size_t)(nh - 1) * mask_rowtiles(M) * NTm * 64 + mask_idx(m_lo >> 5, NTm, pnc >> 5, pnc & 31);
+        Pb = a.dy[y] + m_lo * a.ld_dy;
     }
     if (QR) {
         const float* W0 = net.params + net.w_off[0];
@@ -1234,36 +1242,35 @@ NAV_DEV void wgrad_hidden(const WgradArgs& a, int y, int job, int split, float* 
     const int x1 = d_in > 1 ? 1 : 0, x2 = d_in > 2 ? 2 : 0, x3 = d_in > 3 ? 3 : 0;
     float4 rp[4], rq[4];
     uint2 rm[4];
-    auto load = [&](int64_t m0) {
+    // r0: the chunk's first row relative to m_lo
+    auto load = [&](int r0) {
 #pragma unroll
         for (int f = 0; f < 4; ++f) {
-            const int64_t m = m0 + rr0 + 8 * f;
-            const int64_t mc = m < m_hi ? m : m_lo;
+            const int rel = r0 + rr0 + 8 * f;
+            const int rc = rel < cnt ? rel : 0;
             if (PR) {
-                const int rr = (int)(mc & 31);
-                rm[f] = *reinterpret_cast<const uint2*>(
-                    mk + mask_idx(mc >> 5, hp >> 5, pnc >> 5, (pnc & 31) + 32 * ((rr >> 2) & 1)));
-                const float* g = a.dy[y] + mc * a.ld_dy;
+                rm[f] = *reinterpret_cast<const uint2*>(mk + (rc >> 5) * (NTm * 64) +
+                                                        32 * ((rc >> 2) & 1));
+                const float* g = Pb + rc * ldp;
                 rp[f] = make_float4(g[0], g[g1], 0.f, 0.f);
             } else {
-                rp[f] = *reinterpret_cast<const float4*>(Pc + mc * hp);
+                rp[f] = *reinterpret_cast<const float4*>(Pb + rc * ldp);
             }
             if (QR) {
-                const float* x = a.in + mc * a.ld_in + a.in_col;
+                const float* x = Qb + rc * ldq;
                 rq[f] = make_float4(x[0], x[x1], x[x2], x[x3]);
             } else {
-                rq[f] = *reinterpret_cast<const float4*>(Qc + mc * hp);
+                rq[f] = *reinterpret_cast<const float4*>(Qb + rc * ldq);
             }
         }
     };
     // staging of row group f of a chunk into LDS buffer buf, one panel at a time
-    auto storeP = [&](int buf, int64_t m0, int f) {
+    auto storeP = [&](int buf, int r0, int f) {
         const int r = rr0 + 8 * f;
-        const bool ok = m0 + r < m_hi;
+        const bool ok = r0 + r < cnt;
         float4 pv = rp[f];
         if (PR) {
-            const int64_t mc = ok ? m0 + r : m_lo;
-            const int rr = (int)(mc & 31);
+            const int rr = ok ? r : 0;  // row within the 32-row tile (r0 is a multiple of 32)
             const int i = (rr & 3) + 4 * (rr >> 3);  // C-layout element of the row
             const float gx = rp[f].x, gy = d_out > 1 ? rp[f].y : 0.f;
             const uint32_t wx = rm[f].x, wy = rm[f].y;
@@ -1274,9 +1281,9 @@ NAV_DEV void wgrad_hidden(const WgradArgs& a, int y, int job, int split, float* 
         }
         *reinterpret_cast<float4*>(Ps + (buf * WG_MC + r) * WA_LD + 4 * c4) = sel4(ok && pc_ok, pv);
     };
-    auto storeQ = [&](int buf, int64_t m0, int f) {
+    auto storeQ = [&](int buf, int r0, int f) {
         const int r = rr0 + 8 * f;
-        const bool ok = m0 + r < m_hi;
+        const bool ok = r0 + r < cnt;
         float4 qv = rq[f];
         if (QR) {
             float4 x = rq[f];
@@ -1290,19 +1297,19 @@ NAV_DEV void wgrad_hidden(const WgradArgs& a, int y, int job, int split, float* 
         }
         *reinterpret_cast<float4*>(Qs + (buf * WG_MC + r) * WA_LD + 4 * c4) = sel4(ok && qc_ok, qv);
     };
-    const int nch = (int)((m_hi - m_lo + WG_MC - 1) / WG_MC);
+    const int nch = (cnt + WG_MC - 1) / WG_MC;
     if (nch > 0) {
-        load(m_lo);
+        load(0);
 #pragma unroll
         for (int f = 0; f < 4; ++f) {
-            storeP(0, m_lo, f);
-            storeQ(0, m_lo, f);
+            storeP(0, 0, f);
+            storeQ(0, 0, f);
         }
     }
     __syncthreads();
     for (int c = 0; c < nch; ++c) {
         const bool more = c + 1 < nch;
-        const int64_t mn = m_lo + (int64_t)(c + 1) * WG_MC;
+        const int mn = (c + 1) * WG_MC;
         if (FULL || more) load(mn);  // rows past m_hi load clamped addresses
         const int buf = c & 1;
         const float* pb = Ps + buf * WG_MC * WA_LD;
@@ -2129,6 +2136,13 @@ int nav_mlp_wgrad(const nav_mlp* nets, int32_t n_nets, int64_t M, const float* i
     }
     if (in_col < 0 || in_col + a.net[0].d_in > ld_in) return NAV_EINVAL;
     if (a.net[0].n_hidden < 2) return 0;
+    {   // per-split row offsets are 32-bit inside the kernel
+        const int64_t per = (((M + splits - 1) / splits) + 31) & ~(int64_t)31;
+        int64_t ld = ld_in > ld_dy ? ld_in : ld_dy;
+        ld = ld > a.net[0].hp ? ld : a.net[0].hp;
+        if (per * ld >= ((int64_t)1 << 31) || (per / 32) * a.net[0].hp * 2 >= ((int64_t)1 << 31))
+            return NAV_EINVAL;
+    }
     a.M = M;
     a.in = in;
     a.ld_in = ld_in;
