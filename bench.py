@@ -111,9 +111,12 @@ def step_kernel_sweep(field, sizes, reps=20):
             env.agent_step(act, rep)
             env.step(act)
         t = prof.KernelTimer(["agent_step", "env_step"])
+        # each kernel back to back, as a training loop / a pure Environment.step loop runs it
+        # (interleaved, env_step paid the write-back of agent_step's dirty lines: PMC r01p)
         with prof.timing(t):
             for _ in range(reps):
                 env.agent_step(act, rep)
+            for _ in range(reps):
                 env.step(act)
         s = t.summary()
         row = {"n_envs": n}

@@ -2,6 +2,8 @@
 // (robot.py) as gfx950 kernels: one env per lane, structure-of-arrays state in HBM, f64 state
 // math (the reference's robot_state is float64), reward/done counts reduced per block through
 // wave shuffles and LDS.
+#include <stdlib.h>
+
 #include "nav_device.h"
 
 using namespace nav;
@@ -76,6 +78,7 @@ __global__ __launch_bounds__(kBlock) void k_env_reset(nav_params p, nav_env_soa 
     reinterpret_cast<double2*>(env.state)[e] = region_sample(reg, u0, u1);
 }
 
+template <bool NT>
 __global__ __launch_bounds__(kBlock) void k_env_step(int64_t n, double2* __restrict__ state,
                                                      const float2* __restrict__ field,
                                                      const double2* __restrict__ action,
@@ -83,10 +86,26 @@ __global__ __launch_bounds__(kBlock) void k_env_step(int64_t n, double2* __restr
     // environment.py:122-127: 16 B state in, 16 B action in, 16 B state out per env
     const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (e >= n) return;
-    const double2 s = state[e];
-    const double2 nx = dynamics(field, s, action[e]);
+    double2 s, a;
+    if (NT) {
+        s.x = __builtin_nontemporal_load(&state[e].x);
+        s.y = __builtin_nontemporal_load(&state[e].y);
+        a.x = __builtin_nontemporal_load(&action[e].x);
+        a.y = __builtin_nontemporal_load(&action[e].y);
+    } else {
+        s = state[e];
+        a = action[e];
+    }
+    const double2 nx = dynamics(field, s, a);
     const bool ok = in_world(nx);
-    if (ok) state[e] = nx;
+    if (NT) {
+        if (ok) {
+            __builtin_nontemporal_store(nx.x, &state[e].x);
+            __builtin_nontemporal_store(nx.y, &state[e].y);
+        }
+    } else if (ok) {
+        state[e] = nx;
+    }
     if (next_out) next_out[e] = ok ? nx : s;
 }
 
@@ -732,7 +751,14 @@ int nav_env_step(const nav_params* p, const nav_env_soa* env, const float* field
     if (!p || !env || env->n < 0 || !field || (env->n && (!env->state || !action)))
         return NAV_EINVAL;
     if (env->n == 0) return 0;
-    hipLaunchKernelGGL(k_env_step, dim3(blocks_for(env->n)), dim3(kBlock), 0, S(stream), env->n,
+    // Non-temporal state/action streams once the 48 B/env working set is past the 256 MB MALL
+    // (>= 4 Mi envs): 219 -> 204 us at 2^24 envs (profiles/r01p_step_ab.log). Below that the
+    // state stays cache-resident between steps, so default-policy accesses.
+    // NAV_ENV_STEP_NT=0/1 forces either (A/B only).
+    static const int nt_env = getenv("NAV_ENV_STEP_NT") ? atoi(getenv("NAV_ENV_STEP_NT")) : -1;
+    const bool nt = nt_env >= 0 ? nt_env != 0 : env->n >= (int64_t(1) << 22);
+    hipLaunchKernelGGL(nt ? k_env_step<true> : k_env_step<false>, dim3(blocks_for(env->n)),
+                       dim3(kBlock), 0, S(stream), env->n,
                        reinterpret_cast<double2*>(env->state),
                        reinterpret_cast<const float2*>(field),
                        reinterpret_cast<const double2*>(action),
