@@ -1,8 +1,9 @@
 """GPU parity of the environment / agent-tick kernels against the oracle and the reference goldens.
 
 Tolerances (north_star): seeding and indexing bit-exact; float state within 1e-5 (observed: f64
-state agrees to ~1e-13 — the only differences come from 1-ulp atan2/sin/cos differences between
-the device math library, libm and numpy's SIMD atan2)."""
+state agrees to ~1e-13 — the kernels move by speed * R(rot) * a instead of the reference's
+speed * |a| * (cos, sin)(atan2 + rot), the same displacement up to a few ulp, and numpy's SIMD
+atan2 differs from libm by 1 ulp)."""
 import ctypes as C
 
 import numpy as np
@@ -62,6 +63,46 @@ def test_env_step_commit_semantics(nav):
     assert np.array_equal(ns.cpu().numpy(), out)
     nan_rows = np.isnan(g["action"]).any(1)
     assert np.array_equal(out[nan_rows], g["state"][nan_rows])  # NaN action: unchanged
+
+
+def test_env_step_full_size_nontemporal_path(nav):
+    """4 Mi + 37 envs (the non-temporal stream path, ragged last block): every env is a tiled copy
+    of a golden case, so each must land on that case's reference result, and bit-identical to the
+    small-n (default cache policy) launch of the same cases."""
+    from nav.vec_env import VecEnv
+    g = golden("dynamics.npz")
+    f = field_of(g["speed"], g["angle"])
+    k = len(g["state"])
+    n = (1 << 22) + 37
+    reps = (n + k - 1) // k
+    st = torch.tensor(g["state"], device=DEV).repeat(reps, 1)[:n].contiguous()
+    ac = torch.tensor(g["action"], device=DEV).repeat(reps, 1)[:n].contiguous()
+    big = VecEnv(n, f, init=False)
+    big.state.copy_(st)
+    ns = torch.zeros(n, 2, dtype=torch.float64, device=DEV)
+    big.step(ac, next_state=ns)
+    small = VecEnv(k, f, init=False)
+    small.state.copy_(st[:k])
+    small.step(ac[:k])
+    torch.cuda.synchronize()
+    out = big.state.cpu().numpy()
+    want = np.tile(g["step"], (reps, 1))[:n]
+    assert np.max(np.abs(out - want)) < 1e-11
+    assert np.array_equal(ns.cpu().numpy(), out)
+    assert np.array_equal(out[:k], small.state.cpu().numpy())
+    del big, st, ac, ns
+    torch.cuda.empty_cache()
+
+
+def test_empty_launches_are_noops(nav):
+    from nav import _lib
+    from nav.vec_env import VecEnv
+    g = golden("dynamics.npz")
+    f = field_of(g["speed"], g["angle"])
+    env = VecEnv(1, f, init=False)
+    s = torch.zeros(0, 2, dtype=torch.float64, device=DEV)
+    assert env.dynamics(s, s).shape == (0, 2)
+    assert _lib.lib().nav_dynamics(None, None, None, None, 0, None) == 0
 
 
 @pytest.mark.parametrize("n,epg", [(4096, 1), (5000, 7), (1, 1)])
