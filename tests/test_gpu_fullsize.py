@@ -1,0 +1,87 @@
+"""GPU checks at the bench configuration (BASELINE config 3: 65 536 envs in 64 groups of 1 024,
+2x256 actor/critic, TD3 batch 32 768): the fused tick of a random subset of envs spread over every
+group against the oracle's restated tick (robot.py:645-675, 727-762, environment.py:98-137) on the
+same inputs, and size-independent invariants of the whole state and of the learner after it."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module")
+def trainer():
+    from nav import _lib
+    from nav.trainer import VecTrainer
+    _lib.require_gpu()
+    torch.cuda.set_device(0)
+    tr = VecTrainer(n_envs=65536, hidden=256, n_hidden=2, batch=32768, updates_per_step=2,
+                    envs_per_group=1024, device=DEV)
+    for _ in range(3):  # the replay ring holds a batch after the first step: learner active
+        tr.step()
+    torch.cuda.synchronize()
+    return tr
+
+
+def test_bench_config_tick_subset_vs_oracle(trainer, orc):
+    from oracle import oracle as O
+    tr, env = trainer, trainer.env
+    n = tr.n
+    fields = env.field.cpu().numpy()
+    speed, angle = np.ascontiguousarray(fields[..., 0]), np.ascontiguousarray(fields[..., 1])
+    ost = O.VecAgentState(n)
+    ost.state[:] = env.state.cpu().numpy()
+    ost.goal[:] = env.goal.cpu().numpy()
+    ost.region[:] = env.region.cpu().numpy()
+    ost.hist[:] = env.hist.cpu().numpy().transpose(1, 0, 2)
+    ost.meta[:] = env.meta.cpu().numpy().astype(np.uint32)
+    ost.plan_index[:] = env.plan_index.cpu().numpy()
+    ost.path_length[:] = env.path_length.cpu().numpy()
+    ost.episodes[:] = env.episodes.cpu().numpy()
+    ost.noise_scale[:] = env.noise_scale.cpu().numpy()
+    pts = env.demo_xy.cpu().numpy()
+    off = env.demo_off.cpu().numpy()
+    epg = n // (len(off) - 1)
+    p = O.default_params(tr.seed)
+    tr.act()
+    a = tr.action.cpu().numpy()
+    assert np.isfinite(a).all() and np.abs(a).max() <= 5.0
+    base = tr.replay.position
+    env.agent_step(tr.action, tr.replay)
+    torch.cuda.synchronize()
+    rows = tr.replay.rows.cpu().numpy()
+    nxt = env.next_state.cpu().numpy()
+    st = env.state.cpu().numpy()
+    rng = np.random.default_rng(5)
+    idx = np.concatenate([g * epg + rng.choice(epg, 2, replace=False)
+                          for g in range(len(off) - 1)])
+    for e in idx:
+        grp = e // epg
+        fl, ns, row, r = ost.tick(p, speed, angle, pts[off[grp]:off[grp + 1]], int(e), a[e])
+        assert np.max(np.abs(ns - nxt[e])) < 1e-11, e
+        assert np.allclose(row, rows[(base + e) % tr.replay.capacity], rtol=1e-5, atol=1e-5), e
+        assert np.max(np.abs(ost.state[e] - st[e])) < 1e-11, e
+    for k in ("plan_index", "path_length", "episodes"):
+        assert np.array_equal(getattr(env, k)[idx].cpu().numpy(), getattr(ost, k)[idx]), k
+
+
+def test_bench_config_invariants(trainer):
+    tr, env = trainer, trainer.env
+    tr.step()
+    torch.cuda.synchronize()
+    s = env.state.cpu().numpy()
+    assert np.isfinite(s).all() and s.min() >= 0.0 and s.max() <= 100.0 - 1.0001
+    plan, path = env.plan_index.cpu().numpy(), env.path_length.cpu().numpy()
+    assert (plan >= 1).all() and (plan < path).all()  # an episode ends at plan == path - 1
+    assert (env.episodes.cpu().numpy() >= 0).all()
+    ns = env.noise_scale.cpu().numpy()
+    assert np.isfinite(ns).all() and (ns > 0).all()
+    filled = min(len(tr.replay), tr.replay.capacity)
+    rows = tr.replay.rows[:filled].cpu().numpy()
+    assert np.isfinite(rows).all()
+    assert np.isin(rows[:, 7], (0.0, 1.0)).all()       # done flag
+    assert (np.abs(rows[:, 2:4]) <= 5.0).all()          # stored actions are clipped
+    for net in tr.td3.networks().values():
+        assert torch.isfinite(net.params).all()
