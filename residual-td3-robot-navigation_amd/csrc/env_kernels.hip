@@ -317,6 +317,10 @@ __global__ __launch_bounds__(kBlock) void k_agent_step(nav_params p, nav_env_soa
 // latency), combined through LDS.
 constexpr int kDemoEnvs = 64;
 constexpr int kDemoSplit = 8;
+#ifndef NAV_DEMO_BATCH
+#define NAV_DEMO_BATCH 16
+#endif
+constexpr int kDemoBatch = NAV_DEMO_BATCH;  // candidates per dependent-load trip (indexed reward)
 constexpr int kDemoBlock = kDemoEnvs * kDemoSplit;
 
 NAV_DEV double demo_min_global(const double2* __restrict__ d, int64_t m, double x, double y) {
@@ -614,18 +618,25 @@ __global__ __launch_bounds__(kBlock) void k_demo_reward_idx(nav_params p, int64_
     if (s.x >= 0.0 && s.x < 100.0 && s.y >= 0.0 && s.y < 100.0) {
         const int64_t k = g * kCells + (int64_t)((int)s.x * NAV_WORLD_CELLS + (int)s.y);
         const int64_t a = start[k], b = start[k + 1];
-        int64_t j = a;
-        double b1 = __builtin_inf();
-        for (; j + 1 < b; j += 2) {
-            const double2 q0 = pts[cand[j]], q1 = pts[cand[j + 1]];
-            best = fmin(best, sqd(s.x, s.y, q0.x, q0.y));
-            b1 = fmin(b1, sqd(s.x, s.y, q1.x, q1.y));
+        // kDemoBatch candidates per trip: their indices, then their points, are independent loads
+        // (two dependent round trips per batch instead of per candidate; a wave runs as many
+        // trips as its longest candidate list). Slots past the list repeat candidate a — a
+        // duplicate cannot change a min, so the result is the same bits as one by one.
+        double bu[kDemoBatch];
+#pragma unroll
+        for (int u = 0; u < kDemoBatch; ++u) bu[u] = __builtin_inf();
+        for (int64_t j = a; j < b; j += kDemoBatch) {
+            int32_t c[kDemoBatch];
+#pragma unroll
+            for (int u = 0; u < kDemoBatch; ++u) c[u] = cand[j + u < b ? j + u : a];
+            double2 q[kDemoBatch];
+#pragma unroll
+            for (int u = 0; u < kDemoBatch; ++u) q[u] = pts[c[u]];
+#pragma unroll
+            for (int u = 0; u < kDemoBatch; ++u) bu[u] = fmin(bu[u], sqd(s.x, s.y, q[u].x, q[u].y));
         }
-        if (j < b) {
-            const double2 q0 = pts[cand[j]];
-            best = fmin(best, sqd(s.x, s.y, q0.x, q0.y));
-        }
-        best = fmin(best, b1);
+#pragma unroll
+        for (int u = 0; u < kDemoBatch; ++u) best = fmin(best, bu[u]);
     } else {  // outside the indexed cells: brute force
         best = demo_min_global(pts, (off ? off[g + 1] - off[g] : 0), s.x, s.y);
     }
