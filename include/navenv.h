@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define NAV_ABI_VERSION 3
+#define NAV_ABI_VERSION 4
 #define NAV_EINVAL (-100000)
 
 #define NAV_WORLD_CELLS 100 /* field = float32 [100][100][2] (speed, angle), x-major: cell cx*100+cy
@@ -178,6 +178,17 @@ int nav_demo_reward_indexed(const nav_params* p, int64_t n, const double* next_s
                             const int64_t* cell_start, const int32_t* cand,
                             const nav_replay* replay, int64_t replay_base, double* reward_out,
                             void* stream);
+/* nav_agent_step + nav_demo_reward_indexed in one launch (same results bit for bit): flagged envs
+ * get their demo-proximity reward through the index before the replay row is written, so the row
+ * is stored once with the final reward. reward_out (nullable) [n] receives the reward of the
+ * flagged envs only, as nav_demo_reward_indexed writes it. Replaces the pair of calls the
+ * reference makes per step: robot.py:661-675 process_transition -> compute_reward (727-762). */
+int nav_agent_step_indexed(const nav_params* p, const nav_env_soa* env, const float* field,
+                           const double* action, const nav_replay* replay, int64_t replay_base,
+                           const nav_step_out* out, const double* demo_xy,
+                           const int64_t* demo_off, int32_t envs_per_group,
+                           const int64_t* cell_start, const int32_t* cand, double* reward_out,
+                           void* stream);
 /* robot.py:753 min_j ||p_i - d_j|| (scipy cdist euclidean, f64) for n points [n][2]. */
 int nav_demo_min(const double* points, int64_t n, const double* demo_xy, int64_t m,
                  double* out, void* stream);

@@ -129,8 +129,7 @@ struct TransOut {
 };
 
 NAV_DEV TransOut transition(const nav_params& p, const nav_env_soa& env, int64_t e, double2 s,
-                            double2 a, double2 ns, uint32_t meta, int32_t plan, int32_t path,
-                            float4* __restrict__ rows, int64_t slot) {
+                            double2 a, double2 ns, uint32_t meta, int32_t plan, int32_t path) {
     double2* hist = reinterpret_cast<double2*>(env.hist);
     const double2 g = reinterpret_cast<const double2*>(env.goal)[e];
     TransOut t;
@@ -175,8 +174,6 @@ NAV_DEV TransOut transition(const nav_params& p, const nav_env_soa& env, int64_t
         if (!t.demo_term) t.r -= p.stuck_penalty;
     }
     t.done = plan == path - 1;  // robot.py:672
-    rows[2 * slot] = make_float4((float)s.x, (float)s.y, (float)a.x, (float)a.y);
-    rows[2 * slot + 1] = make_float4((float)t.r, (float)ns.x, (float)ns.y, t.done ? 1.f : 0.f);
     t.meta = (goal_reached ? M_GOAL : 0u) | (stuck_flag ? M_STUCK : 0u) | (meta & M_DEMO) |
              ((uint32_t)cnt << 8) | ((uint32_t)head << 12);
     return t;
@@ -185,6 +182,13 @@ NAV_DEV TransOut transition(const nav_params& p, const nav_env_soa& env, int64_t
 NAV_DEV uint8_t flag_byte(const TransOut& t, bool ended) {
     return (uint8_t)((t.done ? F_DONE : 0) | (t.goal_hit ? F_GOAL : 0) | (t.stuck ? F_STUCK : 0) |
                      (ended ? F_ENDED : 0) | (t.demo_term ? F_DEMO : 0));
+}
+
+// ReplayBuffer.push (robot.py:79-96) of (s, a, r, s', done) as one 32-B row.
+NAV_DEV void push_row(float4* __restrict__ rows, int64_t slot, double2 s, double2 a, double r,
+                      double2 ns, bool done) {
+    rows[2 * slot] = make_float4((float)s.x, (float)s.y, (float)a.x, (float)a.y);
+    rows[2 * slot + 1] = make_float4((float)r, (float)ns.x, (float)ns.y, done ? 1.f : 0.f);
 }
 
 // Robot.check_if_stuck alone (robot.py:509-538): history ring update + stuck verdict.
@@ -230,82 +234,14 @@ __global__ __launch_bounds__(kBlock) void k_transition(nav_params p, nav_env_soa
     const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (e >= env.n) return;
     const uint32_t meta = env.meta[e];
-    const TransOut t = transition(p, env, e, st[e], act[e], nst[e], meta, env.plan_index[e],
-                                  env.path_length[e], rows, (base + e) % cap);
+    const double2 s = st[e], a = act[e], ns = nst[e];
+    const TransOut t = transition(p, env, e, s, a, ns, meta, env.plan_index[e],
+                                  env.path_length[e]);
+    push_row(rows, (base + e) % cap, s, a, t.r, ns, t.done);
     env.meta[e] = t.meta;
     if (out.next_state) reinterpret_cast<double2*>(out.next_state)[e] = nst[e];
     if (out.goal_term) out.goal_term[e] = t.gt;
     if (out.flags) out.flags[e] = flag_byte(t, false);
-}
-
-// One training tick per env (see navenv.h nav_agent_step).
-__global__ __launch_bounds__(kBlock) void k_agent_step(nav_params p, nav_env_soa env,
-                                                       const float2* __restrict__ field,
-                                                       const double2* __restrict__ action,
-                                                       float4* __restrict__ rows, int64_t cap,
-                                                       int64_t base, nav_step_out out) {
-    const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    float st_r = 0.f, st_done = 0.f, st_goal = 0.f, st_stuck = 0.f, st_end = 0.f;
-    if (e < env.n) {
-        double2* state = reinterpret_cast<double2*>(env.state);
-        const double2 s = state[e];
-        const double2 a = action[e];
-        const uint32_t meta = env.meta[e];
-        int32_t plan = env.plan_index[e];
-        const int32_t path = env.path_length[e];
-
-        // environment.py:122-127
-        double2 ns = dynamics(field, s, a);
-        if (!in_world(ns)) ns = s;
-        TransOut t = transition(p, env, e, s, a, ns, meta, plan, path, rows, (base + e) % cap);
-
-        // next tick: robot.py:479-487 end check -> Robot.reset (492-506) + Environment.reset
-        const bool ended = t.done || (t.meta & (M_GOAL | M_STUCK));
-        if (ended) {
-            const int32_t ep = env.episodes[e] + 1;
-            env.episodes[e] = ep;
-            env.path_length[e] = path + p.path_increase;
-            env.noise_scale[e] = env.noise_scale[e] * p.noise_decay;
-            plan = 1;  // Robot.reset sets 0, the next tick's increment makes it 1
-            t.meta &= ~(M_GOAL | M_STUCK);
-            const uint4 w = philox(0u, (uint32_t)e, NAV_TAG_RESET, (uint32_t)ep, p.seed_lo,
-                                   p.seed_hi);
-            const double4 rg = reinterpret_cast<const double4*>(env.region)[e];
-            const double reg[4] = {rg.x, rg.y, rg.z, rg.w};
-            state[e] = region_sample(reg, u01(w.x, w.y), u01(w.z, w.w));
-        } else {
-            plan += 1;
-            state[e] = ns;
-        }
-        env.plan_index[e] = plan;
-        env.meta[e] = t.meta;
-        if (out.next_state) reinterpret_cast<double2*>(out.next_state)[e] = ns;
-        if (out.goal_term) out.goal_term[e] = t.gt;
-        if (out.flags) out.flags[e] = flag_byte(t, ended);
-        st_r = (float)t.r;
-        st_done = t.done ? 1.f : 0.f;
-        st_goal = t.goal_hit ? 1.f : 0.f;
-        st_stuck = t.stuck ? 1.f : 0.f;
-        st_end = ended ? 1.f : 0.f;
-    }
-    if (out.block_stats) {
-        // per-block reduction: wave shuffles -> LDS -> one 32-B row per block (deterministic)
-        __shared__ float part[kBlock / 64][5];
-        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-        const float v0 = wave_sum(st_r), v1 = wave_sum(st_done), v2 = wave_sum(st_goal);
-        const float v3 = wave_sum(st_stuck), v4 = wave_sum(st_end);
-        if (lane == 0) {
-            part[wv][0] = v0; part[wv][1] = v1; part[wv][2] = v2; part[wv][3] = v3;
-            part[wv][4] = v4;
-        }
-        __syncthreads();
-        if (threadIdx.x < 8) {
-            float acc = 0.f;
-            if (threadIdx.x < 5)
-                for (int w = 0; w < kBlock / 64; ++w) acc += part[w][threadIdx.x];
-            out.block_stats[(int64_t)blockIdx.x * 8 + threadIdx.x] = acc;
-        }
-    }
 }
 
 // robot.py:753 demo-proximity min distance, f64 exactly as scipy's cdist (dx*dx + dy*dy, no
@@ -594,30 +530,24 @@ __global__ __launch_bounds__(kBlock) void k_demo_index_fill(const double2* __res
     }
 }
 
-// The demo-proximity term through the index: lane = env, its cell = the dynamics cell of s'.
-__global__ __launch_bounds__(kBlock) void k_demo_reward_idx(nav_params p, int64_t n,
-                                                            const double2* __restrict__ ns,
-                                                            const double* __restrict__ gterm,
-                                                            const uint8_t* __restrict__ flags,
-                                                            const double2* __restrict__ demo,
-                                                            const int64_t* __restrict__ off,
-                                                            int32_t epg,
-                                                            const int64_t* __restrict__ start,
-                                                            const int32_t* __restrict__ cand,
-                                                            float* __restrict__ rows,
-                                                            int64_t cap, int64_t base,
-                                                            double* __restrict__ reward_out) {
-    const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (e >= n) return;
-    const uint8_t f = flags[e];
-    if (!(f & F_DEMO)) return;
-    const double2 s = ns[e];
-    const int64_t g = off ? e / epg : 0;
-    const double2* pts = demo + (off ? off[g] : 0);
+// The demo set of env e through the index: squared distance to the nearest demonstration point
+// of its group (robot.py:753), the candidates of the dynamics cell of s' (brute force outside the
+// indexed cells).
+struct DemoIdx {
+    const double2* demo;
+    const int64_t* off;
+    int32_t epg;
+    const int64_t* start;
+    const int32_t* cand;
+};
+
+NAV_DEV double demo_min2_idx(const DemoIdx& d, int64_t e, double2 s) {
+    const int64_t g = d.off ? e / d.epg : 0;
+    const double2* pts = d.demo + (d.off ? d.off[g] : 0);
     double best = __builtin_inf();
     if (s.x >= 0.0 && s.x < 100.0 && s.y >= 0.0 && s.y < 100.0) {
         const int64_t k = g * kCells + (int64_t)((int)s.x * NAV_WORLD_CELLS + (int)s.y);
-        const int64_t a = start[k], b = start[k + 1];
+        const int64_t a = d.start[k], b = d.start[k + 1];
         // kDemoBatch candidates per trip: their indices, then their points, are independent loads
         // (two dependent round trips per batch instead of per candidate; a wave runs as many
         // trips as its longest candidate list). Slots past the list repeat candidate a — a
@@ -628,7 +558,7 @@ __global__ __launch_bounds__(kBlock) void k_demo_reward_idx(nav_params p, int64_
         for (int64_t j = a; j < b; j += kDemoBatch) {
             int32_t c[kDemoBatch];
 #pragma unroll
-            for (int u = 0; u < kDemoBatch; ++u) c[u] = cand[j + u < b ? j + u : a];
+            for (int u = 0; u < kDemoBatch; ++u) c[u] = d.cand[j + u < b ? j + u : a];
             double2 q[kDemoBatch];
 #pragma unroll
             for (int u = 0; u < kDemoBatch; ++u) q[u] = pts[c[u]];
@@ -638,15 +568,117 @@ __global__ __launch_bounds__(kBlock) void k_demo_reward_idx(nav_params p, int64_
 #pragma unroll
         for (int u = 0; u < kDemoBatch; ++u) best = fmin(best, bu[u]);
     } else {  // outside the indexed cells: brute force
-        best = demo_min_global(pts, (off ? off[g + 1] - off[g] : 0), s.x, s.y);
+        best = demo_min_global(pts, (d.off ? d.off[g + 1] - d.off[g] : 0), s.x, s.y);
     }
-    const double mn = sqrt(best);
-    double r = gterm[e] + p.demo_factor * (-mn);
-    if (f & F_STUCK) r -= p.stuck_penalty;
+    return best;
+}
+
+// robot.py:749-757 reward of a flagged env: goal term + demo_factor * -min dist, minus the stuck
+// penalty (the order nav_demo_reward uses).
+NAV_DEV double demo_reward_of(const nav_params& p, double gterm, double min2, bool stuck) {
+    double r = gterm + p.demo_factor * (-sqrt(min2));
+    if (stuck) r -= p.stuck_penalty;
+    return r;
+}
+
+// The demo-proximity term through the index: lane = env, its cell = the dynamics cell of s'.
+__global__ __launch_bounds__(kBlock) void k_demo_reward_idx(nav_params p, int64_t n,
+                                                            const double2* __restrict__ ns,
+                                                            const double* __restrict__ gterm,
+                                                            const uint8_t* __restrict__ flags,
+                                                            DemoIdx d, float* __restrict__ rows,
+                                                            int64_t cap, int64_t base,
+                                                            double* __restrict__ reward_out) {
+    const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (e >= n) return;
+    const uint8_t f = flags[e];
+    if (!(f & F_DEMO)) return;
+    const double r = demo_reward_of(p, gterm[e], demo_min2_idx(d, e, ns[e]), (f & F_STUCK) != 0);
     const int64_t slot = (base + e) % cap;
     rows[slot * NAV_ROW + 4] = (float)r;
     if (reward_out) reward_out[e] = r;
 }
+
+// One training tick per env (see navenv.h nav_agent_step). DEMO: the demo-proximity reward of
+// flagged envs through the index in the same launch (nav_agent_step_indexed), so the replay row
+// is written once, with the final reward.
+template <bool DEMO>
+__global__ __launch_bounds__(kBlock) void k_agent_step(nav_params p, nav_env_soa env,
+                                                       const float2* __restrict__ field,
+                                                       const double2* __restrict__ action,
+                                                       float4* __restrict__ rows, int64_t cap,
+                                                       int64_t base, nav_step_out out,
+                                                       DemoIdx d, double* __restrict__ reward_out) {
+    const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    float st_r = 0.f, st_done = 0.f, st_goal = 0.f, st_stuck = 0.f, st_end = 0.f;
+    if (e < env.n) {
+        double2* state = reinterpret_cast<double2*>(env.state);
+        const double2 s = state[e];
+        const double2 a = action[e];
+        const uint32_t meta = env.meta[e];
+        int32_t plan = env.plan_index[e];
+        const int32_t path = env.path_length[e];
+
+        // environment.py:122-127
+        double2 ns = dynamics(field, s, a);
+        if (!in_world(ns)) ns = s;
+        TransOut t = transition(p, env, e, s, a, ns, meta, plan, path);
+        double r = t.r;
+        if (DEMO && t.demo_term) {
+            r = demo_reward_of(p, t.gt, demo_min2_idx(d, e, ns), t.stuck);
+            if (reward_out) reward_out[e] = r;
+        }
+        push_row(rows, (base + e) % cap, s, a, r, ns, t.done);
+
+        // next tick: robot.py:479-487 end check -> Robot.reset (492-506) + Environment.reset
+        const bool ended = t.done || (t.meta & (M_GOAL | M_STUCK));
+        if (ended) {
+            const int32_t ep = env.episodes[e] + 1;
+            env.episodes[e] = ep;
+            env.path_length[e] = path + p.path_increase;
+            env.noise_scale[e] = env.noise_scale[e] * p.noise_decay;
+            plan = 1;  // Robot.reset sets 0, the next tick's increment makes it 1
+            t.meta &= ~(M_GOAL | M_STUCK);
+            const uint4 w = philox(0u, (uint32_t)e, NAV_TAG_RESET, (uint32_t)ep, p.seed_lo,
+                                   p.seed_hi);
+            const double4 rg = reinterpret_cast<const double4*>(env.region)[e];
+            const double reg[4] = {rg.x, rg.y, rg.z, rg.w};
+            state[e] = region_sample(reg, u01(w.x, w.y), u01(w.z, w.w));
+        } else {
+            plan += 1;
+            state[e] = ns;
+        }
+        env.plan_index[e] = plan;
+        env.meta[e] = t.meta;
+        if (out.next_state) reinterpret_cast<double2*>(out.next_state)[e] = ns;
+        if (out.goal_term) out.goal_term[e] = t.gt;
+        if (out.flags) out.flags[e] = flag_byte(t, ended);
+        st_r = (float)t.r;
+        st_done = t.done ? 1.f : 0.f;
+        st_goal = t.goal_hit ? 1.f : 0.f;
+        st_stuck = t.stuck ? 1.f : 0.f;
+        st_end = ended ? 1.f : 0.f;
+    }
+    if (out.block_stats) {
+        // per-block reduction: wave shuffles -> LDS -> one 32-B row per block (deterministic)
+        __shared__ float part[kBlock / 64][5];
+        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+        const float v0 = wave_sum(st_r), v1 = wave_sum(st_done), v2 = wave_sum(st_goal);
+        const float v3 = wave_sum(st_stuck), v4 = wave_sum(st_end);
+        if (lane == 0) {
+            part[wv][0] = v0; part[wv][1] = v1; part[wv][2] = v2; part[wv][3] = v3;
+            part[wv][4] = v4;
+        }
+        __syncthreads();
+        if (threadIdx.x < 8) {
+            float acc = 0.f;
+            if (threadIdx.x < 5)
+                for (int w = 0; w < kBlock / 64; ++w) acc += part[w][threadIdx.x];
+            out.block_stats[(int64_t)blockIdx.x * 8 + threadIdx.x] = acc;
+        }
+    }
+}
+
 
 __global__ __launch_bounds__(kBlock) void k_compute_reward(nav_params p, int64_t n,
                                                            const double2* __restrict__ ns,
@@ -797,11 +829,33 @@ int nav_agent_step(const nav_params* p, const nav_env_soa* env, const float* fie
         replay->capacity <= 0 || replay_base < 0 || !out)
         return NAV_EINVAL;
     if (env->n == 0) return 0;
-    hipLaunchKernelGGL(k_agent_step, dim3(blocks_for(env->n)), dim3(kBlock), 0, S(stream), *p,
-                       *env, reinterpret_cast<const float2*>(field),
+    hipLaunchKernelGGL(k_agent_step<false>, dim3(blocks_for(env->n)), dim3(kBlock), 0,
+                       S(stream), *p, *env, reinterpret_cast<const float2*>(field),
                        reinterpret_cast<const double2*>(action),
                        reinterpret_cast<float4*>(replay->rows), replay->capacity,
-                       replay_base % replay->capacity, *out);
+                       replay_base % replay->capacity, *out, DemoIdx{}, nullptr);
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_agent_step_indexed(const nav_params* p, const nav_env_soa* env, const float* field,
+                           const double* action, const nav_replay* replay, int64_t replay_base,
+                           const nav_step_out* out, const double* demo_xy,
+                           const int64_t* demo_off, int32_t envs_per_group,
+                           const int64_t* cell_start, const int32_t* cand, double* reward_out,
+                           void* stream) {
+    if (!p || !env_ok(env) || !field || !action || !replay || !replay->rows ||
+        replay->capacity <= 0 || replay_base < 0 || !out || (demo_off && envs_per_group <= 0))
+        return NAV_EINVAL;
+    if (env->n == 0) return 0;
+    if (!demo_xy || !cell_start || !cand) return NAV_EINVAL;
+    const DemoIdx d{reinterpret_cast<const double2*>(demo_xy), demo_off,
+                    envs_per_group > 0 ? envs_per_group : 1, cell_start, cand};
+    hipLaunchKernelGGL(k_agent_step<true>, dim3(blocks_for(env->n)), dim3(kBlock), 0,
+                       S(stream), *p, *env, reinterpret_cast<const float2*>(field),
+                       reinterpret_cast<const double2*>(action),
+                       reinterpret_cast<float4*>(replay->rows), replay->capacity,
+                       replay_base % replay->capacity, *out, d, reward_out);
     NAV_CHECK_LAUNCH();
     return 0;
 }
@@ -946,11 +1000,12 @@ int nav_demo_reward_indexed(const nav_params* p, int64_t n, const double* next_s
     if (n == 0) return 0;
     if (!next_state || !goal_term || !flags || !demo_xy || !cell_start || !cand)
         return NAV_EINVAL;
+    const DemoIdx d{reinterpret_cast<const double2*>(demo_xy), demo_off,
+                    envs_per_group > 0 ? envs_per_group : 1, cell_start, cand};
     hipLaunchKernelGGL(k_demo_reward_idx, dim3(blocks_for(n)), dim3(kBlock), 0, S(stream), *p,
-                       n, reinterpret_cast<const double2*>(next_state), goal_term, flags,
-                       reinterpret_cast<const double2*>(demo_xy), demo_off,
-                       envs_per_group > 0 ? envs_per_group : 1, cell_start, cand, replay->rows,
-                       replay->capacity, replay_base % replay->capacity, reward_out);
+                       n, reinterpret_cast<const double2*>(next_state), goal_term, flags, d,
+                       replay->rows, replay->capacity, replay_base % replay->capacity,
+                       reward_out);
     NAV_CHECK_LAUNCH();
     return 0;
 }

@@ -13,7 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # NAV_LIB: load another build of the same ABI instead (A/B timing of kernel variants only)
 LIB_PATH = os.environ.get("NAV_LIB") or os.path.join(HERE, "libnavenv.so")
 NAV_EINVAL = -100000
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 _dp = C.POINTER(C.c_double)
 _vp = C.c_void_p
@@ -81,6 +81,9 @@ SIGNATURES = [
     ("nav_demo_reward_indexed", C.c_int, [_P(NavParams), C.c_int64, _vp, _vp, _vp, _vp, _vp,
                                           C.c_int32, _vp, _vp, _P(NavReplay), C.c_int64, _vp,
                                           _vp]),
+    ("nav_agent_step_indexed", C.c_int, [_P(NavParams), _P(NavEnvSoa), _vp, _vp, _P(NavReplay),
+                                         C.c_int64, _P(NavStepOut), _vp, _vp, C.c_int32, _vp,
+                                         _vp, _vp, _vp]),
     ("nav_demo_min", C.c_int, [_vp, C.c_int64, _vp, C.c_int64, _vp, _vp]),
     ("nav_compute_reward", C.c_int, [_P(NavParams), C.c_int64, _vp, _vp, _vp, C.c_int64,
                                      C.c_int32, _vp, _vp, _vp]),

@@ -4,6 +4,7 @@
 gfx950 kernels of libnavenv.so through the C-ABI. One env = one lane; n envs advance per launch.
 """
 import ctypes as C
+import os
 
 import torch
 
@@ -106,6 +107,9 @@ class VecEnv:
         self.demo_xy = None
         self.demo_off = None
         self.demo_index = None
+        # demo reward fused into the tick launch (nav_agent_step_indexed); NAV_FUSE_DEMO=0 keeps
+        # the two launches (A/B and the fused-vs-unfused parity test)
+        self.fuse_demo = os.environ.get("NAV_FUSE_DEMO", "1") != "0"
         if init:
             self.init(demo_flag)
 
@@ -147,6 +151,16 @@ class VecEnv:
         base = replay.position
         s = stream_handle(stream)
         rd = replay.desc()
+        ix = self.demo_index if (self.demo_xy is not None and self.demo_xy.shape[0] > 0) else None
+        if ix is not None and self.fuse_demo:
+            # one launch: tick + indexed demo reward (bit-identical to the two-launch path)
+            with prof.region("agent_step", float(prof.AGENT_STEP_BYTES * self.n)):
+                lib().nav_agent_step_indexed(
+                    C.byref(self.p), C.byref(self.soa), ptr(self.field), ptr(action), C.byref(rd),
+                    base, C.byref(self.out), ptr(self.demo_xy), ptr(self.demo_off),
+                    self.envs_per_group, ptr(ix.cell_start), ptr(ix.cand), ptr(reward_out), s)
+            replay.advance(self.n)
+            return base
         with prof.region("agent_step", float(prof.AGENT_STEP_BYTES * self.n)):
             lib().nav_agent_step(C.byref(self.p), C.byref(self.soa), ptr(self.field),
                                  ptr(action), C.byref(rd), base, C.byref(self.out), s)

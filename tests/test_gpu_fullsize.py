@@ -85,3 +85,32 @@ def test_bench_config_invariants(trainer):
     assert (np.abs(rows[:, 2:4]) <= 5.0).all()          # stored actions are clipped
     for net in tr.td3.networks().values():
         assert torch.isfinite(net.params).all()
+
+
+def test_fused_demo_reward_is_bit_identical():
+    """nav_agent_step_indexed (tick + demo reward in one launch) vs nav_agent_step followed by
+    nav_demo_reward_indexed: same replay rows, env state, rewards and learner, bit for bit."""
+    from nav.trainer import VecTrainer
+    runs = []
+    for fused in (True, False):
+        tr = VecTrainer(n_envs=8192, hidden=256, n_hidden=2, batch=4096, updates_per_step=2,
+                        envs_per_group=1024, device=DEV)
+        tr.env.fuse_demo = fused
+        rewards = []
+        for _ in range(5):
+            tr.act()
+            r = torch.full((tr.n,), float("nan"), dtype=torch.float64, device=DEV)
+            tr.env.agent_step(tr.action, tr.replay, reward_out=r)
+            tr.steps += 1
+            tr.learn()
+            rewards.append(r)
+        torch.cuda.synchronize()
+        runs.append((tr, torch.stack(rewards)))
+    (a, ra), (b, rb) = runs
+    assert torch.equal(a.replay.rows, b.replay.rows)
+    assert torch.equal(a.env.state, b.env.state)
+    assert torch.equal(a.env.flags, b.env.flags)
+    assert torch.equal(ra.isnan(), rb.isnan()) and torch.equal(ra.nan_to_num(), rb.nan_to_num())
+    assert (~ra.isnan()).any()  # some envs took the demo term
+    for k, net in a.td3.networks().items():
+        assert torch.equal(net.params, b.td3.networks()[k].params), k
