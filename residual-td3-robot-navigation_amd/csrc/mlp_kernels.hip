@@ -1157,7 +1157,7 @@ constexpr int WG_MC = 32;   // rows per staged chunk
 constexpr int WA_W = 128;   // tile width
 constexpr int WA_LD = 132;  // LDS row stride of the 128-column panels
 #ifndef WG_STAGE0
-#define WG_STAGE0 8         // first MFMA step that stages the next chunk (its loads land first)
+#define WG_STAGE0 6         // first MFMA step that stages the next chunk (A/B r01r: 6 over 4, 8)
 #endif
 
 inline size_t wgrad_lds_bytes() { return (size_t)2 * 2 * WG_MC * WA_LD * 4; }

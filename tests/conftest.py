@@ -31,3 +31,11 @@ def orc():
     from oracle import oracle
     oracle.build()
     return oracle
+
+
+@pytest.fixture(autouse=True)
+def _seeded_torch():
+    """Every test draws its unseeded torch inputs from the same stream: reproducible runs."""
+    import torch
+    torch.manual_seed(0)
+    yield
