@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define NAV_ABI_VERSION 4
+#define NAV_ABI_VERSION 5
 #define NAV_EINVAL (-100000)
 
 #define NAV_WORLD_CELLS 100 /* field = float32 [100][100][2] (speed, angle), x-major: cell cx*100+cy
@@ -77,8 +77,9 @@ typedef struct nav_step_out {
     double* next_state;   /* [n][2] next state BEFORE any auto-reset (Environment.step return) */
     double* goal_term;    /* [n] -||s'-goal|| (robot.py:741), consumed by nav_demo_reward      */
     uint8_t* flags;       /* [n] bit0 done, bit1 goal, bit2 stuck, bit3 ended, bit4 demo term  */
-    float* block_stats;   /* nullable: [gridDim][8] = sum reward, n_done, n_goal, n_stuck,
-                             n_ended, 0, 0, 0 (wave shuffles -> LDS, one row per block)       */
+    float* block_stats;   /* nullable: [ceil(n/64)][8], row k = envs [64k, 64k+64): sum reward
+                             (w/o demo term), n_done, n_goal, n_stuck, n_ended, 0, 0, 0
+                             (one wave's shuffle tree per row: deterministic)                 */
 } nav_step_out;
 
 /* Replay ring (device): rows [capacity][8] float32 (robot.py:58-124 ReplayBuffer). */
@@ -128,6 +129,11 @@ int nav_env_reset(const nav_params* p, const nav_env_soa* env, const uint8_t* ma
  * result is inside the world. action [n][2] f64. next_state (nullable) receives the result. */
 int nav_env_step(const nav_params* p, const nav_env_soa* env, const float* field,
                  const double* action, double* next_state, void* stream);
+/* environment.py:122-127 Environment.step applied K times in one launch (the pure-step loop of
+ * robot-learning.py's tick without the agent): the state stays in registers; actions [K][n][2] f64;
+ * next_states (nullable) [K][n][2] receives each step's committed state. */
+int nav_env_step_k(const nav_params* p, const nav_env_soa* env, const float* field,
+                   const double* actions, int32_t K, double* next_states, void* stream);
 /* environment.py:98-119 Environment.dynamics, pure: out = f(state, action), n pairs. */
 int nav_dynamics(const float* field, const double* state, const double* action, double* out,
                  int64_t n, void* stream);
@@ -136,16 +142,23 @@ int nav_dynamics(const float* field, const double* state, const double* action, 
 /* One training tick for every env, fused: Environment.step (environment.py:122-127) ->
  * Robot.process_transition (robot.py:645-675: reward w/o demo term, check_if_stuck, done, push
  * to the replay row (replay_base + e) % capacity) -> next tick's end-of-episode check and
- * Robot.reset + Environment.reset (robot.py:479-506, environment.py:130-137). */
+ * Robot.reset + Environment.reset (robot.py:479-506, environment.py:130-137).
+ * demo_pending != 0: the caller runs nav_demo_reward(_indexed) next for the envs flagged
+ * (flags bit4) — their demo-proximity term and stuck penalty are written then; 0: no demo set
+ * exists, so (robot.py:749-751) the reward is the goal term and the stuck penalty is taken here.
+ * replay->capacity must be >= n (one slot per env per launch). */
 int nav_agent_step(const nav_params* p, const nav_env_soa* env, const float* field,
                    const double* action, const nav_replay* replay,
-                   int64_t replay_base, const nav_step_out* out, void* stream);
+                   int64_t replay_base, const nav_step_out* out, int32_t demo_pending,
+                   void* stream);
 /* Robot.process_transition (robot.py:645-675) without the environment step, for callers that
  * step the Environment themselves (the N = 1 drop-in): reward w/o demo term, check_if_stuck,
- * done, replay push; meta/hist updated, plan_index/path_length read (not advanced). */
+ * done, replay push; meta/hist updated, plan_index/path_length read (not advanced).
+ * demo_pending as nav_agent_step. */
 int nav_transition(const nav_params* p, const nav_env_soa* env, const double* state,
                    const double* action, const double* next_state, const nav_replay* replay,
-                   int64_t replay_base, const nav_step_out* out, void* stream);
+                   int64_t replay_base, const nav_step_out* out, int32_t demo_pending,
+                   void* stream);
 /* Robot.check_if_stuck (robot.py:509-538) alone: updates the history ring (hist, meta bits
  * 8-14) with `state` [n][2] and writes stuck [n] (0/1). */
 int nav_check_if_stuck(const nav_params* p, const nav_env_soa* env, const double* state,
@@ -319,6 +332,18 @@ int nav_grad_reduce_adam(const nav_mlp* nets, int32_t n_nets, const float* const
                          float* const* grads, float* const* m, float* const* v, float beta1,
                          float beta2, float eps, const float* step_size, const float* bc2_sqrt,
                          void* stream);
+/* nav_grad_reduce of 1 or 2 same-shape networks in one launch (the twin critics' gradients into
+ * one contiguous bucket for the shared-policy all-reduce). */
+int nav_grad_reduce_multi(const nav_mlp* nets, int32_t n_nets, const float* const* hidden_slabs,
+                          int32_t splits, const float* const* edge_slabs, int64_t edge_blocks,
+                          float* const* grads, void* stream);
+/* nav_adam of 1 or 2 networks in one launch on gradients g / grad_div (shared policy, BASELINE
+ * config 5: the bucket holds the SUM over ranks after the all-reduce, grad_div = world size, as
+ * torch DDP's averaging; grad_div 1 = the plain step, bit-identical to nav_adam). step_size and
+ * bc2_sqrt are host arrays [n_nets]. */
+int nav_adam_multi(const nav_mlp* nets, int32_t n_nets, const float* const* grads,
+                   float* const* m, float* const* v, float beta1, float beta2, float eps,
+                   const float* step_size, const float* bc2_sqrt, float grad_div, void* stream);
 /* torch.optim.Adam step (robot.py:236-239; torch 2.10 single-tensor semantics) on a flat buffer,
  * step_size = lr/(1-b1^t), bc2_sqrt = sqrt(1-b2^t) precomputed by the caller; refreshes `packed`
  * of `net` (net->params must equal params). */

@@ -4,14 +4,11 @@
 // wave shuffles and LDS.
 #include <stdlib.h>
 
-#include "nav_device.h"
+#include "nav_tick.h"
 
 using namespace nav;
 
 namespace {
-
-constexpr uint32_t M_GOAL = 1u, M_STUCK = 2u, M_DEMO = 4u;
-constexpr uint8_t F_DONE = 1, F_GOAL = 2, F_STUCK = 4, F_ENDED = 8, F_DEMO = 16;
 
 NAV_DEV void region_of(int r, double u, double* reg) {
     // environment.py:29-49 (left, right, bottom, top)
@@ -118,79 +115,6 @@ __global__ __launch_bounds__(kBlock) void k_dynamics(int64_t n, const float2* __
     out[e] = dynamics(field, s[e], a[e]);
 }
 
-// Robot.process_transition (robot.py:645-675) for env e given (s, a, s'): reward without the
-// demo term (robot.py:727-762; the term is added by nav_demo_reward for flagged envs),
-// check_if_stuck on the pre-step state (robot.py:509-538, ring of 5 in hist [5][n]), done, and
-// ReplayBuffer.push (robot.py:79-96) as one 32-B row. Returns the updated meta word.
-struct TransOut {
-    double r, gt;
-    bool goal_hit, demo_term, stuck, done;
-    uint32_t meta;
-};
-
-NAV_DEV TransOut transition(const nav_params& p, const nav_env_soa& env, int64_t e, double2 s,
-                            double2 a, double2 ns, uint32_t meta, int32_t plan, int32_t path) {
-    double2* hist = reinterpret_cast<double2*>(env.hist);
-    const double2 g = reinterpret_cast<const double2*>(env.goal)[e];
-    TransOut t;
-    bool goal_reached = (meta & M_GOAL) != 0;
-    t.gt = -norm2(ns.x - g.x, ns.y - g.y);
-    t.goal_hit = t.gt >= -p.goal_threshold;
-    t.demo_term = false;
-    if (t.goal_hit) {
-        goal_reached = true;
-        t.r = p.goal_reward;
-    } else {
-        t.r = t.gt;
-        t.demo_term = (meta & M_DEMO) != 0;
-    }
-    int cnt = (int)((meta >> 8) & 7u), head = (int)((meta >> 12) & 7u);
-    t.stuck = false;
-    if (cnt >= NAV_HIST) {
-        bool all = true;
-#pragma unroll
-        for (int k = 0; k < NAV_HIST; ++k) {
-            const double2 h = hist[(int64_t)k * env.n + e];
-            const double d = norm2(s.x - h.x, s.y - h.y);
-            all = all && (d < p.stuck_threshold);
-        }
-        if (all) {
-            t.stuck = true;
-            cnt = 0;
-        } else {
-            head = head == NAV_HIST - 1 ? 0 : head + 1;
-            cnt -= 1;
-        }
-    }
-    {
-        int sl = head + cnt;
-        if (sl >= NAV_HIST) sl -= NAV_HIST;
-        hist[(int64_t)sl * env.n + e] = s;
-        cnt += 1;
-    }
-    bool stuck_flag = (meta & M_STUCK) != 0;
-    if (t.stuck) {
-        stuck_flag = true;
-        if (!t.demo_term) t.r -= p.stuck_penalty;
-    }
-    t.done = plan == path - 1;  // robot.py:672
-    t.meta = (goal_reached ? M_GOAL : 0u) | (stuck_flag ? M_STUCK : 0u) | (meta & M_DEMO) |
-             ((uint32_t)cnt << 8) | ((uint32_t)head << 12);
-    return t;
-}
-
-NAV_DEV uint8_t flag_byte(const TransOut& t, bool ended) {
-    return (uint8_t)((t.done ? F_DONE : 0) | (t.goal_hit ? F_GOAL : 0) | (t.stuck ? F_STUCK : 0) |
-                     (ended ? F_ENDED : 0) | (t.demo_term ? F_DEMO : 0));
-}
-
-// ReplayBuffer.push (robot.py:79-96) of (s, a, r, s', done) as one 32-B row.
-NAV_DEV void push_row(float4* __restrict__ rows, int64_t slot, double2 s, double2 a, double r,
-                      double2 ns, bool done) {
-    rows[2 * slot] = make_float4((float)s.x, (float)s.y, (float)a.x, (float)a.y);
-    rows[2 * slot + 1] = make_float4((float)r, (float)ns.x, (float)ns.y, done ? 1.f : 0.f);
-}
-
 // Robot.check_if_stuck alone (robot.py:509-538): history ring update + stuck verdict.
 __global__ __launch_bounds__(kBlock) void k_check_if_stuck(nav_params p, nav_env_soa env,
                                                            const double2* __restrict__ st,
@@ -230,13 +154,14 @@ __global__ __launch_bounds__(kBlock) void k_transition(nav_params p, nav_env_soa
                                                        const double2* __restrict__ act,
                                                        const double2* __restrict__ nst,
                                                        float4* __restrict__ rows, int64_t cap,
-                                                       int64_t base, nav_step_out out) {
+                                                       int64_t base, nav_step_out out,
+                                                       int32_t demo_pending) {
     const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (e >= env.n) return;
     const uint32_t meta = env.meta[e];
     const double2 s = st[e], a = act[e], ns = nst[e];
     const TransOut t = transition(p, env, e, s, a, ns, meta, env.plan_index[e],
-                                  env.path_length[e]);
+                                  env.path_length[e], demo_pending != 0);
     push_row(rows, (base + e) % cap, s, a, t.r, ns, t.done);
     env.meta[e] = t.meta;
     if (out.next_state) reinterpret_cast<double2*>(out.next_state)[e] = nst[e];
@@ -253,27 +178,7 @@ __global__ __launch_bounds__(kBlock) void k_transition(nav_params p, nav_env_soa
 // latency), combined through LDS.
 constexpr int kDemoEnvs = 64;
 constexpr int kDemoSplit = 8;
-#ifndef NAV_DEMO_BATCH
-#define NAV_DEMO_BATCH 16
-#endif
-constexpr int kDemoBatch = NAV_DEMO_BATCH;  // candidates per dependent-load trip (indexed reward)
 constexpr int kDemoBlock = kDemoEnvs * kDemoSplit;
-
-NAV_DEV double demo_min_global(const double2* __restrict__ d, int64_t m, double x, double y) {
-    double best = __builtin_inf();
-    for (int64_t j = 0; j < m; ++j) {
-        const double2 q = d[j];
-        const double dx = x - q.x, dy = y - q.y;
-        const double v = dx * dx + dy * dy;
-        best = v < best ? v : best;
-    }
-    return best;
-}
-
-NAV_DEV double sqd(double x, double y, double px, double py) {
-    const double dx = x - px, dy = y - py;
-    return dx * dx + dy * dy;
-}
 
 NAV_DEV double demo_min_uniform(const double* __restrict__ d, int m, double x, double y) {
     double b0 = __builtin_inf(), b1 = b0, b2 = b0, b3 = b0;
@@ -401,8 +306,6 @@ __global__ __launch_bounds__(kBlock) void k_demo_min(const double2* __restrict__
 // The candidate list of C = { p : mindist^2(p, C) <= U^2 (1 + 1e-12) + 1e-12 } contains p* for
 // every query in C; the kernel then takes the same f64 minimum over it as over all points, so the
 // result is bit-identical to the brute force (tests/test_gpu_env.py checks it).
-constexpr int kCells = NAV_WORLD_CELLS * NAV_WORLD_CELLS;
-
 NAV_DEV double cell_maxd2(double px, double py, double lx, double ly) {
     const double fx = fmax(fabs(px - lx), fabs(px - (lx + 1.0)));
     const double fy = fmax(fabs(py - ly), fabs(py - (ly + 1.0)));
@@ -530,57 +433,6 @@ __global__ __launch_bounds__(kBlock) void k_demo_index_fill(const double2* __res
     }
 }
 
-// The demo set of env e through the index: squared distance to the nearest demonstration point
-// of its group (robot.py:753), the candidates of the dynamics cell of s' (brute force outside the
-// indexed cells).
-struct DemoIdx {
-    const double2* demo;
-    const int64_t* off;
-    int32_t epg;
-    const int64_t* start;
-    const int32_t* cand;
-};
-
-NAV_DEV double demo_min2_idx(const DemoIdx& d, int64_t e, double2 s) {
-    const int64_t g = d.off ? e / d.epg : 0;
-    const double2* pts = d.demo + (d.off ? d.off[g] : 0);
-    double best = __builtin_inf();
-    if (s.x >= 0.0 && s.x < 100.0 && s.y >= 0.0 && s.y < 100.0) {
-        const int64_t k = g * kCells + (int64_t)((int)s.x * NAV_WORLD_CELLS + (int)s.y);
-        const int64_t a = d.start[k], b = d.start[k + 1];
-        // kDemoBatch candidates per trip: their indices, then their points, are independent loads
-        // (two dependent round trips per batch instead of per candidate; a wave runs as many
-        // trips as its longest candidate list). Slots past the list repeat candidate a — a
-        // duplicate cannot change a min, so the result is the same bits as one by one.
-        double bu[kDemoBatch];
-#pragma unroll
-        for (int u = 0; u < kDemoBatch; ++u) bu[u] = __builtin_inf();
-        for (int64_t j = a; j < b; j += kDemoBatch) {
-            int32_t c[kDemoBatch];
-#pragma unroll
-            for (int u = 0; u < kDemoBatch; ++u) c[u] = d.cand[j + u < b ? j + u : a];
-            double2 q[kDemoBatch];
-#pragma unroll
-            for (int u = 0; u < kDemoBatch; ++u) q[u] = pts[c[u]];
-#pragma unroll
-            for (int u = 0; u < kDemoBatch; ++u) bu[u] = fmin(bu[u], sqd(s.x, s.y, q[u].x, q[u].y));
-        }
-#pragma unroll
-        for (int u = 0; u < kDemoBatch; ++u) best = fmin(best, bu[u]);
-    } else {  // outside the indexed cells: brute force
-        best = demo_min_global(pts, (d.off ? d.off[g + 1] - d.off[g] : 0), s.x, s.y);
-    }
-    return best;
-}
-
-// robot.py:749-757 reward of a flagged env: goal term + demo_factor * -min dist, minus the stuck
-// penalty (the order nav_demo_reward uses).
-NAV_DEV double demo_reward_of(const nav_params& p, double gterm, double min2, bool stuck) {
-    double r = gterm + p.demo_factor * (-sqrt(min2));
-    if (stuck) r -= p.stuck_penalty;
-    return r;
-}
-
 // The demo-proximity term through the index: lane = env, its cell = the dynamics cell of s'.
 __global__ __launch_bounds__(kBlock) void k_demo_reward_idx(nav_params p, int64_t n,
                                                             const double2* __restrict__ ns,
@@ -601,84 +453,45 @@ __global__ __launch_bounds__(kBlock) void k_demo_reward_idx(nav_params p, int64_
 
 // One training tick per env (see navenv.h nav_agent_step). DEMO: the demo-proximity reward of
 // flagged envs through the index in the same launch (nav_agent_step_indexed), so the replay row
-// is written once, with the final reward.
+// is written once, with the final reward. One statistics row per wave (64 envs).
 template <bool DEMO>
 __global__ __launch_bounds__(kBlock) void k_agent_step(nav_params p, nav_env_soa env,
                                                        const float2* __restrict__ field,
                                                        const double2* __restrict__ action,
                                                        float4* __restrict__ rows, int64_t cap,
                                                        int64_t base, nav_step_out out,
-                                                       DemoIdx d, double* __restrict__ reward_out) {
+                                                       DemoIdx d, int32_t demo_pending,
+                                                       double* __restrict__ reward_out) {
     const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    float st_r = 0.f, st_done = 0.f, st_goal = 0.f, st_stuck = 0.f, st_end = 0.f;
-    if (e < env.n) {
-        double2* state = reinterpret_cast<double2*>(env.state);
-        const double2 s = state[e];
-        const double2 a = action[e];
-        const uint32_t meta = env.meta[e];
-        int32_t plan = env.plan_index[e];
-        const int32_t path = env.path_length[e];
-
-        // environment.py:122-127
-        double2 ns = dynamics(field, s, a);
-        if (!in_world(ns)) ns = s;
-        TransOut t = transition(p, env, e, s, a, ns, meta, plan, path);
-        double r = t.r;
-        if (DEMO && t.demo_term) {
-            r = demo_reward_of(p, t.gt, demo_min2_idx(d, e, ns), t.stuck);
-            if (reward_out) reward_out[e] = r;
-        }
-        push_row(rows, (base + e) % cap, s, a, r, ns, t.done);
-
-        // next tick: robot.py:479-487 end check -> Robot.reset (492-506) + Environment.reset
-        const bool ended = t.done || (t.meta & (M_GOAL | M_STUCK));
-        if (ended) {
-            const int32_t ep = env.episodes[e] + 1;
-            env.episodes[e] = ep;
-            env.path_length[e] = path + p.path_increase;
-            env.noise_scale[e] = env.noise_scale[e] * p.noise_decay;
-            plan = 1;  // Robot.reset sets 0, the next tick's increment makes it 1
-            t.meta &= ~(M_GOAL | M_STUCK);
-            const uint4 w = philox(0u, (uint32_t)e, NAV_TAG_RESET, (uint32_t)ep, p.seed_lo,
-                                   p.seed_hi);
-            const double4 rg = reinterpret_cast<const double4*>(env.region)[e];
-            const double reg[4] = {rg.x, rg.y, rg.z, rg.w};
-            state[e] = region_sample(reg, u01(w.x, w.y), u01(w.z, w.w));
-        } else {
-            plan += 1;
-            state[e] = ns;
-        }
-        env.plan_index[e] = plan;
-        env.meta[e] = t.meta;
-        if (out.next_state) reinterpret_cast<double2*>(out.next_state)[e] = ns;
-        if (out.goal_term) out.goal_term[e] = t.gt;
-        if (out.flags) out.flags[e] = flag_byte(t, ended);
-        st_r = (float)t.r;
-        st_done = t.done ? 1.f : 0.f;
-        st_goal = t.goal_hit ? 1.f : 0.f;
-        st_stuck = t.stuck ? 1.f : 0.f;
-        st_end = ended ? 1.f : 0.f;
-    }
-    if (out.block_stats) {
-        // per-block reduction: wave shuffles -> LDS -> one 32-B row per block (deterministic)
-        __shared__ float part[kBlock / 64][5];
-        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-        const float v0 = wave_sum(st_r), v1 = wave_sum(st_done), v2 = wave_sum(st_goal);
-        const float v3 = wave_sum(st_stuck), v4 = wave_sum(st_end);
-        if (lane == 0) {
-            part[wv][0] = v0; part[wv][1] = v1; part[wv][2] = v2; part[wv][3] = v3;
-            part[wv][4] = v4;
-        }
-        __syncthreads();
-        if (threadIdx.x < 8) {
-            float acc = 0.f;
-            if (threadIdx.x < 5)
-                for (int w = 0; w < kBlock / 64; ++w) acc += part[w][threadIdx.x];
-            out.block_stats[(int64_t)blockIdx.x * 8 + threadIdx.x] = acc;
-        }
-    }
+    TickStats st{0.f, 0.f, 0.f, 0.f, 0.f};
+    if (e < env.n)
+        st = agent_tick<DEMO>(p, env, field, e, action[e], rows, cap, base, out, d,
+                              demo_pending != 0, reward_out);
+    if (out.block_stats && e - (threadIdx.x & 63) < env.n) wave_stats(st, out.block_stats, e);
 }
 
+// Environment.step for K consecutive steps per launch (environment.py:122-127 applied K times):
+// the state stays in registers, actions [K][n][2] stream in, next_out (nullable) [K][n][2]
+// receives every step's committed state. Bytes per env-step 16 (+16 with next_out) + 32/K.
+__global__ __launch_bounds__(kBlock) void k_env_step_k(int64_t n, int32_t K,
+                                                       double2* __restrict__ state,
+                                                       const float2* __restrict__ field,
+                                                       const double2* __restrict__ action,
+                                                       double2* __restrict__ next_out) {
+    const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (e >= n) return;
+    double2 s = state[e];
+    double2 a = action[e];
+    for (int32_t k = 0; k < K; ++k) {
+        // the next step's action is in flight under this step's dynamics
+        const double2 an = k + 1 < K ? action[(int64_t)(k + 1) * n + e] : a;
+        const double2 nx = dynamics(field, s, a);
+        if (in_world(nx)) s = nx;
+        if (next_out) next_out[(int64_t)k * n + e] = s;
+        a = an;
+    }
+    state[e] = s;
+}
 
 __global__ __launch_bounds__(kBlock) void k_compute_reward(nav_params p, int64_t n,
                                                            const double2* __restrict__ ns,
@@ -810,6 +623,21 @@ int nav_env_step(const nav_params* p, const nav_env_soa* env, const float* field
     return 0;
 }
 
+int nav_env_step_k(const nav_params* p, const nav_env_soa* env, const float* field,
+                   const double* actions, int32_t K, double* next_states, void* stream) {
+    if (!p || !env || env->n < 0 || K < 0 || !field ||
+        (env->n && K && (!env->state || !actions)))
+        return NAV_EINVAL;
+    if (env->n == 0 || K == 0) return 0;
+    hipLaunchKernelGGL(k_env_step_k, dim3(blocks_for(env->n)), dim3(kBlock), 0, S(stream),
+                       env->n, K, reinterpret_cast<double2*>(env->state),
+                       reinterpret_cast<const float2*>(field),
+                       reinterpret_cast<const double2*>(actions),
+                       reinterpret_cast<double2*>(next_states));
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
 int nav_dynamics(const float* field, const double* state, const double* action, double* out,
                  int64_t n, void* stream) {
     if (n < 0 || (n && (!field || !state || !action || !out))) return NAV_EINVAL;
@@ -824,16 +652,17 @@ int nav_dynamics(const float* field, const double* state, const double* action, 
 
 int nav_agent_step(const nav_params* p, const nav_env_soa* env, const float* field,
                    const double* action, const nav_replay* replay, int64_t replay_base,
-                   const nav_step_out* out, void* stream) {
+                   const nav_step_out* out, int32_t demo_pending, void* stream) {
+    // one slot per env per launch: a ring smaller than n would let two envs write one slot
     if (!p || !env_ok(env) || !field || !action || !replay || !replay->rows ||
-        replay->capacity <= 0 || replay_base < 0 || !out)
+        replay->capacity < env->n || replay->capacity <= 0 || replay_base < 0 || !out)
         return NAV_EINVAL;
     if (env->n == 0) return 0;
     hipLaunchKernelGGL(k_agent_step<false>, dim3(blocks_for(env->n)), dim3(kBlock), 0,
                        S(stream), *p, *env, reinterpret_cast<const float2*>(field),
                        reinterpret_cast<const double2*>(action),
                        reinterpret_cast<float4*>(replay->rows), replay->capacity,
-                       replay_base % replay->capacity, *out, DemoIdx{}, nullptr);
+                       replay_base % replay->capacity, *out, DemoIdx{}, demo_pending, nullptr);
     NAV_CHECK_LAUNCH();
     return 0;
 }
@@ -845,7 +674,8 @@ int nav_agent_step_indexed(const nav_params* p, const nav_env_soa* env, const fl
                            const int64_t* cell_start, const int32_t* cand, double* reward_out,
                            void* stream) {
     if (!p || !env_ok(env) || !field || !action || !replay || !replay->rows ||
-        replay->capacity <= 0 || replay_base < 0 || !out || (demo_off && envs_per_group <= 0))
+        replay->capacity < env->n || replay->capacity <= 0 || replay_base < 0 || !out ||
+        (demo_off && envs_per_group <= 0))
         return NAV_EINVAL;
     if (env->n == 0) return 0;
     if (!demo_xy || !cell_start || !cand) return NAV_EINVAL;
@@ -855,16 +685,17 @@ int nav_agent_step_indexed(const nav_params* p, const nav_env_soa* env, const fl
                        S(stream), *p, *env, reinterpret_cast<const float2*>(field),
                        reinterpret_cast<const double2*>(action),
                        reinterpret_cast<float4*>(replay->rows), replay->capacity,
-                       replay_base % replay->capacity, *out, d, reward_out);
+                       replay_base % replay->capacity, *out, d, 1, reward_out);
     NAV_CHECK_LAUNCH();
     return 0;
 }
 
 int nav_transition(const nav_params* p, const nav_env_soa* env, const double* state,
                    const double* action, const double* next_state, const nav_replay* replay,
-                   int64_t replay_base, const nav_step_out* out, void* stream) {
-    if (!p || !env || env->n < 0 || !replay || !replay->rows || replay->capacity <= 0 ||
-        replay_base < 0 || !out)
+                   int64_t replay_base, const nav_step_out* out, int32_t demo_pending,
+                   void* stream) {
+    if (!p || !env || env->n < 0 || !replay || !replay->rows || replay->capacity < env->n ||
+        replay->capacity <= 0 || replay_base < 0 || !out)
         return NAV_EINVAL;
     if (env->n == 0) return 0;
     if (!env->goal || !env->hist || !env->meta || !env->plan_index || !env->path_length ||
@@ -875,7 +706,7 @@ int nav_transition(const nav_params* p, const nav_env_soa* env, const double* st
                        reinterpret_cast<const double2*>(action),
                        reinterpret_cast<const double2*>(next_state),
                        reinterpret_cast<float4*>(replay->rows), replay->capacity,
-                       replay_base % replay->capacity, *out);
+                       replay_base % replay->capacity, *out, demo_pending);
     NAV_CHECK_LAUNCH();
     return 0;
 }

@@ -1570,6 +1570,42 @@ __global__ __launch_bounds__(kBlock) void k_adam(float4* __restrict__ p,
     }
 }
 
+// torch.optim.Adam of up to 2 networks in one launch from flat gradients that a collective
+// produced (shared policy: the SUM all-reduce of the bucket); g / grad_div is the averaged
+// gradient (grad_div 1: the plain step, bit-identical to k_adam).
+struct AdamNet {
+    float4* p;
+    const float4* g;
+    float4* m;
+    float4* v;
+    int64_t n4;
+    float step_size, bc2s;
+    PackInfo pk;
+};
+struct AdamArgs {
+    AdamNet q[2];
+    int n;
+    int64_t total4;
+    float b1w, b2, omb2, eps, gdiv;
+};
+
+__global__ __launch_bounds__(kBlock) void k_adam_multi(AdamArgs a) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < a.total4;
+         i += (int64_t)gridDim.x * kBlock) {
+        const bool second = a.n > 1 && i >= a.q[0].n4;
+        const AdamNet& q = second ? a.q[1] : a.q[0];
+        const int64_t j = second ? i - a.q[0].n4 : i;
+        float4 pp = q.p[j], gg = q.g[j], mm = q.m[j], vv = q.v[j];
+        gg.x = gg.x / a.gdiv; gg.y = gg.y / a.gdiv; gg.z = gg.z / a.gdiv; gg.w = gg.w / a.gdiv;
+        adam1(pp.x, gg.x, mm.x, vv.x, a.b1w, a.b2, a.omb2, a.eps, q.step_size, q.bc2s);
+        adam1(pp.y, gg.y, mm.y, vv.y, a.b1w, a.b2, a.omb2, a.eps, q.step_size, q.bc2s);
+        adam1(pp.z, gg.z, mm.z, vv.z, a.b1w, a.b2, a.omb2, a.eps, q.step_size, q.bc2s);
+        adam1(pp.w, gg.w, mm.w, vv.w, a.b1w, a.b2, a.omb2, a.eps, q.step_size, q.bc2s);
+        q.p[j] = pp; q.m[j] = mm; q.v[j] = vv;
+        if (q.pk.packed) repack(q.pk, j * 4, pp);
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void k_polyak(float4* __restrict__ t,
                                                    const float4* __restrict__ s, int64_t n4,
                                                    float omt, float tau, PackInfo pk) {
@@ -2170,6 +2206,63 @@ int nav_grad_reduce(const nav_mlp* net, const float* hidden_slabs, int32_t split
     a.nblk = edge_blocks;
     hipLaunchKernelGGL(k_grad_reduce<false>, dim3((unsigned)(a.n[0].nbh + a.n[0].nbe)),
                        dim3(kBlock), 0, S(stream), a);
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_grad_reduce_multi(const nav_mlp* nets, int32_t n_nets, const float* const* hidden_slabs,
+                          int32_t splits, const float* const* edge_slabs, int64_t edge_blocks,
+                          float* const* grads, void* stream) {
+    RedArgs a{};
+    if (!nets || n_nets < 1 || n_nets > 2 || !hidden_slabs || !edge_slabs || edge_blocks < 1 ||
+        splits < 0 || !grads)
+        return NAV_EINVAL;
+    int blocks = 0;
+    for (int i = 0; i < n_nets; ++i) {
+        if (!edge_slabs[i] || !grads[i] ||
+            !red_net(&nets[i], hidden_slabs[i], splits, edge_slabs[i], grads[i], &a.n[i]))
+            return NAV_EINVAL;
+        if (a.n[i].net.hp != a.n[0].net.hp || a.n[i].net.n_hidden != a.n[0].net.n_hidden)
+            return NAV_EINVAL;
+        blocks += a.n[i].nbh + a.n[i].nbe;
+    }
+    a.splits = splits;
+    a.nblk = edge_blocks;
+    hipLaunchKernelGGL(k_grad_reduce<false>, dim3((unsigned)blocks), dim3(kBlock), 0, S(stream),
+                       a);
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_adam_multi(const nav_mlp* nets, int32_t n_nets, const float* const* grads,
+                   float* const* m, float* const* v, float beta1, float beta2, float eps,
+                   const float* step_size, const float* bc2_sqrt, float grad_div, void* stream) {
+    AdamArgs a{};
+    if (!nets || n_nets < 1 || n_nets > 2 || !grads || !m || !v || !step_size || !bc2_sqrt ||
+        !(grad_div > 0.f))
+        return NAV_EINVAL;
+    for (int i = 0; i < n_nets; ++i) {
+        MlpDev d;
+        if (!make_dev(&nets[i], &d) || !grads[i] || !m[i] || !v[i]) return NAV_EINVAL;
+        AdamNet& q = a.q[i];
+        q.p = reinterpret_cast<float4*>(nets[i].params);
+        q.g = reinterpret_cast<const float4*>(grads[i]);
+        q.m = reinterpret_cast<float4*>(m[i]);
+        q.v = reinterpret_cast<float4*>(v[i]);
+        q.n4 = d.count / 4;
+        q.step_size = step_size[i];
+        q.bc2s = bc2_sqrt[i];
+        q.pk = pack_info(d, nets[i].packed);
+        a.total4 += q.n4;
+    }
+    a.n = n_nets;
+    a.b1w = 1.0f - beta1;
+    a.b2 = beta2;
+    a.omb2 = 1.0f - beta2;
+    a.eps = eps;
+    a.gdiv = grad_div;
+    hipLaunchKernelGGL(k_adam_multi, dim3(grid_stride_blocks(a.total4)), dim3(kBlock), 0,
+                       S(stream), a);
     NAV_CHECK_LAUNCH();
     return 0;
 }

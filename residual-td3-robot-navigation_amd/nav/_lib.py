@@ -13,7 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # NAV_LIB: load another build of the same ABI instead (A/B timing of kernel variants only)
 LIB_PATH = os.environ.get("NAV_LIB") or os.path.join(HERE, "libnavenv.so")
 NAV_EINVAL = -100000
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 _dp = C.POINTER(C.c_double)
 _vp = C.c_void_p
@@ -65,12 +65,13 @@ SIGNATURES = [
     ("nav_env_reset", C.c_int, [_P(NavParams), _P(NavEnvSoa), _vp, _vp, _vp]),
     ("nav_env_step", C.c_int, [_P(NavParams), _P(NavEnvSoa), _vp, _vp, _vp, _vp]),
     ("nav_dynamics", C.c_int, [_vp, _vp, _vp, _vp, C.c_int64, _vp]),
+    ("nav_env_step_k", C.c_int, [_P(NavParams), _P(NavEnvSoa), _vp, _vp, C.c_int32, _vp, _vp]),
     ("nav_agent_step", C.c_int, [_P(NavParams), _P(NavEnvSoa), _vp, _vp, _P(NavReplay),
-                                 C.c_int64, _P(NavStepOut), _vp]),
+                                 C.c_int64, _P(NavStepOut), C.c_int32, _vp]),
     ("nav_demo_reward", C.c_int, [_P(NavParams), C.c_int64, _vp, _vp, _vp, _vp, _vp, C.c_int64,
                                   C.c_int32, _P(NavReplay), C.c_int64, _vp, _vp]),
     ("nav_transition", C.c_int, [_P(NavParams), _P(NavEnvSoa), _vp, _vp, _vp, _P(NavReplay),
-                                 C.c_int64, _P(NavStepOut), _vp]),
+                                 C.c_int64, _P(NavStepOut), C.c_int32, _vp]),
     ("nav_check_if_stuck", C.c_int, [_P(NavParams), _P(NavEnvSoa), _vp, _vp, _vp]),
     ("nav_rollout", C.c_int, [_vp, C.c_int64, C.c_int32, _vp, _vp, _vp, _vp, _vp, _vp]),
     ("nav_replay_push", C.c_int, [_P(NavReplay), C.c_int64, C.c_int64, _vp, _vp, _vp, _vp, _vp,
@@ -119,6 +120,11 @@ SIGNATURES = [
     ("nav_grad_reduce_adam", C.c_int, [_P(NavMlp), C.c_int32, _P(_vp), C.c_int32, _P(_vp),
                                        C.c_int64, _P(_vp), _P(_vp), _P(_vp), C.c_float, C.c_float,
                                        C.c_float, _P(C.c_float), _P(C.c_float), _vp]),
+    ("nav_grad_reduce_multi", C.c_int, [_P(NavMlp), C.c_int32, _P(_vp), C.c_int32, _P(_vp),
+                                        C.c_int64, _P(_vp), _vp]),
+    ("nav_adam_multi", C.c_int, [_P(NavMlp), C.c_int32, _P(_vp), _P(_vp), _P(_vp), C.c_float,
+                                 C.c_float, C.c_float, _P(C.c_float), _P(C.c_float), C.c_float,
+                                 _vp]),
     ("nav_adam", C.c_int, [_P(NavMlp), _vp, _vp, _vp, C.c_float, C.c_float, C.c_float,
                            C.c_float, C.c_float, _vp]),
     ("nav_polyak", C.c_int, [_P(NavMlp), _P(NavMlp), C.c_float, _vp]),

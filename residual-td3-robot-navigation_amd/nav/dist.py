@@ -3,7 +3,8 @@ gloo on CPU for tests).
 
 Envs are independent, so the vectorised path shards as independent env blocks (seed + rank) with
 no data-path collective. A shared policy (BASELINE config 5) adds exactly one collective: the
-all-reduce of each flat gradient buffer before the (redundant, bit-identical) optimizer steps.
+SUM all-reduce of each flat gradient bucket (twin critics as one bucket per epoch, the actor's on
+policy epochs) before the redundant, bit-identical optimizer steps.
 """
 import os
 
@@ -22,17 +23,30 @@ def shard_seed(base_seed, rank):
     return int(base_seed) + int(rank)
 
 
+class GradAllReduce:
+    """Shared-policy gradient exchange (BASELINE config 5): ONE in-place SUM all-reduce per flat
+    gradient bucket (RCCL over xGMI for GPU tensors, gloo for CPU tensors). The learner divides
+    by `world_size` inside its Adam launch (nav_adam_multi's grad_div), as torch DDP's average.
+    Every rank receives the same bytes, so the redundant Adam / Polyak steps keep the ranks'
+    parameters bit-identical."""
+
+    def __init__(self, world_size, group=None):
+        self.world_size = int(world_size)
+        self.group = group
+        self.calls = 0
+        self.bytes = 0
+
+    def __call__(self, bucket):
+        dist.all_reduce(bucket, op=dist.ReduceOp.SUM, group=self.group)
+        self.calls += 1
+        self.bytes += bucket.numel() * bucket.element_size()
+
+
 def make_grad_hook(world_size, group=None):
-    """Shared-policy gradient averaging: sum over ranks (RCCL ring over xGMI for GPU tensors),
-    then / world_size. Deterministic reduction order per backend, identical on every rank."""
+    """The learner's grad_hook for a shared policy over `world_size` ranks (None for one)."""
     if world_size <= 1:
         return None
-
-    def hook(g):
-        dist.all_reduce(g, op=dist.ReduceOp.SUM, group=group)
-        g.div_(world_size)
-
-    return hook
+    return GradAllReduce(world_size, group)
 
 
 def broadcast_params(tensors, src=0, group=None):

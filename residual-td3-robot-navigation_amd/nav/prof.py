@@ -22,6 +22,12 @@ ENV_STEP_BYTES = 48
 AGENT_STEP_BYTES = 237
 
 
+def env_step_k_bytes(K, with_next):
+    """nav_env_step_k per env-step: the action (16), each step's state out (16) if kept, and the
+    state read + written once per launch (32 / K)."""
+    return 16.0 + (16.0 if with_next else 0.0) + 32.0 / K
+
+
 def mlp_fwd_flops(d_in, d_out, h, nh, rows):
     return 2.0 * rows * (d_in * h + (nh - 1) * h * h + h * d_out)
 

@@ -267,10 +267,11 @@ class Robot:
         rd = self.memory.desc()
         base = self.memory.position
         s = stream_handle()
+        has_demo = self._demo.shape[0] > 0
         lib().nav_transition(C.byref(self._p), C.byref(self._soa), ptr(self._sas[0]),
                              ptr(self._sas[1]), ptr(self._sas[2]), C.byref(rd), base,
-                             C.byref(self._out), s)
-        if self._demo.shape[0] > 0:
+                             C.byref(self._out), int(has_demo), s)
+        if has_demo:
             lib().nav_demo_reward(C.byref(self._p), 1, ptr(self._ns_out), ptr(self._gterm),
                                   ptr(self._flags), ptr(self._demo), None, self._demo.shape[0],
                                   1, C.byref(rd), base, None, s)
@@ -287,6 +288,9 @@ class Robot:
         self.augment_demonstration_data(demonstration_states, demonstration_actions)
         self.draw_path(demonstration_states, colour=[0, 255, 0], width=2)
         n = len(demonstration_states) - 1
+        if n < 1:  # a 1-state demonstration has no transition: the reference pushes nothing
+            self.goal_reached = False
+            return
         ds = np.asarray(demonstration_states, np.float64)
         rewards = self._compute_rewards(ds[1:n + 1])
         done = np.zeros(n, np.uint8)

@@ -6,9 +6,10 @@ provides the stream. Sampling: robot.py:98-115 draws `batch_size` rows without r
 <=10 000-row buffer; here rows are drawn with replacement by Philox (NAV_TAG_SAMPLE) from the
 device ring, or taken from an injected index tensor (parity tests, the N=1 drop-in).
 """
+import contextlib
 import ctypes as C
-import os
 import math
+import os
 
 import torch
 
@@ -68,7 +69,10 @@ class TD3:
         self.critic_optimizer_2 = _Adam(self.critic_network_2, c.critic_lr)
         self.seed = seed
         self.update_counter = 0  # Philox counter for sampling / smoothing noise
-        self.grad_hook = grad_hook  # e.g. RCCL all-reduce of flat grads (shared policy)
+        # shared policy (BASELINE config 5): grad_hook(bucket) SUM-all-reduces a flat gradient
+        # bucket in place (nav.dist.GradAllReduce: RCCL over xGMI); Adam divides by grad_div
+        self.grad_hook = grad_hook
+        self.grad_div = float(getattr(grad_hook, "world_size", 1)) if grad_hook else 1.0
         # train_critic's row backward inside the critic_rows launch (NAV_CRITIC_ROW_BWD=0: its
         # own launch; tuning / A/B only)
         self.row_backward = os.environ.get("NAV_CRITIC_ROW_BWD", "1") != "0"
@@ -109,42 +113,64 @@ class TD3:
         hc = max(4, L.nav_mlp_hidden_count(hp, nh))
         self.hslab, self.hslab2 = f(max(sc, sa), hc), f(sc, hc)
         self.grad_a = f(self.actor_network.count)
-        self.grad_c1 = f(self.critic_network_1.count)
-        self.grad_c2 = f(self.critic_network_1.count)
+        # the twin critics' flat gradients as ONE contiguous bucket (one all-reduce per epoch)
+        cc = self.critic_network_1.count
+        self.grad_c = f(2 * cc)
+        self.grad_c1, self.grad_c2 = self.grad_c[:cc], self.grad_c[cc:]
         self._B = B
 
-    def _grads_and_step(self, nets, opts, M, inp, ld_in, in_col, acts, dz, dy, ld_dy, masks,
-                        eslabs, grads, hslabs, s, stream):
-        """Hidden weight gradients of 1-2 same-shape nets (one MFMA launch, split-M slabs), then
-        the fixed-order reduce of those and the fwd/bwd edge partials fused with each net's Adam
-        step (robot.py:236-239). With a grad_hook (shared policy: RCCL all-reduce) the reduce
-        writes the flat gradients, the hook runs, then Adam steps separately."""
-        n = len(nets)
+    def _wgrad(self, nets, M, inp, ld_in, in_col, acts, dz, dy, ld_dy, masks, hslabs, s):
+        """Hidden x hidden weight gradients of 1-2 same-shape nets: one MFMA launch writing
+        `splits` partial slabs per net."""
         net = nets[0]
         splits = self.splits_a if net is self.actor_network else self.splits_c
         if net.n_hidden > 1:
-            with prof.region("mlp_wgrad", n * prof.mlp_wgrad_flops(net.hidden, net.n_hidden, M)):
-                lib().nav_mlp_wgrad(descs(*nets), n, M, ptr(inp), ld_in, in_col, parr(*acts),
-                                    parr(*dz), parr(*dy), ld_dy, parr(*masks), parr(*hslabs),
-                                    splits, s)
-        nbytes = sum(4.0 * (splits * (x.count - e.shape[1]) + e.numel() + 3 * x.count)
-                     for x, e in zip(nets, eslabs))
+            with prof.region("mlp_wgrad", len(nets) * prof.mlp_wgrad_flops(net.hidden,
+                                                                           net.n_hidden, M)):
+                lib().nav_mlp_wgrad(descs(*nets), len(nets), M, ptr(inp), ld_in, in_col,
+                                    parr(*acts), parr(*dz), parr(*dy), ld_dy, parr(*masks),
+                                    parr(*hslabs), splits, s)
+        return splits
+
+    def _reduce_bytes(self, nets, eslabs, splits, adam):
+        return sum(4.0 * (splits * (x.count - e.shape[1]) + e.numel() +
+                          (4 if adam else 1) * x.count) for x, e in zip(nets, eslabs))
+
+    def _grads_and_step(self, nets, opts, M, inp, ld_in, in_col, acts, dz, dy, ld_dy, masks,
+                        eslabs, grads, hslabs, s, stream):
+        """Weight gradients, then the fixed-order reduce of those and the fwd/bwd edge partials
+        fused with each net's Adam step (robot.py:236-239): 2 launches for 1-2 nets. With a
+        grad_hook (shared policy) the reduce writes the flat gradient bucket, the hook
+        all-reduces it, and one multi-net Adam launch applies bucket / world_size."""
+        splits = self._wgrad(nets, M, inp, ld_in, in_col, acts, dz, dy, ld_dy, masks, hslabs, s)
         if self.grad_hook is None:
             coeffs = [o.advance() for o in opts]
-            with prof.region("grad_reduce", nbytes):
+            with prof.region("grad_reduce", self._reduce_bytes(nets, eslabs, splits, True)):
                 lib().nav_grad_reduce_adam(
-                    descs(*nets), n, parr(*hslabs), splits, parr(*eslabs), self.nblk,
+                    descs(*nets), len(nets), parr(*hslabs), splits, parr(*eslabs), self.nblk,
                     parr(*grads), parr(*[o.m for o in opts]), parr(*[o.v for o in opts]),
                     opts[0].b1, opts[0].b2, opts[0].eps,
-                    (C.c_float * n)(*[c[0] for c in coeffs]), (C.c_float * n)(*[c[1] for c in coeffs]),
-                    s)
+                    (C.c_float * len(nets))(*[c[0] for c in coeffs]),
+                    (C.c_float * len(nets))(*[c[1] for c in coeffs]), s)
             return
-        for x, o, h, e, g in zip(nets, opts, hslabs, eslabs, grads):
-            with prof.region("grad_reduce", nbytes / n):
-                lib().nav_grad_reduce(C.byref(x.desc()), ptr(h), splits, ptr(e), self.nblk,
-                                      ptr(g), s)
-            self.grad_hook(g)
-            o.step(g, stream)
+        with prof.region("grad_reduce", self._reduce_bytes(nets, eslabs, splits, False)):
+            lib().nav_grad_reduce_multi(descs(*nets), len(nets), parr(*hslabs), splits,
+                                        parr(*eslabs), self.nblk, parr(*grads), s)
+        bucket = self.grad_c if len(nets) == 2 else grads[0]
+        # the collective runs on torch's current stream: make it the launch stream, so it
+        # starts after the reduce and Adam starts after it
+        with torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext():
+            self.grad_hook(bucket)
+        self._adam(nets, opts, grads, s, self.grad_div)
+
+    def _adam(self, nets, opts, grads, s, grad_div=1.0):
+        """One multi-net Adam launch on flat gradients (already reduced) / grad_div."""
+        coeffs = [o.advance() for o in opts]
+        n = len(nets)
+        lib().nav_adam_multi(descs(*nets), n, parr(*grads), parr(*[o.m for o in opts]),
+                             parr(*[o.v for o in opts]), opts[0].b1, opts[0].b2, opts[0].eps,
+                             (C.c_float * n)(*[c[0] for c in coeffs]),
+                             (C.c_float * n)(*[c[1] for c in coeffs]), float(grad_div), s)
 
     def _bwd(self, nets, M, dy, ld_dy, masks, s, inp=None, ld_in=0, in_col=0, h_top=None,
              dz=None, save_mask=0, dx=None, eslab=None):
@@ -160,11 +186,10 @@ class TD3:
                                    save_mask, parr(*(dx or nil)), parr(*(eslab or nil)), s)
 
     # robot.py:312-366
-    def train_critic(self, replay, idx=None, eps=None, stream=None):
+    def _critic_rows(self, replay, idx, eps, s):
         c = self.cfg
         B = c.batch_size
         self._workspace(B)
-        s = stream_handle(stream)
         c1, c2 = self.critic_network_1, self.critic_network_2
         mid = c1.middle_layers()
         rd = replay.desc()
@@ -185,17 +210,44 @@ class TD3:
                 parr(self.eslab1, self.eslab2), parr(self.acts1, self.acts2), mid,
                 parr(self.mask1, self.mask2), int(self.row_backward), parr(self.dz1, self.dz2),
                 mid, s)
-        bt = self.batch
-        crit, opts = [c1, c2], [self.critic_optimizer_1, self.critic_optimizer_2]
         if not self.row_backward:  # separate backward launch (A/B of the fusion)
-            self._bwd(crit, B, [self.dq1, self.dq2], 1, [self.mask1, self.mask2], s, inp=bt,
-                      ld_in=8, in_col=0, dz=[self.dz1, self.dz2], save_mask=mid,
+            self._bwd([c1, c2], B, [self.dq1, self.dq2], 1, [self.mask1, self.mask2], s,
+                      inp=self.batch, ld_in=8, in_col=0, dz=[self.dz1, self.dz2], save_mask=mid,
                       eslab=[self.eslab1, self.eslab2])
-        # both critics' weight gradients and reduce + Adam: one launch each
-        self._grads_and_step(crit, opts, B, bt, 8, 0, [self.acts1, self.acts2],
-                             [self.dz1, self.dz2], [self.dq1, self.dq2], 1,
-                             [self.mask1, self.mask2], [self.eslab1, self.eslab2],
+
+    def _critic_wgrad_args(self):
+        return (self.batch, 8, 0, [self.acts1, self.acts2], [self.dz1, self.dz2],
+                [self.dq1, self.dq2], 1, [self.mask1, self.mask2])
+
+    def train_critic(self, replay, idx=None, eps=None, stream=None):
+        s = stream_handle(stream)
+        self._critic_rows(replay, idx, eps, s)
+        c1, c2 = self.critic_network_1, self.critic_network_2
+        B = self.cfg.batch_size
+        # both critics' weight gradients, then reduce + Adam: one launch each
+        self._grads_and_step([c1, c2], [self.critic_optimizer_1, self.critic_optimizer_2], B,
+                             *self._critic_wgrad_args(), [self.eslab1, self.eslab2],
                              [self.grad_c1, self.grad_c2], [self.hslab, self.hslab2], s, stream)
+
+    def critic_gradients(self, replay, idx=None, eps=None, stream=None):
+        """train_critic's gradient phase alone: both critics' flat gradients into the `grad_c`
+        bucket ([critic 1 | critic 2], contiguous), no parameter changes. With critic_step this
+        is train_critic's shared-policy path split where the collective goes."""
+        s = stream_handle(stream)
+        self._critic_rows(replay, idx, eps, s)
+        c1, c2 = self.critic_network_1, self.critic_network_2
+        splits = self._wgrad([c1, c2], self.cfg.batch_size, *self._critic_wgrad_args(),
+                             [self.hslab, self.hslab2], s)
+        lib().nav_grad_reduce_multi(descs(c1, c2), 2, parr(self.hslab, self.hslab2), splits,
+                                    parr(self.eslab1, self.eslab2), self.nblk,
+                                    parr(self.grad_c1, self.grad_c2), s)
+        return self.grad_c
+
+    def critic_step(self, grad_div=1.0, stream=None):
+        """Adam on both critics from the `grad_c` bucket / grad_div (one launch)."""
+        self._adam([self.critic_network_1, self.critic_network_2],
+                   [self.critic_optimizer_1, self.critic_optimizer_2],
+                   [self.grad_c1, self.grad_c2], stream_handle(stream), grad_div)
 
     def critic_loss_values(self):
         """(loss1, loss2) of the last train_critic (mean squared TD error), synchronising."""
@@ -203,11 +255,10 @@ class TD3:
         return t[0].item(), t[1].item()
 
     # robot.py:369-398
-    def train_actor(self, replay, idx=None, stream=None):
+    def _actor_rows(self, replay, idx, s):
         c = self.cfg
         B = c.batch_size
         self._workspace(B)
-        s = stream_handle(stream)
         net = self.actor_network
         c1 = self.critic_network_1
         rd = replay.desc()
@@ -224,9 +275,31 @@ class TD3:
                 ptr(self.batch2), ptr(self.q1), ptr(self.da), ptr(self.acts_a),
                 net.middle_layers(), ptr(self.dz_a), net.middle_layers(),
                 ptr(self.mask_a), ptr(self.mask1), ptr(self.eslab_a), s)
-        self._grads_and_step([net], [self.actor_optimizer], B, self.batch2, 8, 0, [self.acts_a],
-                             [self.dz_a], [self.da], 2, [self.mask_a], [self.eslab_a],
-                             [self.grad_a], [self.hslab], s, stream)
+
+    def _actor_wgrad_args(self):
+        return (self.batch2, 8, 0, [self.acts_a], [self.dz_a], [self.da], 2, [self.mask_a])
+
+    def train_actor(self, replay, idx=None, stream=None):
+        s = stream_handle(stream)
+        self._actor_rows(replay, idx, s)
+        self._grads_and_step([self.actor_network], [self.actor_optimizer], self.cfg.batch_size,
+                             *self._actor_wgrad_args(), [self.eslab_a], [self.grad_a],
+                             [self.hslab], s, stream)
+
+    def actor_gradients(self, replay, idx=None, stream=None):
+        """train_actor's gradient phase alone: the actor's flat gradient into `grad_a`."""
+        s = stream_handle(stream)
+        self._actor_rows(replay, idx, s)
+        net = self.actor_network
+        splits = self._wgrad([net], self.cfg.batch_size, *self._actor_wgrad_args(),
+                             [self.hslab], s)
+        lib().nav_grad_reduce_multi(descs(net), 1, parr(self.hslab), splits,
+                                    parr(self.eslab_a), self.nblk, parr(self.grad_a), s)
+        return self.grad_a
+
+    def actor_step(self, grad_div=1.0, stream=None):
+        self._adam([self.actor_network], [self.actor_optimizer], [self.grad_a],
+                   stream_handle(stream), grad_div)
 
     def actor_loss_value(self):
         return -(self.q1.sum() / self._B).item()

@@ -97,7 +97,7 @@ class VecEnv:
         self.next_state = torch.zeros(n, 2, dtype=f64, device=d)
         self.goal_term = torch.zeros(n, dtype=f64, device=d)
         self.flags = torch.zeros(n, dtype=torch.uint8, device=d)
-        self.block_stats = torch.zeros((n + 255) // 256, 8, dtype=torch.float32, device=d)
+        self.block_stats = torch.zeros((n + 63) // 64, 8, dtype=torch.float32, device=d)
         self.goal_draws = torch.zeros(n, dtype=i32, device=d)
         self.soa = NavEnvSoa(n, *[t.data_ptr() for t in (
             self.state, self.goal, self.region, self.hist, self.meta, self.plan_index,
@@ -131,6 +131,16 @@ class VecEnv:
                                ptr(next_state), stream_handle(stream))
         return self.state
 
+    # environment.py:122-127 applied K times in one launch (state in registers)
+    def step_k(self, actions, next_states=None, stream=None):
+        K = actions.shape[0]
+        assert actions.shape == (K, self.n, 2) and actions.is_contiguous()
+        with prof.region("env_step_k", float(prof.env_step_k_bytes(K, next_states is not None)
+                                             * self.n)):
+            lib().nav_env_step_k(C.byref(self.p), C.byref(self.soa), ptr(self.field),
+                                 ptr(actions), K, ptr(next_states), stream_handle(stream))
+        return self.state
+
     def dynamics(self, state, action, out=None, stream=None):
         out = out if out is not None else torch.empty_like(state)
         lib().nav_dynamics(ptr(self.field), ptr(state), ptr(action), ptr(out), state.shape[0],
@@ -161,10 +171,12 @@ class VecEnv:
                     self.envs_per_group, ptr(ix.cell_start), ptr(ix.cand), ptr(reward_out), s)
             replay.advance(self.n)
             return base
+        has_demo = self.demo_xy is not None and self.demo_xy.shape[0] > 0
         with prof.region("agent_step", float(prof.AGENT_STEP_BYTES * self.n)):
             lib().nav_agent_step(C.byref(self.p), C.byref(self.soa), ptr(self.field),
-                                 ptr(action), C.byref(rd), base, C.byref(self.out), s)
-        if self.demo_xy is not None and self.demo_xy.shape[0] > 0:
+                                 ptr(action), C.byref(rd), base, C.byref(self.out),
+                                 int(has_demo), s)
+        if has_demo:
             m = self.demo_xy.shape[0] if self.demo_off is None else 0
             m_per = self.demo_xy.shape[0] if self.demo_off is None else \
                 self.demo_xy.shape[0] / max(1, self.demo_off.shape[0] - 1)

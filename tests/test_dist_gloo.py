@@ -45,9 +45,32 @@ def _worker_shard(rank, ws, port, q):
     dist.destroy_process_group()
 
 
+def _bucket_step(net, opt, X, Y, hook):
+    """One shared-policy step the way nav.td3 takes it: every gradient of the net into ONE flat
+    bucket, the hook's SUM all-reduce, then Adam on bucket / world_size (nav_adam_multi's
+    grad_div)."""
+    ts = net.tensors()
+    for t in ts:
+        t.requires_grad_(True)
+    loss = torch.nn.functional.mse_loss(net.forward(X), Y)
+    grads = torch.autograd.grad(loss, ts)
+    for t in ts:
+        t.requires_grad_(False)
+    bucket = torch.cat([g.reshape(-1) for g in grads])
+    div = 1.0
+    if hook is not None:
+        hook(bucket)
+        div = float(hook.world_size)
+    parts, o = [], 0
+    for g in grads:
+        parts.append((bucket[o:o + g.numel()] / div).view_as(g))
+        o += g.numel()
+    opt.step(parts)
+
+
 def _worker_shared_policy(rank, ws, port, q):
     _init(rank, ws, port)
-    from nav.dist import broadcast_params, make_grad_hook
+    from nav.dist import GradAllReduce, broadcast_params, make_grad_hook
     from oracle.td3_oracle import MLP, Adam, make_mlp_params
     torch.manual_seed(100 + rank)  # ranks start different: broadcast must fix that
     net = MLP(make_mlp_params(5 + rank, [4, 64, 64, 1]))
@@ -55,25 +78,17 @@ def _worker_shared_policy(rank, ws, port, q):
     rng = np.random.default_rng(7)
     X = torch.tensor(rng.standard_normal((64, 4)), dtype=torch.float32)
     Y = torch.tensor(rng.standard_normal((64, 1)), dtype=torch.float32)
-    half = slice(rank * 32, (rank + 1) * 32)  # stratified: each rank its local half
+    half = slice(rank * 32, (rank + 1) * 32)  # per-rank batch B / world: each rank its half
     hook = make_grad_hook(ws)
+    assert isinstance(hook, GradAllReduce) and hook.world_size == ws
     opt = Adam(net.tensors(), 1e-3)
     for _ in range(3):
-        ts = net.tensors()
-        for t in ts:
-            t.requires_grad_(True)
-        loss = torch.nn.functional.mse_loss(net.forward(X[half]), Y[half])
-        grads = [g.contiguous() for g in torch.autograd.grad(loss, ts)]
-        for t in ts:
-            t.requires_grad_(False)
-        for g in grads:
-            hook(g)
-        opt.step(grads)
+        _bucket_step(net, opt, X[half], Y[half], hook)
     flat = torch.cat([t.reshape(-1) for t in net.tensors()])
     out = [torch.zeros_like(flat) for _ in range(ws)]
     dist.all_gather(out, flat)
     if rank == 0:
-        q.put([o.numpy() for o in out])
+        q.put(([o.numpy() for o in out], hook.calls, hook.bytes))
     dist.destroy_process_group()
 
 
@@ -104,8 +119,10 @@ def test_independent_env_blocks_world2():
 
 def test_shared_policy_allreduce_equals_full_batch_world2():
     from oracle.td3_oracle import MLP, Adam, make_mlp_params
-    flats = _spawn(_worker_shared_policy)
+    flats, calls, nbytes = _spawn(_worker_shared_policy)
     np.testing.assert_array_equal(flats[0], flats[1])  # ranks stay bit-identical
+    n_params = flats[0].size
+    assert calls == 3 and nbytes == 3 * 4 * n_params  # one bucket message per step
     # single process, full batch of 64 = mean of the two 32-row halves' gradients
     net = MLP(make_mlp_params(5, [4, 64, 64, 1]))
     rng = np.random.default_rng(7)
@@ -113,13 +130,6 @@ def test_shared_policy_allreduce_equals_full_batch_world2():
     Y = torch.tensor(rng.standard_normal((64, 1)), dtype=torch.float32)
     opt = Adam(net.tensors(), 1e-3)
     for _ in range(3):
-        ts = net.tensors()
-        for t in ts:
-            t.requires_grad_(True)
-        loss = torch.nn.functional.mse_loss(net.forward(X), Y)
-        grads = torch.autograd.grad(loss, ts)
-        for t in ts:
-            t.requires_grad_(False)
-        opt.step(grads)
+        _bucket_step(net, opt, X, Y, None)
     flat = torch.cat([t.reshape(-1) for t in net.tensors()]).numpy()
     np.testing.assert_allclose(flats[0], flat, rtol=0, atol=1e-6)

@@ -94,6 +94,67 @@ def test_env_step_full_size_nontemporal_path(nav):
     torch.cuda.empty_cache()
 
 
+def test_env_step_k_equals_k_single_steps(nav):
+    """nav_env_step_k (K steps, state in registers) == K nav_env_step launches, bit for bit,
+    golden cases as starting states and random / NaN / out-of-range actions per step."""
+    from nav.vec_env import VecEnv
+    g = golden("dynamics.npz")
+    f = field_of(g["speed"], g["angle"])
+    n, K = len(g["state"]), 9
+    rng = np.random.default_rng(4)
+    acts = rng.uniform(-7, 7, (K, n, 2))
+    acts[3, ::17] = np.nan
+    a = torch.tensor(acts, device=DEV)
+    one = VecEnv(n, f, init=False)
+    many = VecEnv(n, f, init=False)
+    for e in (one, many):
+        e.state.copy_(torch.tensor(g["state"], device=DEV))
+    nxt = torch.zeros(K, n, 2, dtype=torch.float64, device=DEV)
+    many.step_k(a, next_states=nxt)
+    for k in range(K):
+        one.step(a[k].contiguous())
+        assert torch.equal(nxt[k], one.state), k
+    assert torch.equal(many.state, one.state)
+    many.step_k(a)  # without the per-step output
+    for k in range(K):
+        one.step(a[k].contiguous())
+    assert torch.equal(many.state, one.state)
+
+
+def test_demo_flag_without_demo_set_keeps_stuck_penalty(nav, orc):
+    """demo_flag set but no demonstration set — the reference's compute_reward returns
+    the goal term (robot.py:749-751) and process_transition still subtracts the stuck penalty
+    (robot.py:667-669). Motionless envs get stuck after 5 ticks; rows vs the oracle tick."""
+    from nav.vec_env import ReplayRing, VecEnv
+    from oracle.oracle import VecAgentState, default_params
+    g = golden("trace.npz")
+    n = 300
+    env = VecEnv(n, field_of(g["speed"], g["angle"]), seed=17, envs_per_group=1,
+                 demo_flag=True)
+    assert (env.meta.cpu().numpy() & 4).all()
+    rep = ReplayRing(n, DEV)
+    p = default_params(17)
+    ost = VecAgentState(n)
+    rng = np.random.default_rng(2)
+    stuck_seen = 0
+    for t in range(8):
+        a = rng.uniform(-1e-3, 1e-3, (n, 2))
+        a[n // 2:] = rng.uniform(-5, 5, (n - n // 2, 2))
+        _sync_oracle(env, ost)
+        base = rep.position
+        env.agent_step(torch.tensor(a, device=DEV), rep)
+        torch.cuda.synchronize()
+        rows = rep.rows.cpu().numpy()
+        fl = env.flags.cpu().numpy()
+        assert not (fl & 16).any()  # no demo term is pending without a demo set
+        for e in range(n):
+            flo, ns, row, r = ost.tick(p, g["speed"], g["angle"], np.zeros((0, 2)), e, a[e])
+            assert (flo & 15) == (fl[e] & 15), (t, e)
+            assert np.allclose(row, rows[(base + e) % rep.capacity], rtol=1e-6, atol=1e-5), (t, e)
+        stuck_seen += int(((fl & 4) != 0).sum())
+    assert stuck_seen > 0
+
+
 def test_empty_launches_are_noops(nav):
     from nav import _lib
     from nav.vec_env import VecEnv

@@ -56,7 +56,7 @@ def test_gfx950_code_object_present(navlib):
 def test_abi_and_layout(navlib):
     from nav.mlp import layer_offsets
     from nav._lib import NavMlp
-    assert navlib.nav_abi_version() == 4
+    assert navlib.nav_abi_version() == 5
     for d_in, d_out, hidden, nh in ((2, 2, 200, 3), (4, 1, 200, 3), (2, 2, 256, 2),
                                     (4, 1, 256, 2), (4, 1, 32, 1)):
         hp = (hidden + 31) // 32 * 32
