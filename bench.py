@@ -58,7 +58,7 @@ def pmc_traffic(region):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--envs", type=int, default=65536)
     ap.add_argument("--hidden", type=int, default=256)
@@ -70,6 +70,9 @@ def parse():
     ap.add_argument("--shared-policy", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sweep", action="store_true")
+    ap.add_argument("--no-utd-sweep", action="store_true")
+    ap.add_argument("--long-steps", type=int, default=200,
+                    help="extra event-free timed run of this many steps (extra key timed_long)")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--breakdown", action="store_true", help="print the per-kernel table")
     ap.add_argument("--presleep", type=int, default=0,
@@ -132,24 +135,82 @@ def step_kernel_sweep(field, sizes, reps=20):
     return out
 
 
+def cpu_info():
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return model, os.cpu_count()
+
+
 def cpu_baseline(args, trainer):
-    from oracle.cpu_loop import CPUPort, time_port
+    """The oracle CPU port of the same workload (C OpenMP tick with the same exact demo index as
+    the GPU, torch-CPU fp32 TD3), bounded sample; plus the single-env one-core C rates."""
+    from oracle.cpu_loop import CPUPort, single_env_rates, time_port
     from oracle import oracle as O
-    from nav.fields import make_fields
     n = args.envs
-    speed, angle = make_fields(args.seed)
+    fields = trainer.field.cpu().numpy()
+    speed, angle = fields[..., 0].copy(), fields[..., 1].copy()
     pts = trainer.env.demo_xy.cpu().numpy()
     off = trainer.env.demo_off.cpu().numpy() if trainer.env.demo_off is not None else \
         [0, len(pts)]
     port = CPUPort(n, args.hidden, args.layers, args.batch, args.updates,
                    args.envs_per_group, args.seed, speed, angle, pts, off)
-    k, dt = time_port(port, args.cpu_budget, 6)
-    return {"value": k * n / dt, "unit": "env-steps/s", "cores": max(O.lib().orc_threads(),
-                                                                      torch.get_num_threads()),
+    k, dt = time_port(port, args.cpu_budget, 64)
+    single = single_env_rates(speed, angle, pts[off[0]:off[1]], 2.0)
+    model, nproc = cpu_info()
+    threads = max(O.lib().orc_threads(), torch.get_num_threads())
+    return {"value": k * n / dt, "unit": "env-steps/s", "cores": threads,
             "kind": "port",
             "sample": f"{k} vector steps of the same workload ({n} envs, TD3 {args.updates} "
                       f"epochs x batch {args.batch}, {args.layers}x{args.hidden}) on the oracle "
-                      f"CPU port (C OpenMP env tick + torch-CPU fp32 TD3), {dt:.1f} s"}
+                      f"CPU port: C OpenMP env tick with the same exact bucketed demo index as the "
+                      f"GPU + torch-CPU fp32 TD3, {threads} threads, {dt:.1f} s",
+            "cpu_model": model, "nproc": nproc,
+            "single_env_1core": {k2: round(v, 1) for k2, v in single.items()},
+            "single_env_note": "one env, one core, the C restatement looping in one call: "
+                               "Environment.step alone / the whole agent tick without the learner"}
+
+
+def timed_steps(tr, steps, ws, dev):
+    """Wall time of `steps` training steps between barrier + synchronize on both sides, max over
+    ranks."""
+    from nav.dist import max_over_ranks
+    barrier(ws)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        tr.step()
+    torch.cuda.synchronize()
+    barrier(ws)
+    dt = time.perf_counter() - t0
+    return max_over_ranks(dt, dev) if ws > 1 else dt
+
+
+def utd_sweep(args, dev, points=((8192, 2), (32768, 2), (32768, 8)), steps=30):
+    """env-steps/s at other update-to-data ratios (sampled transitions per collected one =
+    epochs x batch / envs): 0.25, 1 (the headline's), 4."""
+    from nav.trainer import VecTrainer
+    out = []
+    for batch, epochs in points:
+        tr = VecTrainer(n_envs=args.envs, hidden=args.hidden, n_hidden=args.layers, batch=batch,
+                        updates_per_step=epochs, seed=args.seed,
+                        envs_per_group=args.envs_per_group, device=dev)
+        for _ in range(4):
+            tr.step()
+        dt = timed_steps(tr, steps, 1, dev)
+        out.append({"update_to_data": epochs * batch / args.envs, "batch": batch,
+                    "td3_epochs_per_step": epochs, "steps": steps,
+                    "ms_per_step": round(1e3 * dt / steps, 4),
+                    "env_steps_per_s": args.envs * steps / dt})
+        del tr
+        torch.cuda.empty_cache()
+    return out
 
 
 def main():
@@ -170,7 +231,10 @@ def main():
         return
     from nav.dist import broadcast_params, make_grad_hook, max_over_ranks, shard_seed
     hook = make_grad_hook(ws) if args.shared_policy else None  # RCCL all-reduce over xGMI
-    tr = VecTrainer(n_envs=args.envs, hidden=args.hidden, n_hidden=args.layers, batch=args.batch,
+    # shared policy: the global batch is split over the ranks (each samples B / world rows from
+    # its local replay, the SUM all-reduce + / world makes it the full-batch update)
+    rank_batch = args.batch // ws if (args.shared_policy and ws > 1) else args.batch
+    tr = VecTrainer(n_envs=args.envs, hidden=args.hidden, n_hidden=args.layers, batch=rank_batch,
                     updates_per_step=args.updates, seed=shard_seed(args.seed, rank),
                     envs_per_group=args.envs_per_group, device=dev, grad_hook=hook)
     if args.shared_policy and ws > 1:  # same initial policy on every rank
@@ -207,6 +271,13 @@ def main():
     ksum = timer.summary()
     env_steps = args.envs * args.steps * ws
     value = env_steps / dt
+    # a longer event-free timed run beside the contract's K steps (extra key)
+    timed_long = None
+    if args.long_steps > 0:
+        dtl = timed_steps(tr, args.long_steps, ws, dev)
+        timed_long = {"steps": args.long_steps, "ms_per_step": 1e3 * dtl / args.long_steps,
+                      "value": args.envs * args.long_steps * ws / dtl,
+                      "note": "same loop, no HIP events in the timed region"}
 
     if rank == 0 and args.no_timed_events:
         print(json.dumps({"value": value, "ms_per_step": 1e3 * dt / args.steps,
@@ -249,6 +320,7 @@ def main():
                       "at_65536": sweep[0]["agent_step"]}
         # CPU baseline: rank 0 at N = 1 only (a reported baseline, not part of the scaling runs)
         cpu = None if (args.no_cpu_baseline or ws > 1) else cpu_baseline(args, tr)
+        utd = None if (args.no_utd_sweep or ws > 1) else utd_sweep(args, dev)
         line = {
             "metric": "env-steps/sec at 65 536 parallel envs (full residual-TD3 update)",
             "value": value, "unit": "env-steps/s", "n_gpus": ws, "steps": args.steps,
@@ -260,6 +332,7 @@ def main():
                        "envs_per_gpu": args.envs, "envs_per_group": args.envs_per_group,
                        "hidden": args.hidden, "layers": args.layers, "batch": args.batch,
                        "td3_epochs_per_step": args.updates,
+                       "rank_batch": rank_batch,
                        "update_to_data": args.updates * args.batch / args.envs,
                        "parallelism": ("dp%d-shared-policy" % ws if args.shared_policy and ws > 1
                                        else "independent-env-blocks x%d" % ws)},
@@ -271,7 +344,12 @@ def main():
                             v["launches"] / 2, "ms_per_step": v["total_ms"] / 2}
                         for k, v in breakdown.items()},
             "cpu_baseline": cpu,
+            "timed_long": timed_long,
+            "utd_sweep": utd,
         }
+        if hook is not None:
+            line["allreduce"] = {"messages_per_step": hook.calls / max(1, tr.steps),
+                                 "bytes_per_step": hook.bytes / max(1, tr.steps)}
         print(json.dumps(line), flush=True)
     if ws > 1:
         torch.distributed.destroy_process_group()

@@ -2,8 +2,10 @@
 
 Same per-vector-step work as nav.trainer.VecTrainer, restated on the host: actor forward on torch
 CPU fp32 + the act epilogue, the fused env/agent tick from the C oracle (OpenMP over envs, each
-group with its demonstration set), then `updates` TD3 epochs of the oracle learner (torch CPU).
-Timed on a bounded number of vector steps by bench.py; never part of the product path.
+group with its demonstration set and the same exact bucketed demo index as the GPU tick), then
+`updates` TD3 epochs of the oracle learner (torch CPU). Timed on a bounded number of vector steps
+by bench.py; never part of the product path. `single_env_rates` times the reference's single-env
+loop pieces on one core.
 """
 import ctypes as C
 import time
@@ -36,6 +38,10 @@ class CPUPort:
         self.st.meta[:] = 4
         self.demo_pts = np.ascontiguousarray(demo_pts, np.float64)
         self.demo_off = np.asarray(demo_off, np.int64)
+        # the same exact bucketed demo index the GPU tick uses (O.DemoIndexCPU == brute force,
+        # tests/test_oracle_golden.py), one per group
+        self.index = [O.DemoIndexCPU(self.demo_pts[self.demo_off[g]:self.demo_off[g + 1]])
+                      for g in range(len(self.demo_off) - 1)]
         sizes = lambda di, do: [di] + [hidden] * n_hidden + [do]  # noqa: E731
         self.td3 = TD3Oracle(make_mlp_params(seed, sizes(2, 2), 0.0),
                              make_mlp_params(seed + 1, sizes(4, 1), 0.0),
@@ -69,7 +75,8 @@ class CPUPort:
                 f(st.meta, O._u32p), f(st.plan_index, O._i32p), f(st.path_length, O._i32p),
                 f(st.episodes, O._i32p), f(st.noise_scale, O._dp), a[lo:].ctypes.data_as(O._dp),
                 ns[lo:].ctypes.data_as(O._dp), O.ptr(self.rows, O._fp), self.cap,
-                (self.pos + lo) % self.cap, lo)
+                (self.pos + lo) % self.cap, lo, O.ptr(self.index[g].start, O._i64p),
+                O.ptr(self.index[g].cand, O._i32p))
         self.pos = (self.pos + self.n) % self.cap
         self.size = min(self.size + self.n, self.cap)
         # TD3 epochs (robot.py:272-285) on batches with replacement
@@ -98,3 +105,30 @@ def time_port(port, budget_s=15.0, max_steps=8):
             break
     dt = time.perf_counter() - t0
     return k, dt
+
+
+def single_env_rates(speed, angle, demo_pts, seconds=2.0):
+    """One env on one core: Environment.step alone (environment.py:122-127) and the
+    whole per-step agent tick (step + process_transition with the demo term through the index +
+    episode control + replay push), the C restatement looping inside one call, env-steps/s."""
+    p = O.default_params()
+    sp = np.ascontiguousarray(speed, np.float32)
+    an = np.ascontiguousarray(angle, np.float32)
+    demo = np.ascontiguousarray(demo_pts, np.float64)
+    ix = O.DemoIndexCPU(demo)
+    acts = np.ascontiguousarray(np.random.default_rng(3).uniform(-5, 5, (4096, 2)))
+    out = {}
+    for name, tick in (("env_step_per_s", 0), ("agent_tick_per_s", 1)):
+        K, dt = 1 << 14, 0.0
+        while True:
+            t0 = time.perf_counter()
+            O.lib().orc_single_env_run(C.byref(p), O.ptr(sp, O._fp), O.ptr(an, O._fp),
+                                       O.ptr(demo, O._dp), len(demo), O.ptr(ix.start, O._i64p),
+                                       O.ptr(ix.cand, O._i32p), O.ptr(acts, O._dp), len(acts), K,
+                                       tick)
+            dt = time.perf_counter() - t0
+            if dt > seconds / 4 or K > (1 << 30):
+                break
+            K *= 4
+        out[name] = K / dt
+    return out

@@ -336,12 +336,138 @@ void orc_act_epilogue(const double* s, const double* g, const float* res, double
     }
 }
 
-int orc_vec_agent_tick(const orc_params_t* p, const float* speed, const float* angle,
-                       const double* demo, int64_t m, uint32_t env, double* state,
-                       const double* goal, const double* region, double* hist, uint32_t* meta,
-                       int32_t* plan_index, int32_t* path_length, int32_t* episodes,
-                       double* noise_scale, const double* action, double* next_out, float* row,
-                       double* reward_out, const double* reset_state) {
+/* ---- exact nearest-demo index for the CPU port (the cpu_baseline leg does the GPU's algorithm):
+ * per dynamics cell C a candidate list holding, for every query in C, its nearest demo point.
+ * Any demo point q bounds the nearest distance of every x in C by U = maxdist(q, C), and the
+ * nearest point p* has mindist(p*, C) <= U, so {p : mindist^2(p, C) <= U^2} suffices; the min over
+ * it is the same f64 value as over all points (tests/test_oracle_golden.py checks it). The
+ * construction buckets the points into the 1 x 1 cells and searches rings of buckets. */
+static double cell_maxd2(double px, double py, double lx, double ly) {
+    double fx = fmax(fabs(px - lx), fabs(px - (lx + 1.0)));
+    double fy = fmax(fabs(py - ly), fabs(py - (ly + 1.0)));
+    return fx * fx + fy * fy;
+}
+
+static double cell_mind2(double px, double py, double lx, double ly) {
+    double nx = fmax(0.0, fmax(lx - px, px - (lx + 1.0)));
+    double ny = fmax(0.0, fmax(ly - py, py - (ly + 1.0)));
+    return nx * nx + ny * ny;
+}
+
+static int bucket_of(double v) {
+    int b = (int)floor(v);
+    return b < 0 ? 0 : (b > 99 ? 99 : b);
+}
+
+int64_t orc_demo_index_build(const double* demo, int64_t m, int64_t* cell_start, int32_t* cand,
+                             int64_t cap) {
+    /* buckets (CSR) of the in-world points; points outside [0,100)^2 go to a side list that
+     * every cell checks (augmentation noise can push a demo point off the world) */
+    int64_t* bstart = (int64_t*)calloc(10001, sizeof(int64_t));
+    int32_t* bpts = (int32_t*)malloc((size_t)(m > 0 ? m : 1) * sizeof(int32_t));
+    int32_t* outside = (int32_t*)malloc((size_t)(m > 0 ? m : 1) * sizeof(int32_t));
+    int64_t n_out = 0;
+    for (int64_t j = 0; j < m; ++j) {
+        double x = demo[2 * j], y = demo[2 * j + 1];
+        if (x >= 0.0 && x < 100.0 && y >= 0.0 && y < 100.0)
+            bstart[bucket_of(x) * 100 + bucket_of(y) + 1]++;
+        else
+            outside[n_out++] = (int32_t)j;
+    }
+    for (int k = 0; k < 10000; ++k) bstart[k + 1] += bstart[k];
+    int64_t* fill = (int64_t*)malloc(10000 * sizeof(int64_t));
+    memcpy(fill, bstart, 10000 * sizeof(int64_t));
+    for (int64_t j = 0; j < m; ++j) {
+        double x = demo[2 * j], y = demo[2 * j + 1];
+        if (x >= 0.0 && x < 100.0 && y >= 0.0 && y < 100.0)
+            bpts[fill[bucket_of(x) * 100 + bucket_of(y)]++] = (int32_t)j;
+    }
+    free(fill);
+    int64_t total = 0;
+    for (int cell = 0; cell < 10000; ++cell) {
+        const int cx = cell / 100, cy = cell % 100;
+        const double lx = (double)cx, ly = (double)cy;
+        double u = INFINITY;
+        for (int64_t o = 0; o < n_out; ++o)
+            u = fmin(u, cell_maxd2(demo[2 * outside[o]], demo[2 * outside[o] + 1], lx, ly));
+        /* rings of buckets around the cell until one ring past the first non-empty one */
+        int hit = -1;
+        for (int r = 0; r < 100; ++r) {
+            int any = 0;
+            for (int bx = cx - r; bx <= cx + r; ++bx) {
+                if (bx < 0 || bx > 99) continue;
+                for (int by = cy - r; by <= cy + r; ++by) {
+                    if (by < 0 || by > 99) continue;
+                    if (abs(bx - cx) != r && abs(by - cy) != r) continue;
+                    const int b = bx * 100 + by;
+                    for (int64_t t = bstart[b]; t < bstart[b + 1]; ++t) {
+                        const int32_t j = bpts[t];
+                        u = fmin(u, cell_maxd2(demo[2 * j], demo[2 * j + 1], lx, ly));
+                        any = 1;
+                    }
+                }
+            }
+            if (any && hit < 0) hit = r;
+            if (hit >= 0 && r >= hit + 1) break;
+        }
+        const double lim = u * (1.0 + 1e-12) + 1e-12;
+        /* a point in a bucket at Chebyshev distance d is at least d - 1 from the cell */
+        const int R = isinf(lim) ? 100 : (int)ceil(sqrt(lim)) + 1;
+        const int64_t first = total;
+        for (int bx = cx - R; bx <= cx + R; ++bx) {
+            if (bx < 0 || bx > 99) continue;
+            for (int by = cy - R; by <= cy + R; ++by) {
+                if (by < 0 || by > 99) continue;
+                const int b = bx * 100 + by;
+                for (int64_t t = bstart[b]; t < bstart[b + 1]; ++t) {
+                    const int32_t j = bpts[t];
+                    if (cell_mind2(demo[2 * j], demo[2 * j + 1], lx, ly) <= lim) {
+                        if (cand && total < cap) cand[total] = j;
+                        ++total;
+                    }
+                }
+            }
+        }
+        for (int64_t o = 0; o < n_out; ++o) {
+            const int32_t j = outside[o];
+            if (cell_mind2(demo[2 * j], demo[2 * j + 1], lx, ly) <= lim) {
+                if (cand && total < cap) cand[total] = j;
+                ++total;
+            }
+        }
+        if (cell_start) {
+            cell_start[cell] = first;
+            cell_start[cell + 1] = total;
+        }
+    }
+    free(bstart);
+    free(bpts);
+    free(outside);
+    return total;
+}
+
+/* robot.py:753 min distance through the index (brute force off the indexed world) */
+double orc_demo_min_idx(const double* demo, int64_t m, const int64_t* cell_start,
+                        const int32_t* cand, double x, double y) {
+    if (!(x >= 0.0 && x < 100.0 && y >= 0.0 && y < 100.0)) return orc_demo_min(demo, m, x, y);
+    const int k = (int)x * 100 + (int)y;
+    double best = INFINITY;
+    for (int64_t t = cell_start[k]; t < cell_start[k + 1]; ++t) {
+        const int32_t j = cand[t];
+        double dx = x - demo[2 * j], dy = y - demo[2 * j + 1];
+        double q = dx * dx + dy * dy;
+        if (q < best) best = q;
+    }
+    return sqrt(best);
+}
+
+static int tick_impl(const orc_params_t* p, const float* speed, const float* angle,
+                     const double* demo, int64_t m, const int64_t* idx_start,
+                     const int32_t* idx_cand, uint32_t env, double* state, const double* goal,
+                     const double* region, double* hist, uint32_t* meta, int32_t* plan_index,
+                     int32_t* path_length, int32_t* episodes, double* noise_scale,
+                     const double* action, double* next_out, float* row, double* reward_out,
+                     const double* reset_state) {
     uint32_t mt = *meta;
     int goal_reached = (int)(mt & 1u), stuck_flag = (int)((mt >> 1) & 1u);
     int demo_flag = (int)((mt >> 2) & 1u);
@@ -351,8 +477,20 @@ int orc_vec_agent_tick(const orc_params_t* p, const float* speed, const float* a
     orc_step(speed, angle, ns, action); /* environment.py:122-127 */
 
     /* robot.py:645-675 process_transition */
-    double r = orc_compute_reward(ns, goal, demo, m, demo_flag, &goal_reached, p->goal_threshold,
-                                  p->goal_reward, p->demo_factor);
+    double r;
+    if (idx_start && m > 0) { /* compute_reward (robot.py:727-762) with the indexed minimum */
+        double g = -orc_norm2(ns[0] - goal[0], ns[1] - goal[1]);
+        if (g >= -p->goal_threshold) {
+            goal_reached = 1;
+            r = p->goal_reward;
+        } else {
+            double mn = orc_demo_min_idx(demo, m, idx_start, idx_cand, ns[0], ns[1]);
+            r = g + p->demo_factor * (demo_flag ? -mn : 0.0);
+        }
+    } else {
+        r = orc_compute_reward(ns, goal, demo, m, demo_flag, &goal_reached, p->goal_threshold,
+                               p->goal_reward, p->demo_factor);
+    }
     /* hist is laid out [5][2] for this env */
     int stuck = orc_check_if_stuck(hist, &cnt, &head, s, p->stuck_threshold);
     if (stuck) {
@@ -395,6 +533,17 @@ int orc_vec_agent_tick(const orc_params_t* p, const float* speed, const float* a
     return flags;
 }
 
+int orc_vec_agent_tick(const orc_params_t* p, const float* speed, const float* angle,
+                       const double* demo, int64_t m, uint32_t env, double* state,
+                       const double* goal, const double* region, double* hist, uint32_t* meta,
+                       int32_t* plan_index, int32_t* path_length, int32_t* episodes,
+                       double* noise_scale, const double* action, double* next_out, float* row,
+                       double* reward_out, const double* reset_state) {
+    return tick_impl(p, speed, angle, demo, m, NULL, NULL, env, state, goal, region, hist, meta,
+                     plan_index, path_length, episodes, noise_scale, action, next_out, row,
+                     reward_out, reset_state);
+}
+
 int orc_threads(void) {
 #ifdef _OPENMP
     return omp_get_max_threads();
@@ -409,17 +558,42 @@ void orc_vec_agent_step_batch(const orc_params_t* p, const float* speed, const f
                               uint32_t* meta, int32_t* plan_index, int32_t* path_length,
                               int32_t* episodes, double* noise_scale, const double* action,
                               double* next_out, float* rows, int64_t cap, int64_t base,
-                              int64_t env0) {
-    /* hist here is [n][5][2] (env-major; the device layout differs, the values do not) */
+                              int64_t env0, const int64_t* idx_start, const int32_t* idx_cand) {
+    /* hist here is [n][5][2] (env-major; the device layout differs, the values do not);
+     * idx_start / idx_cand (nullable): the demo set's orc_demo_index_build index */
 #ifdef _OPENMP
 #pragma omp parallel for schedule(static)
 #endif
     for (int64_t e = 0; e < n; ++e) {
         int64_t slot = (base + e) % cap;
-        orc_vec_agent_tick(p, speed, angle, demo, m, (uint32_t)(env0 + e), state + 2 * e,
-                           goal + 2 * e,
-                           region + 4 * e, hist + 10 * e, meta + e, plan_index + e,
-                           path_length + e, episodes + e, noise_scale + e, action + 2 * e,
-                           next_out + 2 * e, rows + 8 * slot, NULL, NULL);
+        tick_impl(p, speed, angle, demo, m, idx_start, idx_cand, (uint32_t)(env0 + e),
+                  state + 2 * e, goal + 2 * e, region + 4 * e, hist + 10 * e, meta + e,
+                  plan_index + e, path_length + e, episodes + e, noise_scale + e, action + 2 * e,
+                  next_out + 2 * e, rows + 8 * slot, NULL, NULL);
     }
+}
+
+/* Single-env loop on one core for the cpu_baseline's per-env figures: K steps of
+ * Environment.step alone (tick = 0) or of the whole agent tick (tick = 1: step, process_transition
+ * with the demo term through the index, episode control, replay push into a 1024-row ring),
+ * actions cycled from actions [n_act][2]. Returns a checksum of the final state. */
+double orc_single_env_run(const orc_params_t* p, const float* speed, const float* angle,
+                          const double* demo, int64_t m, const int64_t* idx_start,
+                          const int32_t* idx_cand, const double* actions, int64_t n_act,
+                          int64_t K, int tick) {
+    double state[2] = {50.0, 50.0}, goal[2], region[4], hist[10] = {0}, ns[2];
+    uint32_t meta = 4u;
+    int32_t plan = 5, path = p->path_length0, ep = 5;
+    double noise = 1.0;
+    static float rows[1024 * 8];
+    orc_vec_init_one(p, 0, region, goal);
+    for (int64_t k = 0; k < K; ++k) {
+        const double* a = actions + 2 * (k % n_act);
+        if (tick)
+            tick_impl(p, speed, angle, demo, m, idx_start, idx_cand, 0u, state, goal, region, hist,
+                      &meta, &plan, &path, &ep, &noise, a, ns, rows + 8 * (k & 1023), NULL, NULL);
+        else
+            orc_step(speed, angle, state, a);
+    }
+    return state[0] + state[1];
 }

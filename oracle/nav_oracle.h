@@ -112,7 +112,21 @@ void orc_vec_agent_step_batch(const orc_params_t* p, const float* speed, const f
                               uint32_t* meta, int32_t* plan_index, int32_t* path_length,
                               int32_t* episodes, double* noise_scale, const double* action,
                               double* next_state_out, float* replay_rows, int64_t replay_cap,
-                              int64_t replay_base, int64_t env0 /* global index of env 0 */);
+                              int64_t replay_base, int64_t env0 /* global index of env 0 */,
+                              const int64_t* idx_start, const int32_t* idx_cand /* nullable */);
+
+/* Exact nearest-demo index (per 1 x 1 dynamics cell, the candidates that can be nearest to any
+ * query in the cell): cell_start [10001], cand [returned total]; call with cand = NULL (cap 0) to
+ * size. orc_demo_min_idx = orc_demo_min through it, the same f64 value. */
+int64_t orc_demo_index_build(const double* demo_xy, int64_t m, int64_t* cell_start, int32_t* cand,
+                             int64_t cap);
+double orc_demo_min_idx(const double* demo_xy, int64_t m, const int64_t* cell_start,
+                        const int32_t* cand, double x, double y);
+/* K single-env steps on one core: Environment.step alone (tick 0) or the whole agent tick (1). */
+double orc_single_env_run(const orc_params_t* p, const float* speed, const float* angle,
+                          const double* demo_xy, int64_t m, const int64_t* idx_start,
+                          const int32_t* idx_cand, const double* actions, int64_t n_act,
+                          int64_t K, int tick);
 
 #ifdef __cplusplus
 }

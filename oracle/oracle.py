@@ -86,7 +86,14 @@ def lib():
         L.orc_vec_agent_step_batch.argtypes = [C.POINTER(Params), _fp, _fp, _dp, C.c_int64,
                                                C.c_int64, _dp, _dp, _dp, _dp, _u32p, _i32p, _i32p,
                                                _i32p, _dp, _dp, _dp, _fp, C.c_int64, C.c_int64,
-                                               C.c_int64]
+                                               C.c_int64, _i64p, _i32p]
+        L.orc_demo_index_build.restype = C.c_int64
+        L.orc_demo_index_build.argtypes = [_dp, C.c_int64, _i64p, _i32p, C.c_int64]
+        L.orc_single_env_run.restype = C.c_double
+        L.orc_single_env_run.argtypes = [C.POINTER(Params), _fp, _fp, _dp, C.c_int64, _i64p,
+                                         _i32p, _dp, C.c_int64, C.c_int64, C.c_int]
+        L.orc_demo_min_idx.restype = C.c_double
+        L.orc_demo_min_idx.argtypes = [_dp, C.c_int64, _i64p, _i32p, C.c_double, C.c_double]
         _lib = L
     return _lib
 
@@ -96,6 +103,24 @@ def ptr(a, t):
         return None
     assert a.flags["C_CONTIGUOUS"], "oracle arrays must be C-contiguous"
     return a.ctypes.data_as(t)
+
+
+class DemoIndexCPU:
+    """orc_demo_index_build over one demo set (the CPU port's counterpart of nav's DemoIndex)."""
+
+    def __init__(self, demo):
+        self.demo = np.ascontiguousarray(demo, np.float64).reshape(-1, 2)
+        m = len(self.demo)
+        self.start = np.zeros(10001, np.int64)
+        total = lib().orc_demo_index_build(ptr(self.demo, _dp), m, ptr(self.start, _i64p), None, 0)
+        self.cand = np.zeros(max(total, 1), np.int32)
+        lib().orc_demo_index_build(ptr(self.demo, _dp), m, ptr(self.start, _i64p),
+                                   ptr(self.cand, _i32p), total)
+        self.total = total
+
+    def min(self, x, y):
+        return lib().orc_demo_min_idx(ptr(self.demo, _dp), len(self.demo), ptr(self.start, _i64p),
+                                      ptr(self.cand, _i32p), x, y)
 
 
 def default_params(seed=1707366464):

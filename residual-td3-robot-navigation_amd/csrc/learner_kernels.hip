@@ -1,0 +1,1107 @@
+// learner_kernels.hip — the cross-row half of the residual-TD3 learner (robot.py:236-310) on
+// gfx950: hidden x hidden weight gradients on MFMA, the fixed-order gradient reduce fused with
+// torch's Adam, multi-net Adam for the shared-policy bucket, Polyak soft updates (all refreshing
+// the packed MFMA weight images), and the replay sampling / copy glue. The row-local half
+// (forward, row backward, the fused train_critic / train_actor row programs) is mlp_kernels.hip.
+#include "mlp_common.h"
+
+namespace {
+
+// ---------------- hidden x hidden weight gradients (split-M partial slabs) ----------------
+// dW_L = dz_L^T h_{L-1} for L = 1 .. nh-1 over the rows of each split. The thin layers' gradients
+// (W0, every bias, Wo, bo) are edge partials of the forward / backward kernels instead.
+//
+// Work decomposition: one workgroup = 8 waves = one 64 x 64 output tile (n0.., k0..) of one
+// layer of one network over the rows of one split; each wave takes 1/8 of the split's rows and
+// keeps the tile in 4 v_mfma_f32_32x32x2_f32 accumulators (the MFMA K dimension is the batch
+// row), the 8 partial tiles are summed through LDS in wave order and the workgroup writes ONE
+// 16 KB partial slab tile. 256 workgroups (one per CU, 2 waves per SIMD) cover the twin critics
+// at 8 splits or the actor at 16, so the slabs are 4 MB per launch (was 64 row splits x 128 x 128
+// tiles = 27 MB) and the reduce reads 8-16 slabs instead of 64.
+// Operands come straight from registers, no panel staging and no barrier in the row loop: for
+// the batch rows (2 per MFMA step: lane half h = row parity) every lane forms its own A element
+// P[row][n0 + 32 i + lane] and B element Q[row][k0 + 32 j + lane]. P = dz of the top hidden
+// layer is recomputed as top_unit(dy row, Wo column) under the forward's ReLU bit; Q = h_0 as
+// layer0_unit(x row, W0 row, b0) — the same bits the backward / forward produced, so a 2-hidden-
+// layer network reads only its input rows, dy rows and 1 bit per element. The row data (x, dy)
+// of 64 rows is loaded coalesced (lane = row), parked in a wave-private LDS slot and read back
+// as a broadcast per lane half; saved panels of deeper networks are read per element.
+struct WgradArgs {
+    MlpDev net[2];          // 1 or 2 networks, same shapes, same input rows
+    int64_t M;
+    const float* in;        // layer-0 input rows: h_0 is recomputed (layer0_unit)
+    int ld_in, in_col;
+    const float* acts[2];   // [nh][M][hp]: saved h_L, 1 <= L <= nh-2
+    const float* dz[2];     // [nh][M][hp]: saved dz_L, 1 <= L <= nh-2
+    const float* dy[2];     // dz_{nh-1} is recomputed: top_unit(dy row, Wo) under the ReLU bit
+    int ld_dy;
+    const uint16_t* masks[2];  // the forward's ReLU bit image
+    float* slabs[2];        // [splits][(nh-1) hp hp]
+    int splits;
+    int TT;                 // 64-wide tiles across hp
+    int n_hid;              // tile jobs per network = (nh - 1) * TT * TT
+    int64_t per_split;      // rows per split (multiple of 64)
+    int64_t per_wave;       // rows per wave (multiple of 64)
+};
+
+#ifndef NAV_WG_WAVES
+#define NAV_WG_WAVES 8
+#endif
+#ifndef NAV_WG_EXP
+#define NAV_WG_EXP 0  // tuning probes: 1 = operands without VALU math, 2 = without LDS reads
+#endif
+constexpr int WG_WAVES = NAV_WG_WAVES;
+constexpr int WG_THREADS = WG_WAVES * 64;
+constexpr int WG_TILE = 64;
+constexpr int WG_CHUNK = 64;  // rows per staged chunk (lane = row)
+// LDS: 8 partial 64 x 64 tiles for the in-workgroup reduction + per wave 64 rows of (x[4], dy[2])
+constexpr int WG_STAGE_FLOATS = WG_CHUNK * 6;  // one slot; 2 slots per wave (double buffer)
+inline size_t wgrad_lds_bytes() {
+    return ((size_t)WG_WAVES * WG_TILE * WG_TILE + (size_t)WG_WAVES * 2 * WG_STAGE_FLOATS) * 4;
+}
+
+// rows [r_lo, r_hi) of one wave into acc (tile n0.., k0.. of layer L of net y)
+template <bool PR, bool QR>
+NAV_DEV void wgrad_rows(const WgradArgs& a, int y, int L, int n0, int k0, int64_t r_lo,
+                        int64_t r_hi, float* stage, f32x16 (&acc)[2][2]) {
+    const MlpDev& net = a.net[y];
+    const int hp = net.hp, nh = net.n_hidden, d_in = net.d_in, d_out = net.d_out;
+    const int lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
+    const int64_t M = a.M, MH = M * hp;
+    // 32-column sub-tiles inside hp (wave-uniform); absent columns read a clamped valid column
+    const bool nv1 = n0 + 32 < hp, kv1 = k0 + 32 < hp;
+    const int cn[2] = {n0 + l32, nv1 ? n0 + 32 + l32 : n0 + l32};
+    const int ck[2] = {k0 + l32, kv1 ? k0 + 32 + l32 : k0 + l32};
+    float wo[2][2] = {{0.f, 0.f}, {0.f, 0.f}}, w0[2][4] = {}, b0[2] = {0.f, 0.f};
+    if (PR) {
+        const float* Wo = net.params + net.w_off[nh];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            wo[i][0] = Wo[cn[i]];
+            wo[i][1] = d_out > 1 ? Wo[hp + cn[i]] : 0.f;
+        }
+    }
+    if (QR) {
+        const float* W0 = net.params + net.w_off[0];
+        const float* bb = net.params + net.b_off[0];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) w0[j][k] = k < d_in ? W0[ck[j] * d_in + k] : 0.f;
+            b0[j] = bb[ck[j]];
+        }
+    }
+    const int NTm = hp >> 5;
+    const uint16_t* mk = PR ? a.masks[y] + (size_t)(nh - 1) * mask_rowtiles(M) * NTm * 64 : nullptr;
+    const int tm0 = n0 >> 5, tm1 = nv1 ? tm0 + 1 : tm0;
+    const float* Psv = PR ? nullptr : a.dz[y] + (int64_t)L * MH;
+    const float* Qsv = QR ? nullptr : a.acts[y] + (int64_t)(L - 1) * MH;
+    float* xs = stage;                  // [64][4]
+    float* gs = stage + WG_CHUNK * 4;   // [64][2]
+
+    // one chunk's row data in registers: x row (QR), dy row (PR), and the ReLU words of the
+    // chunk's 2 row tiles x 2 column tiles (PR): bits of rows with (row & 4) == 0 in the low half
+    float4 cx = make_float4(0.f, 0.f, 0.f, 0.f);
+    float2 cg = make_float2(0.f, 0.f);
+    uint32_t cm[2][2] = {{0u, 0u}, {0u, 0u}};
+    auto load = [&](int64_t rb) {
+        const int64_t r = rb + lane;
+        const bool ok = r < r_hi;
+        const int64_t rc = ok ? r : r_lo;
+        if (QR) {
+            const float* x = a.in + rc * a.ld_in + a.in_col;
+            cx.x = ok ? x[0] : 0.f;
+            cx.y = ok && d_in > 1 ? x[1] : 0.f;
+            cx.z = ok && d_in > 2 ? x[2] : 0.f;
+            cx.w = ok && d_in > 3 ? x[3] : 0.f;
+        }
+        if (PR) {
+            const float* g = a.dy[y] + rc * a.ld_dy;
+            cg.x = ok ? g[0] : 0.f;
+            cg.y = ok && d_out > 1 ? g[1] : 0.f;
+            const int64_t rt0 = rb >> 5;
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int t = 0; t < 2; ++t) {
+                    const uint16_t* w = mk + ((rt0 + t) * NTm + (i ? tm1 : tm0)) * 64 + l32;
+                    cm[i][t] = (uint32_t)w[0] | ((uint32_t)w[32] << 16);
+                }
+        }
+    };
+    auto park = [&]() {
+        if (QR) *reinterpret_cast<float4*>(xs + lane * 4) = cx;
+        if (PR) *reinterpret_cast<float2*>(gs + lane * 2) = cg;
+    };
+    if (r_lo >= r_hi) return;
+    load(r_lo);
+    park();
+    uint32_t mw[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) mw[i][t] = cm[i][t] >> h;  // the lane half's row parity
+    for (int64_t rb = r_lo; rb < r_hi; rb += WG_CHUNK) {
+        const bool more = rb + WG_CHUNK < r_hi;
+        if (more) load(rb + WG_CHUNK);  // next chunk in flight under this one
+#pragma unroll
+        for (int s = 0; s < WG_CHUNK / 2; ++s) {
+            const int rr = 2 * s + h;  // row of this lane half inside the chunk
+            float p[2], q[2];
+            if (PR) {
+                const float2 g = *reinterpret_cast<const float2*>(gs + rr * 2);
+                // bit of row rr in the C-layout mask word: element (rr & 3) + 4 (rr >> 3 & 3) of
+                // lane half (rr >> 2) & 1 (the +h of rr was folded into mw)
+                const int sh = 16 * ((s >> 1) & 1) + 2 * (s & 1) + 4 * ((s & 15) >> 2);
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const uint32_t bit = (mw[i][s >> 4] >> sh) & 1u;
+                    p[i] = bit ? top_unit(g.x, g.y, wo[i][0], wo[i][1]) : 0.f;
+                }
+            } else {
+                const int64_t r = rb + rr;
+                const bool ok = r < r_hi;
+                const float* src = Psv + (ok ? r : r_lo) * hp;
+#pragma unroll
+                for (int i = 0; i < 2; ++i) p[i] = ok ? src[cn[i]] : 0.f;
+            }
+            if (QR) {
+                const float4 x = *reinterpret_cast<const float4*>(xs + rr * 4);
+#pragma unroll
+                for (int j = 0; j < 2; ++j) q[j] = layer0_unit(x, w0[j][0], w0[j][1], w0[j][2], w0[j][3], b0[j]);
+            } else {
+                const int64_t r = rb + rr;
+                const bool ok = r < r_hi;
+                const float* src = Qsv + (ok ? r : r_lo) * hp;
+#pragma unroll
+                for (int j = 0; j < 2; ++j) q[j] = ok ? src[ck[j]] : 0.f;
+            }
+            acc[0][0] = mfma(p[0], q[0], acc[0][0]);
+            if (kv1) acc[0][1] = mfma(p[0], q[1], acc[0][1]);
+            if (nv1) acc[1][0] = mfma(p[1], q[0], acc[1][0]);
+            if (nv1 && kv1) acc[1][1] = mfma(p[1], q[1], acc[1][1]);
+        }
+        if (more) {
+            park();  // this wave's reads of the slot were issued above: LDS keeps them in order
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int t = 0; t < 2; ++t) mw[i][t] = cm[i][t] >> h;
+        }
+    }
+}
+
+// The fast path of wgrad_rows for a full 64 x 64 tile of a 2-hidden-layer network (P and Q both
+// recomputed — the bench shape): branch-free and software-pipelined. Step s's 4 MFMAs are issued
+// interleaved with the VALU that forms step s+1's operands (sched_group_barrier: 1 MFMA, then a
+// quarter of the VALU), and the LDS row data is read two steps ahead, so neither the operand
+// math nor the LDS latency sits between two MFMAs of the wave. The row data is double-buffered
+// per wave: the next chunk is parked into the other slot half-way through the current one.
+NAV_DEV void wgrad_rows_fast(const WgradArgs& a, int y, int n0, int k0, int64_t r_lo,
+                             int64_t r_hi, float* stage, f32x16 (&acc)[2][2]) {
+    const MlpDev& net = a.net[y];
+    const int hp = net.hp, nh = net.n_hidden, d_in = net.d_in, d_out = net.d_out;
+    const int lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
+    const int64_t M = a.M;
+    const int cn[2] = {n0 + l32, n0 + 32 + l32};
+    const int ck[2] = {k0 + l32, k0 + 32 + l32};
+    float wo[2][2], w0[2][4], b0[2];
+    {
+        const float* Wo = net.params + net.w_off[nh];
+        const float* W0 = net.params + net.w_off[0];
+        const float* bb = net.params + net.b_off[0];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            wo[i][0] = Wo[cn[i]];
+            wo[i][1] = d_out > 1 ? Wo[hp + cn[i]] : 0.f;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) w0[i][k] = k < d_in ? W0[ck[i] * d_in + k] : 0.f;
+            b0[i] = bb[ck[i]];
+        }
+    }
+    const int NTm = hp >> 5;
+    const uint16_t* mk = a.masks[y] + (size_t)(nh - 1) * mask_rowtiles(M) * NTm * 64;
+    const int tm0 = n0 >> 5;
+    // the next chunk's raw loads stay untouched in registers until park(): anything computed
+    // from them here would pin a memory-latency wait at the top of the chunk
+    const bool xv4 = ((a.in_col | a.ld_in) & 3) == 0 && (reinterpret_cast<uintptr_t>(a.in) & 15) == 0;
+    const int nxl = a.ld_in - a.in_col < 4 ? a.ld_in - a.in_col : 4;  // x loads in bounds
+    float4 rx = make_float4(0.f, 0.f, 0.f, 0.f);
+    float rg0 = 0.f, rg1 = 0.f;
+    uint32_t rm[2][2][2];
+    int64_t rbl = r_lo;  // first row of the chunk the raw registers hold
+    auto load = [&](int64_t rb) {
+        rbl = rb;
+        const int64_t r = rb + lane;
+        const int64_t rc = r < r_hi ? r : r_lo;
+        const float* x = a.in + rc * a.ld_in + a.in_col;
+        if (xv4) {
+            rx = *reinterpret_cast<const float4*>(x);
+        } else {
+            rx.x = x[0];
+            if (nxl > 1) rx.y = x[1];
+            if (nxl > 2) rx.z = x[2];
+            if (nxl > 3) rx.w = x[3];
+        }
+        const float* g = a.dy[y] + rc * a.ld_dy;
+        rg0 = g[0];
+        if (d_out > 1) rg1 = g[1];
+        const int64_t rt0 = rb >> 5;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                const uint16_t* w = mk + ((rt0 + t) * NTm + tm0 + i) * 64 + l32;
+                rm[i][t][0] = w[0];
+                rm[i][t][1] = w[32];
+            }
+    };
+    // slot b: x [64][4] then dy [64][2]; rows past r_hi and inputs past d_in / d_out are zero;
+    // mwo receives the chunk's mask words shifted by the lane half's row parity
+    auto park = [&](int b, uint32_t (&mwo)[2][2]) {
+        const bool ok = rbl + lane < r_hi;
+        float* sl = stage + b * WG_STAGE_FLOATS;
+        const float4 x = make_float4(ok ? rx.x : 0.f, ok && d_in > 1 ? rx.y : 0.f,
+                                     ok && d_in > 2 ? rx.z : 0.f, ok && d_in > 3 ? rx.w : 0.f);
+        *reinterpret_cast<float4*>(sl + lane * 4) = x;
+        *reinterpret_cast<float2*>(sl + WG_CHUNK * 4 + lane * 2) =
+            make_float2(ok ? rg0 : 0.f, ok && d_out > 1 ? rg1 : 0.f);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int t = 0; t < 2; ++t) mwo[i][t] = (rm[i][t][0] | (rm[i][t][1] << 16)) >> h;
+    };
+    struct Row {
+        float4 x;
+        float2 g;
+    };
+    auto read = [&](int b, int s) {
+        const float* sl = stage + b * WG_STAGE_FLOATS;
+        const int rr = 2 * s + h;
+        Row r;
+        if (NAV_WG_EXP == 2) {
+            r.x = make_float4(wo[0][0] + s, wo[0][1], wo[1][0], wo[1][1]);
+            r.g = make_float2(b0[0] + s, b0[1]);
+            return r;
+        }
+        r.x = *reinterpret_cast<const float4*>(sl + rr * 4);
+        r.g = *reinterpret_cast<const float2*>(sl + WG_CHUNK * 4 + rr * 2);
+        return r;
+    };
+    // operands of chunk step s from its row data and the chunk's (h-shifted) mask words
+    auto operands = [&](const Row& r, const uint32_t (&m)[2][2], int s, float (&p)[2],
+                        float (&q)[2]) {
+        if (NAV_WG_EXP == 1) {
+            p[0] = r.g.x; p[1] = r.g.y; q[0] = r.x.x; q[1] = r.x.y;
+            return;
+        }
+        const int sh = 16 * ((s >> 1) & 1) + 2 * (s & 1) + 4 * ((s & 15) >> 2);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const float v = top_unit(r.g.x, r.g.y, wo[i][0], wo[i][1]);
+            p[i] = (m[i][(s >> 4) & 1] >> sh) & 1u ? v : 0.f;
+            q[i] = layer0_unit(r.x, w0[i][0], w0[i][1], w0[i][2], w0[i][3], b0[i]);
+        }
+    };
+    if (r_lo >= r_hi) return;
+    uint32_t mw[2][2], mwn[2][2];
+    load(r_lo);
+    park(0, mw);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) mwn[i][t] = mw[i][t];
+    float p[2], q[2];
+    Row ra = read(0, 0), rb1 = read(0, 1);
+    operands(ra, mw, 0, p, q);
+    ra = rb1;  // row data of step 1
+    int buf = 0;
+    for (int64_t rb = r_lo; rb < r_hi; rb += WG_CHUNK) {
+        const bool more = rb + WG_CHUNK < r_hi;
+        if (more) load(rb + WG_CHUNK);
+#pragma unroll
+        for (int s = 0; s < WG_CHUNK / 2; ++s) {
+            if (s == WG_CHUNK / 4 && more) park(buf ^ 1, mwn);
+            __builtin_amdgcn_sched_barrier(0);
+            // LDS read of step s + 2 (the next chunk's slot for the last two steps)
+            Row rn = ra;
+            if (s + 2 < WG_CHUNK / 2) rn = read(buf, s + 2);
+            else if (more) rn = read(buf ^ 1, s + 2 - WG_CHUNK / 2);
+            // operands of step s + 1 from the row data read one step earlier
+            float pn[2] = {0.f, 0.f}, qn[2] = {0.f, 0.f};
+            if (s + 1 < WG_CHUNK / 2) operands(ra, mw, s + 1, pn, qn);
+            else if (more) operands(ra, mwn, 0, pn, qn);
+            acc[0][0] = mfma(p[0], q[0], acc[0][0]);
+            acc[0][1] = mfma(p[0], q[1], acc[0][1]);
+            acc[1][0] = mfma(p[1], q[0], acc[1][0]);
+            acc[1][1] = mfma(p[1], q[1], acc[1][1]);
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // the 2 LDS reads first
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+                __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);  // up to 6 VALU
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            p[0] = pn[0]; p[1] = pn[1]; q[0] = qn[0]; q[1] = qn[1];
+            ra = rn;
+        }
+        if (more) {
+            buf ^= 1;
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int t = 0; t < 2; ++t) mw[i][t] = mwn[i][t];
+        }
+    }
+}
+
+// The MFMA-operand path for a full 64 x 64 tile of a 2-hidden-layer network (the bench shape).
+// The operands are produced by MFMAs too: per 32-row tile, dz = dy . Wo (K = d_out <= 2, one
+// v_mfma_f32_32x32x2_f32 per 32 columns) and h_0 = x . W0^T + b0 (K = d_in <= 4, two MFMAs on
+// the bias as C) land in the C layout, where lane (l32, h) register e holds row
+// acc_row(e, h) of column l32. Taking the weight-gradient MFMA's K (batch-row) order as
+// step e <-> rows {acc_row(e, 0), acc_row(e, 1)}, register e of those tiles IS the A / B operand
+// of step e, and bit e of the lane's own ReLU mask word (the forward's C-layout image) is the
+// ReLU derivative of exactly that element. Per 64 weight-gradient MFMAs a wave issues 6 operand
+// MFMAs and ~100 VALU (mask, relu) instead of ~320 VALU: the f32 MFMA shares the SIMD's issue
+// with the VALU, so the VALU count per MFMA is what sets the rate. No LDS, no barrier in the
+// row loop. h_0 and dz are the forward's / backward's values as fused f32 chains in the same
+// order (layer0_unit: b + x0 w0 + x1 w1 + ..., top_unit: g0 w0 + g1 w1).
+NAV_DEV void wgrad_rows_mfma(const WgradArgs& a, int y, int n0, int k0, int64_t r_lo,
+                             int64_t r_hi, f32x16 (&acc)[2][2]) {
+    const MlpDev& net = a.net[y];
+    const int hp = net.hp, nh = net.n_hidden, d_in = net.d_in, d_out = net.d_out;
+    const int lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
+    const int64_t M = a.M;
+    const int NTm = hp >> 5;
+    // constant B operands of the operand MFMAs: Wo rows (k = output j = h), W0 columns (k = h,
+    // then 2 + h), and the bias through a K = 2 MFMA of (1, 0) x (b, 0): the C tile starts at b
+    // exactly, so h_0 accumulates in layer0_unit's order b + x0 w0 + x1 w1 + x2 w2 + x3 w3
+    float wob[2], w0b[2][2], bob[2];
+    {
+        const float* Wo = net.params + net.w_off[nh];
+        const float* W0 = net.params + net.w_off[0];
+        const float* bb = net.params + net.b_off[0];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            wob[i] = h < d_out ? Wo[h * hp + n0 + 32 * i + l32] : 0.f;
+            const int c = k0 + 32 * i + l32;
+            w0b[i][0] = h < d_in ? W0[c * d_in + h] : 0.f;
+            w0b[i][1] = 2 + h < d_in ? W0[c * d_in + 2 + h] : 0.f;
+            bob[i] = h == 0 ? bb[c] : 0.f;
+        }
+    }
+    const float one = h == 0 ? 1.f : 0.f;
+    const uint16_t* mk = a.masks[y] + (size_t)(nh - 1) * mask_rowtiles(M) * NTm * 64 +
+                         (size_t)(n0 >> 5) * 64 + lane;
+    const size_t mstride = (size_t)NTm * 64;
+    const float* dyp = a.dy[y];
+    const int ld_dy = a.ld_dy, ld_in = a.ld_in;
+    const float* xin = a.in + a.in_col;
+    // raw loads of a 32-row tile (A operands: lane l32 = row, h = k; the lane's 2 mask words),
+    // from clamped in-bounds addresses; what does not exist is zeroed where it is used
+    const int gk = h < d_out ? h : 0, xk0 = h < d_in ? h : 0, xk1 = 2 + h < d_in ? 2 + h : 0;
+    struct Raw {
+        float g, x0, x1;
+        uint32_t m0, m1;
+    };
+    auto load = [&](int64_t rt) {
+        const int64_t r = rt + l32;
+        const int64_t rc = r < r_hi ? r : r_lo;
+        Raw v;
+        v.g = dyp[rc * ld_dy + gk];
+        const float* x = xin + rc * ld_in;
+        v.x0 = x[xk0];
+        v.x1 = x[xk1];
+        const uint16_t* w = mk + (size_t)(rt >> 5) * mstride;
+        v.m0 = w[0];
+        v.m1 = w[64];
+        return v;
+    };
+    // operand MFMAs of one tile (results in the C layout, masked later by finish())
+    auto issue = [&](int64_t rt, const Raw& v, f32x16 (&P)[2], f32x16 (&Q)[2]) {
+        const bool ok = rt + l32 < r_hi && h < d_out;  // rows past r_hi: dz = 0, add nothing
+        const float g = ok ? v.g : 0.f;
+        const float x0 = h < d_in ? v.x0 : 0.f, x1 = 2 + h < d_in ? v.x1 : 0.f;
+        const f32x16 zero = {};
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            P[i] = mfma(g, wob[i], zero);
+            Q[i] = mfma(one, bob[i], zero);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) Q[i] = mfma(x0, w0b[i][0], Q[i]);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) Q[i] = mfma(x1, w0b[i][1], Q[i]);
+    };
+    // ReLU derivative of the top layer on P (bit e of the lane's word as an all-ones mask) and
+    // the layer-0 ReLU on Q (an integer max of the bit pattern: one v_max_i32)
+    auto finish = [&](const Raw& v, f32x16 (&P)[2], f32x16 (&Q)[2]) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            // v_bfe_i32 of one bit: 0 or all ones
+            P[0][e] = __int_as_float(__float_as_int(P[0][e]) & __builtin_amdgcn_sbfe((int)v.m0, e, 1));
+            P[1][e] = __int_as_float(__float_as_int(P[1][e]) & __builtin_amdgcn_sbfe((int)v.m1, e, 1));
+            Q[0][e] = __int_as_float(max(__float_as_int(Q[0][e]), 0));
+            Q[1][e] = __int_as_float(max(__float_as_int(Q[1][e]), 0));
+        }
+    };
+    if (r_lo >= r_hi) return;
+    // ping-pong operand buffers (a loop-carried copy would cost 64 v_mov per tile, and the VALU
+    // shares the SIMD's issue with the f32 MFMA): tile t uses buffer t & 1 while the operand
+    // MFMAs of tile t + 1 fill the other
+    f32x16 PA[2], QA[2], PB[2], QB[2];
+    Raw cur = load(r_lo);
+    issue(r_lo, cur, PA, QA);
+    Raw nxt = cur;
+    if (r_lo + 32 < r_hi) nxt = load(r_lo + 32);
+    finish(cur, PA, QA);
+    auto step = [&](int64_t rt, f32x16 (&P)[2], f32x16 (&Q)[2], f32x16 (&Pn)[2],
+                    f32x16 (&Qn)[2]) {
+        const bool more = rt + 32 < r_hi;
+        // the next tile's operand MFMAs go first: done long before finish() reads them
+        if (more) issue(rt + 32, nxt, Pn, Qn);
+        Raw nn = nxt;
+        if (rt + 64 < r_hi) nn = load(rt + 64);
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            acc[0][0] = mfma(P[0][e], Q[0][e], acc[0][0]);
+            acc[0][1] = mfma(P[0][e], Q[1][e], acc[0][1]);
+            acc[1][0] = mfma(P[1][e], Q[0][e], acc[1][0]);
+            acc[1][1] = mfma(P[1][e], Q[1][e], acc[1][1]);
+        }
+        if (more) finish(nxt, Pn, Qn);
+        nxt = nn;
+    };
+    for (int64_t rt = r_lo; rt < r_hi; rt += 64) {
+        step(rt, PA, QA, PB, QB);
+        if (rt + 32 < r_hi) step(rt + 32, PB, QB, PA, QA);
+    }
+}
+
+// grid: nets x tile jobs x splits workgroups of 8 waves. Block order is XCD-grouped (blocks b and
+// b + 8 share an XCD's L2): the tile jobs of one (net, split) — which read the same rows — are
+// consecutive in the virtual order v and land on one XCD.
+__global__ __launch_bounds__(WG_THREADS) void k_wgrad(WgradArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int total = gridDim.x;
+    const int b = blockIdx.x;
+    const int v = (total % 8 == 0) ? (b % 8) * (total / 8) + b / 8 : b;
+    const int grp = v / a.n_hid, job = v % a.n_hid;
+    const int y = grp / a.splits, split = grp % a.splits;
+    const MlpDev& net = a.net[y];
+    const int hp = net.hp, nh = net.n_hidden, TT = a.TT;
+    const int L = job / (TT * TT) + 1;
+    const int n0 = ((job % (TT * TT)) / TT) * WG_TILE, k0 = (job % TT) * WG_TILE;
+    const int wv = wave_id(), lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
+    const int64_t M = a.M;
+    const int64_t s_lo = (int64_t)split * a.per_split < M ? (int64_t)split * a.per_split : M;
+    const int64_t s_hi = s_lo + a.per_split < M ? s_lo + a.per_split : M;
+    const int64_t r_lo = s_lo + wv * a.per_wave < s_hi ? s_lo + wv * a.per_wave : s_hi;
+    const int64_t r_hi = r_lo + a.per_wave < s_hi ? r_lo + a.per_wave : s_hi;
+    float* red = smem;                                          // [8][64][64]
+    float* stage = smem + WG_WAVES * WG_TILE * WG_TILE + wv * 2 * WG_STAGE_FLOATS;
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+    const bool pr = L == nh - 1, qr = L == 1;
+    const bool full = n0 + WG_TILE <= hp && k0 + WG_TILE <= hp;
+#if NAV_WG_EXP == 3
+    if (pr && qr && full) wgrad_rows_fast(a, y, n0, k0, r_lo, r_hi, stage, acc);
+#else
+    if (pr && qr && full) wgrad_rows_mfma(a, y, n0, k0, r_lo, r_hi, acc);
+#endif
+    else if (pr && qr) wgrad_rows<true, true>(a, y, L, n0, k0, r_lo, r_hi, stage, acc);
+    else if (pr) wgrad_rows<true, false>(a, y, L, n0, k0, r_lo, r_hi, stage, acc);
+    else if (qr) wgrad_rows<false, true>(a, y, L, n0, k0, r_lo, r_hi, stage, acc);
+    else wgrad_rows<false, false>(a, y, L, n0, k0, r_lo, r_hi, stage, acc);
+    // the 8 partial tiles meet in LDS, summed in wave order
+    float* mine = red + wv * WG_TILE * WG_TILE;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e)
+                mine[(32 * i + acc_row(e, h)) * WG_TILE + 32 * j + l32] = acc[i][j][e];
+    __syncthreads();
+    float* o = a.slabs[y] + (int64_t)split * hidden_w_count(net) + (int64_t)(L - 1) * hp * hp;
+    for (int idx = threadIdx.x; idx < WG_TILE * WG_TILE; idx += WG_THREADS) {
+        const int m = idx / WG_TILE, c = idx % WG_TILE;
+        float s = red[idx];
+#pragma unroll
+        for (int w = 1; w < WG_WAVES; ++w) s += red[w * WG_TILE * WG_TILE + idx];
+        if (n0 + m < hp && k0 + c < hp) o[(int64_t)(n0 + m) * hp + k0 + c] = s;
+    }
+}
+
+// ---------------- optimizer / target update, refreshing the packed images ----------------
+struct PackInfo {
+    int hp, n_hidden;
+    int64_t w_off[kMaxLayers];
+    float* packed;
+};
+
+NAV_DEV void repack(const PackInfo& pk, int64_t i, float4 v) {
+    // i = flat float index of v.x (multiple of 4)
+    for (int L = 1; L < pk.n_hidden; ++L) {
+        const int64_t off = pk.w_off[L], sz = (int64_t)pk.hp * pk.hp;
+        if (i >= off && i < off + sz) {
+            const int64_t e = i - off;
+            const int n = (int)(e / pk.hp), k = (int)(e % pk.hp);
+            float* Wf = pk.packed + (int64_t)(L - 1) * 2 * sz;
+            float* Wb = Wf + sz;
+            *reinterpret_cast<float4*>(Wf + ((int64_t)(k >> 2) * pk.hp + n) * 4) = v;
+            float* d = Wb + ((int64_t)(n >> 2) * pk.hp + k) * 4 + (n & 3);
+            d[0] = v.x; d[4] = v.y; d[8] = v.z; d[12] = v.w;
+            return;
+        }
+    }
+}
+
+NAV_DEV float adam1(float& p, float g, float& m, float& v, float b1w, float b2, float omb2,
+                    float eps, float step_size, float bc2s) {
+    // torch 2.10 _single_tensor_adam: m.lerp_(g, 1-b1); v.mul_(b2).addcmul_(g, g, 1-b2);
+    // denom = v.sqrt()/bc2_sqrt + eps; p.addcdiv_(m, denom, -step_size)
+    m = fmaf(b1w, g - m, m);
+    v = v * b2 + (omb2 * g) * g;
+    const float denom = sqrtf(v) / bc2s + eps;
+    p = p + (-step_size) * (m / denom);
+    return p;
+}
+
+// ---------------- gradient reduce (+ fused Adam) ----------------
+// grad = hidden-W entries: sum of the weight-gradient split slabs (block = 64 float4 columns x 4
+// split groups, the group sums added in order through LDS); every other entry: sum of the
+// per-row-block edge slabs (one wave per float4, lanes take blocks b = lane, lane + 64, ..., a
+// fixed xor tree adds the lanes). Deterministic: the same order on every run. With ADAM the
+// finished gradient goes straight into torch's Adam update (robot.py:236-239) of the parameter
+// it belongs to and the packed MFMA images are refreshed; up to 2 networks per launch.
+struct RedNet {
+    MlpDev net;
+    const float4* hs;
+    const float4* es;
+    float4* grad;  // nullable with ADAM
+    float4* p;
+    float4* m;
+    float4* v;
+    float step_size, bc2s;
+    PackInfo pk;
+    int nbh, nbe;
+};
+
+struct RedArgs {
+    RedNet n[2];
+    int splits;
+    int64_t nblk;
+    float b1w, b2, omb2, eps;
+};
+
+template <bool ADAM>
+NAV_DEV void red_out(const RedArgs& a, const RedNet& rn, int64_t flat4, float4 g) {
+    if (rn.grad) rn.grad[flat4] = g;
+    if (!ADAM) return;
+    float4 pp = rn.p[flat4], mm = rn.m[flat4], vv = rn.v[flat4];
+    adam1(pp.x, g.x, mm.x, vv.x, a.b1w, a.b2, a.omb2, a.eps, rn.step_size, rn.bc2s);
+    adam1(pp.y, g.y, mm.y, vv.y, a.b1w, a.b2, a.omb2, a.eps, rn.step_size, rn.bc2s);
+    adam1(pp.z, g.z, mm.z, vv.z, a.b1w, a.b2, a.omb2, a.eps, rn.step_size, rn.bc2s);
+    adam1(pp.w, g.w, mm.w, vv.w, a.b1w, a.b2, a.omb2, a.eps, rn.step_size, rn.bc2s);
+    rn.p[flat4] = pp;
+    rn.m[flat4] = mm;
+    rn.v[flat4] = vv;
+    if (rn.pk.packed) repack(rn.pk, flat4 * 4, pp);
+}
+
+template <bool ADAM>
+__global__ __launch_bounds__(kBlock) void k_grad_reduce(RedArgs a) {
+    __shared__ float4 part[4][64];
+    const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
+    int b = blockIdx.x;
+    const bool second = b >= a.n[0].nbh + a.n[0].nbe;
+    const RedNet& rn = second ? a.n[1] : a.n[0];
+    if (second) b -= a.n[0].nbh + a.n[0].nbe;
+    const MlpDev& net = rn.net;
+    if (b < rn.nbh) {
+        const int64_t hw4 = hidden_w_count(net) / 4;
+        const int64_t i = (int64_t)b * 64 + c;
+        float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (i < hw4) {
+#pragma unroll 4
+            for (int k = g; k < a.splits; k += 4) {
+                const float4 v = rn.hs[(int64_t)k * hw4 + i];
+                s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+            }
+        }
+        part[g][c] = s;
+        __syncthreads();
+        if (g != 0 || i >= hw4) return;
+        float4 r = part[0][c];
+#pragma unroll
+        for (int q = 1; q < 4; ++q) {
+            r.x += part[q][c].x; r.y += part[q][c].y; r.z += part[q][c].z; r.w += part[q][c].w;
+        }
+        const int64_t per = (int64_t)net.hp * net.hp / 4;
+        const int L = (int)(i / per) + 1;
+        red_out<ADAM>(a, rn, net.w_off[L] / 4 + i % per, r);
+        return;
+    }
+    const int64_t e4 = edge_count(net) / 4;
+    const int64_t o = (int64_t)(b - rn.nbh) * 4 + g;
+    if (o >= e4) return;  // wave-uniform
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t k = c; k < a.nblk; k += 64) {
+        const float4 v = rn.es[k * e4 + o];
+        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) {
+        s.x += __shfl_xor(s.x, d, 64);
+        s.y += __shfl_xor(s.y, d, 64);
+        s.z += __shfl_xor(s.z, d, 64);
+        s.w += __shfl_xor(s.w, d, 64);
+    }
+    if (c == 0) red_out<ADAM>(a, rn, edge_to_flat(net, 4 * o) / 4, s);
+}
+
+// robot.py:293-310 soft update of up to 4 (target, source) pairs in one launch
+struct PolyPair {
+    float4* t;
+    const float4* s;
+    int64_t n4;
+    PackInfo pk;
+};
+struct PolyArgs {
+    PolyPair q[4];
+    int n;
+    int64_t total4;
+    float omt, tau;
+};
+
+__global__ __launch_bounds__(kBlock) void k_adam(float4* __restrict__ p,
+                                                 const float4* __restrict__ g, float4* m,
+                                                 float4* v, int64_t n4, float b1w, float b2,
+                                                 float omb2, float eps, float ss, float bc2s,
+                                                 PackInfo pk) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n4;
+         i += (int64_t)gridDim.x * kBlock) {
+        float4 pp = p[i], gg = g[i], mm = m[i], vv = v[i];
+        adam1(pp.x, gg.x, mm.x, vv.x, b1w, b2, omb2, eps, ss, bc2s);
+        adam1(pp.y, gg.y, mm.y, vv.y, b1w, b2, omb2, eps, ss, bc2s);
+        adam1(pp.z, gg.z, mm.z, vv.z, b1w, b2, omb2, eps, ss, bc2s);
+        adam1(pp.w, gg.w, mm.w, vv.w, b1w, b2, omb2, eps, ss, bc2s);
+        p[i] = pp; m[i] = mm; v[i] = vv;
+        if (pk.packed) repack(pk, i * 4, pp);
+    }
+}
+
+// torch.optim.Adam of up to 2 networks in one launch from flat gradients that a collective
+// produced (shared policy: the SUM all-reduce of the bucket); g / grad_div is the averaged
+// gradient (grad_div 1: the plain step, bit-identical to k_adam).
+struct AdamNet {
+    float4* p;
+    const float4* g;
+    float4* m;
+    float4* v;
+    int64_t n4;
+    float step_size, bc2s;
+    PackInfo pk;
+};
+struct AdamArgs {
+    AdamNet q[2];
+    int n;
+    int64_t total4;
+    float b1w, b2, omb2, eps, gdiv;
+};
+
+__global__ __launch_bounds__(kBlock) void k_adam_multi(AdamArgs a) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < a.total4;
+         i += (int64_t)gridDim.x * kBlock) {
+        const bool second = a.n > 1 && i >= a.q[0].n4;
+        const AdamNet& q = second ? a.q[1] : a.q[0];
+        const int64_t j = second ? i - a.q[0].n4 : i;
+        float4 pp = q.p[j], gg = q.g[j], mm = q.m[j], vv = q.v[j];
+        gg.x = gg.x / a.gdiv; gg.y = gg.y / a.gdiv; gg.z = gg.z / a.gdiv; gg.w = gg.w / a.gdiv;
+        adam1(pp.x, gg.x, mm.x, vv.x, a.b1w, a.b2, a.omb2, a.eps, q.step_size, q.bc2s);
+        adam1(pp.y, gg.y, mm.y, vv.y, a.b1w, a.b2, a.omb2, a.eps, q.step_size, q.bc2s);
+        adam1(pp.z, gg.z, mm.z, vv.z, a.b1w, a.b2, a.omb2, a.eps, q.step_size, q.bc2s);
+        adam1(pp.w, gg.w, mm.w, vv.w, a.b1w, a.b2, a.omb2, a.eps, q.step_size, q.bc2s);
+        q.p[j] = pp; q.m[j] = mm; q.v[j] = vv;
+        if (q.pk.packed) repack(q.pk, j * 4, pp);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_polyak(float4* __restrict__ t,
+                                                   const float4* __restrict__ s, int64_t n4,
+                                                   float omt, float tau, PackInfo pk) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n4;
+         i += (int64_t)gridDim.x * kBlock) {
+        float4 a = t[i];
+        const float4 b = s[i];
+        // robot.py:309 target*(1-tau) + source*tau (two products, one sum)
+        a.x = a.x * omt + b.x * tau;
+        a.y = a.y * omt + b.y * tau;
+        a.z = a.z * omt + b.z * tau;
+        a.w = a.w * omt + b.w * tau;
+        t[i] = a;
+        if (pk.packed) repack(pk, i * 4, a);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_polyak_multi(PolyArgs a) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < a.total4;
+         i += (int64_t)gridDim.x * kBlock) {
+        int64_t j = i;
+        int k = 0;
+        while (k < a.n - 1 && j >= a.q[k].n4) j -= a.q[k++].n4;
+        const PolyPair& q = a.q[k];
+        float4 t = q.t[j];
+        const float4 s = q.s[j];
+        // robot.py:309 target*(1-tau) + source*tau (two products, one sum)
+        t.x = t.x * a.omt + s.x * a.tau;
+        t.y = t.y * a.omt + s.y * a.tau;
+        t.z = t.z * a.omt + s.z * a.tau;
+        t.w = t.w * a.omt + s.w * a.tau;
+        q.t[j] = t;
+        if (q.pk.packed) repack(q.pk, j * 4, t);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_pack(const float4* __restrict__ p, int64_t n4,
+                                                 PackInfo pk) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n4;
+         i += (int64_t)gridDim.x * kBlock)
+        repack(pk, i * 4, p[i]);
+}
+
+// ---------------- TD3 glue ----------------
+__global__ __launch_bounds__(kBlock) void k_replay_sample(const float4* __restrict__ rows,
+                                                          int64_t size, int64_t B,
+                                                          const int64_t* __restrict__ idx,
+                                                          uint32_t s0, uint32_t s1, uint32_t ctr,
+                                                          float4* __restrict__ batch) {
+    const int64_t b = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (b >= B) return;
+    int64_t k;
+    if (idx) {
+        k = idx[b];
+    } else {
+        const uint4 w = philox((uint32_t)b, 0u, NAV_TAG_SAMPLE, ctr, s0, s1);
+        k = (int64_t)(((uint64_t)w.x * (uint64_t)size) >> 32);
+    }
+    batch[2 * b] = rows[2 * k];
+    batch[2 * b + 1] = rows[2 * k + 1];
+}
+
+__global__ __launch_bounds__(kBlock) void k_fill(float* x, int64_t n, float v) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) x[i] = v;
+}
+
+__global__ __launch_bounds__(kBlock) void k_strided_copy(const float* __restrict__ src, int lds,
+                                                         int cs, float* __restrict__ dst, int ldd,
+                                                         int cd, int64_t rows, int cols) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= rows * cols) return;
+    const int64_t r = i / cols;
+    const int c = (int)(i % cols);
+    dst[r * ldd + cd + c] = src[r * lds + cs + c];
+}
+
+inline int blocks_for(int64_t n) { return (int)((n + kBlock - 1) / kBlock); }
+inline int grid_stride_blocks(int64_t n) {
+    const int64_t b = (n + kBlock - 1) / kBlock;
+    return (int)(b < 2048 ? (b > 0 ? b : 1) : 2048);
+}
+
+PackInfo pack_info(const MlpDev& d, float* packed) {
+    PackInfo pk;
+    pk.hp = d.hp;
+    pk.n_hidden = d.n_hidden;
+    for (int l = 0; l < kMaxLayers; ++l) pk.w_off[l] = l <= d.n_hidden ? d.w_off[l] : 0;
+    pk.packed = d.n_hidden > 1 ? packed : nullptr;
+    return pk;
+}
+
+bool red_net(const nav_mlp* net, const float* hs, int splits, const float* es, float* grad,
+             RedNet* rn) {
+    if (!make_dev(net, &rn->net)) return false;
+    if (rn->net.n_hidden > 1 && (!hs || splits < 1)) return false;
+    rn->hs = reinterpret_cast<const float4*>(hs);
+    rn->es = reinterpret_cast<const float4*>(es);
+    rn->grad = reinterpret_cast<float4*>(grad);
+    rn->nbh = (int)((hidden_w_count(rn->net) / 4 + 63) / 64);
+    rn->nbe = (int)((edge_count(rn->net) / 4 + 3) / 4);
+    return true;
+}
+
+
+}  // namespace
+
+extern "C" {
+
+int32_t nav_mlp_wgrad_splits(int32_t n_nets, int32_t hidden_pad, int32_t n_hidden, int64_t M) {
+    if (n_nets < 1 || n_nets > 2 || hidden_pad < 32 || hidden_pad > 256 || (hidden_pad & 31) ||
+        n_hidden < 1 || M < 0)
+        return NAV_EINVAL;
+    if (n_hidden < 2) return 1;
+    const int TT = (hidden_pad + WG_TILE - 1) / WG_TILE;
+    const int64_t jobs = (int64_t)n_nets * (n_hidden - 1) * TT * TT;
+    // one 8-wave workgroup per CU (256 CUs), at least 512 rows (64 per wave) per split
+    int64_t s = 256 / jobs;
+    const int64_t by_rows = (M + 511) / 512;
+    if (s > by_rows) s = by_rows;
+    return (int32_t)(s < 1 ? 1 : s);
+}
+
+int nav_mlp_wgrad(const nav_mlp* nets, int32_t n_nets, int64_t M, const float* in,
+                  int32_t ld_in, int32_t in_col, const float* const* acts,
+                  const float* const* dz, const float* const* dy, int32_t ld_dy,
+                  const uint16_t* const* masks, float* const* slabs, int32_t splits,
+                  void* stream) {
+    WgradArgs a{};
+    if (!nets || n_nets < 1 || n_nets > 2 || M < 1 || splits < 1 || !in || !dy || ld_dy < 0 ||
+        !masks || !slabs)
+        return NAV_EINVAL;
+    for (int i = 0; i < n_nets; ++i) {
+        if (!make_dev(&nets[i], &a.net[i]) || !dy[i] || !masks[i] || !slabs[i]) return NAV_EINVAL;
+        if (a.net[i].hp != a.net[0].hp || a.net[i].d_in != a.net[0].d_in ||
+            a.net[i].n_hidden != a.net[0].n_hidden || a.net[i].d_out != a.net[0].d_out)
+            return NAV_EINVAL;
+        a.acts[i] = acts ? acts[i] : nullptr;
+        a.dz[i] = dz ? dz[i] : nullptr;
+        if (a.net[i].n_hidden > 2 && (!a.acts[i] || !a.dz[i])) return NAV_EINVAL;
+        a.dy[i] = dy[i];
+        a.masks[i] = masks[i];
+        a.slabs[i] = slabs[i];
+    }
+    if (in_col < 0 || in_col + a.net[0].d_in > ld_in) return NAV_EINVAL;
+    if (a.net[0].n_hidden < 2) return 0;
+    a.M = M;
+    a.in = in;
+    a.ld_in = ld_in;
+    a.in_col = in_col;
+    a.ld_dy = ld_dy;
+    a.splits = splits;
+    a.TT = (a.net[0].hp + WG_TILE - 1) / WG_TILE;
+    a.n_hid = (a.net[0].n_hidden - 1) * a.TT * a.TT;
+    // 64-row aligned splits and per-wave ranges: a chunk's mask row tiles start on a tile boundary
+    a.per_split = ((M + splits - 1) / splits + WG_CHUNK - 1) / WG_CHUNK * WG_CHUNK;
+    a.per_wave = ((a.per_split + WG_WAVES - 1) / WG_WAVES + WG_CHUNK - 1) / WG_CHUNK * WG_CHUNK;
+    const int64_t blocks = (int64_t)n_nets * a.n_hid * splits;
+    if (blocks > ((int64_t)1 << 30)) return NAV_EINVAL;
+    const size_t lds = wgrad_lds_bytes();
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wgrad),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k_wgrad, dim3((unsigned)blocks), dim3(WG_THREADS), lds, S(stream), a);
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_grad_reduce(const nav_mlp* net, const float* hidden_slabs, int32_t splits,
+                    const float* edge_slabs, int64_t edge_blocks, float* grad, void* stream) {
+    RedArgs a{};
+    if (!grad || !edge_slabs || edge_blocks < 1 || splits < 0 ||
+        !red_net(net, hidden_slabs, splits, edge_slabs, grad, &a.n[0]))
+        return NAV_EINVAL;
+    a.splits = splits;
+    a.nblk = edge_blocks;
+    hipLaunchKernelGGL(k_grad_reduce<false>, dim3((unsigned)(a.n[0].nbh + a.n[0].nbe)),
+                       dim3(kBlock), 0, S(stream), a);
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_grad_reduce_multi(const nav_mlp* nets, int32_t n_nets, const float* const* hidden_slabs,
+                          int32_t splits, const float* const* edge_slabs, int64_t edge_blocks,
+                          float* const* grads, void* stream) {
+    RedArgs a{};
+    if (!nets || n_nets < 1 || n_nets > 2 || !hidden_slabs || !edge_slabs || edge_blocks < 1 ||
+        splits < 0 || !grads)
+        return NAV_EINVAL;
+    int blocks = 0;
+    for (int i = 0; i < n_nets; ++i) {
+        if (!edge_slabs[i] || !grads[i] ||
+            !red_net(&nets[i], hidden_slabs[i], splits, edge_slabs[i], grads[i], &a.n[i]))
+            return NAV_EINVAL;
+        if (a.n[i].net.hp != a.n[0].net.hp || a.n[i].net.n_hidden != a.n[0].net.n_hidden)
+            return NAV_EINVAL;
+        blocks += a.n[i].nbh + a.n[i].nbe;
+    }
+    a.splits = splits;
+    a.nblk = edge_blocks;
+    hipLaunchKernelGGL(k_grad_reduce<false>, dim3((unsigned)blocks), dim3(kBlock), 0, S(stream),
+                       a);
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_adam_multi(const nav_mlp* nets, int32_t n_nets, const float* const* grads,
+                   float* const* m, float* const* v, float beta1, float beta2, float eps,
+                   const float* step_size, const float* bc2_sqrt, float grad_div, void* stream) {
+    AdamArgs a{};
+    if (!nets || n_nets < 1 || n_nets > 2 || !grads || !m || !v || !step_size || !bc2_sqrt ||
+        !(grad_div > 0.f))
+        return NAV_EINVAL;
+    for (int i = 0; i < n_nets; ++i) {
+        MlpDev d;
+        if (!make_dev(&nets[i], &d) || !grads[i] || !m[i] || !v[i]) return NAV_EINVAL;
+        AdamNet& q = a.q[i];
+        q.p = reinterpret_cast<float4*>(nets[i].params);
+        q.g = reinterpret_cast<const float4*>(grads[i]);
+        q.m = reinterpret_cast<float4*>(m[i]);
+        q.v = reinterpret_cast<float4*>(v[i]);
+        q.n4 = d.count / 4;
+        q.step_size = step_size[i];
+        q.bc2s = bc2_sqrt[i];
+        q.pk = pack_info(d, nets[i].packed);
+        a.total4 += q.n4;
+    }
+    a.n = n_nets;
+    a.b1w = 1.0f - beta1;
+    a.b2 = beta2;
+    a.omb2 = 1.0f - beta2;
+    a.eps = eps;
+    a.gdiv = grad_div;
+    hipLaunchKernelGGL(k_adam_multi, dim3(grid_stride_blocks(a.total4)), dim3(kBlock), 0,
+                       S(stream), a);
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_grad_reduce_adam(const nav_mlp* nets, int32_t n_nets, const float* const* hidden_slabs,
+                         int32_t splits, const float* const* edge_slabs, int64_t edge_blocks,
+                         float* const* grads, float* const* m, float* const* v, float beta1,
+                         float beta2, float eps, const float* step_size, const float* bc2_sqrt,
+                         void* stream) {
+    RedArgs a{};
+    if (!nets || n_nets < 1 || n_nets > 2 || !hidden_slabs || !edge_slabs || edge_blocks < 1 ||
+        splits < 0 || !m || !v || !step_size || !bc2_sqrt)
+        return NAV_EINVAL;
+    int blocks = 0;
+    for (int i = 0; i < n_nets; ++i) {
+        RedNet& rn = a.n[i];
+        if (!edge_slabs[i] || !m[i] || !v[i] ||
+            !red_net(&nets[i], hidden_slabs[i], splits, edge_slabs[i], grads ? grads[i] : nullptr,
+                     &rn))
+            return NAV_EINVAL;
+        rn.p = reinterpret_cast<float4*>(nets[i].params);
+        rn.m = reinterpret_cast<float4*>(m[i]);
+        rn.v = reinterpret_cast<float4*>(v[i]);
+        rn.step_size = step_size[i];
+        rn.bc2s = bc2_sqrt[i];
+        rn.pk = pack_info(rn.net, nets[i].packed);
+        blocks += rn.nbh + rn.nbe;
+    }
+    a.splits = splits;
+    a.nblk = edge_blocks;
+    a.b1w = 1.0f - beta1;
+    a.b2 = beta2;
+    a.omb2 = 1.0f - beta2;
+    a.eps = eps;
+    hipLaunchKernelGGL(k_grad_reduce<true>, dim3((unsigned)blocks), dim3(kBlock), 0, S(stream),
+                       a);
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_polyak_multi(const nav_mlp* targets, const nav_mlp* sources, int32_t n, float tau,
+                     void* stream) {
+    PolyArgs a{};
+    if (!targets || !sources || n < 1 || n > 4) return NAV_EINVAL;
+    for (int i = 0; i < n; ++i) {
+        MlpDev dt, ds;
+        if (!make_dev(&targets[i], &dt) || !make_dev(&sources[i], &ds) || dt.count != ds.count ||
+            dt.hp != ds.hp || dt.n_hidden != ds.n_hidden)
+            return NAV_EINVAL;
+        a.q[i].t = reinterpret_cast<float4*>(targets[i].params);
+        a.q[i].s = reinterpret_cast<const float4*>(sources[i].params);
+        a.q[i].n4 = dt.count / 4;
+        a.q[i].pk = pack_info(dt, targets[i].packed);
+        a.total4 += a.q[i].n4;
+    }
+    a.n = n;
+    a.omt = 1.0f - tau;
+    a.tau = tau;
+    hipLaunchKernelGGL(k_polyak_multi, dim3(grid_stride_blocks(a.total4)), dim3(kBlock), 0,
+                       S(stream), a);
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_adam(const nav_mlp* net, const float* grad, float* m, float* v, float beta1, float beta2,
+             float eps, float step_size, float bc2_sqrt, void* stream) {
+    MlpDev d;
+    if (!make_dev(net, &d) || !grad || !m || !v) return NAV_EINVAL;
+    const int64_t n4 = d.count / 4;
+    hipLaunchKernelGGL(k_adam, dim3(grid_stride_blocks(n4)), dim3(kBlock), 0, S(stream),
+                       reinterpret_cast<float4*>(net->params),
+                       reinterpret_cast<const float4*>(grad), reinterpret_cast<float4*>(m),
+                       reinterpret_cast<float4*>(v), n4, 1.0f - beta1, beta2, 1.0f - beta2, eps,
+                       step_size, bc2_sqrt, pack_info(d, net->packed));
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_polyak(const nav_mlp* target, const nav_mlp* source, float tau, void* stream) {
+    MlpDev dt, ds;
+    if (!make_dev(target, &dt) || !make_dev(source, &ds) || dt.count != ds.count ||
+        dt.hp != ds.hp || dt.n_hidden != ds.n_hidden)
+        return NAV_EINVAL;
+    const int64_t n4 = dt.count / 4;
+    hipLaunchKernelGGL(k_polyak, dim3(grid_stride_blocks(n4)), dim3(kBlock), 0, S(stream),
+                       reinterpret_cast<float4*>(target->params),
+                       reinterpret_cast<const float4*>(source->params), n4, 1.0f - tau, tau,
+                       pack_info(dt, target->packed));
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_mlp_pack(const nav_mlp* net, void* stream) {
+    MlpDev d;
+    if (!make_dev(net, &d)) return NAV_EINVAL;
+    if (d.n_hidden < 2) return 0;
+    const int64_t n4 = d.count / 4;
+    hipLaunchKernelGGL(k_pack, dim3(grid_stride_blocks(n4)), dim3(kBlock), 0, S(stream),
+                       reinterpret_cast<const float4*>(net->params), n4,
+                       pack_info(d, net->packed));
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_replay_sample(const nav_replay* replay, int64_t size, int64_t B, const int64_t* idx,
+                      uint32_t seed_lo, uint32_t seed_hi, uint32_t counter, float* batch,
+                      void* stream) {
+    if (!replay || !replay->rows || size < 1 || size > replay->capacity ||
+        size > ((int64_t)1 << 32) || B < 0 || !batch)
+        return NAV_EINVAL;
+    if (B == 0) return 0;
+    hipLaunchKernelGGL(k_replay_sample, dim3(blocks_for(B)), dim3(kBlock), 0, S(stream),
+                       reinterpret_cast<const float4*>(replay->rows), size, B, idx, seed_lo,
+                       seed_hi, counter, reinterpret_cast<float4*>(batch));
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_fill(float* x, int64_t n, float value, void* stream) {
+    if (n < 0 || (n && !x)) return NAV_EINVAL;
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_fill, dim3(blocks_for(n)), dim3(kBlock), 0, S(stream), x, n, value);
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_strided_copy(const float* src, int32_t ld_src, int32_t col_src, float* dst,
+                     int32_t ld_dst, int32_t col_dst, int64_t rows, int32_t cols, void* stream) {
+    if (rows < 0 || cols < 0 || (rows && cols && (!src || !dst))) return NAV_EINVAL;
+    if (rows == 0 || cols == 0) return 0;
+    hipLaunchKernelGGL(k_strided_copy, dim3(blocks_for(rows * cols)), dim3(kBlock), 0, S(stream),
+                       src, ld_src, col_src, dst, ld_dst, col_dst, rows, cols);
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+}  // extern "C"

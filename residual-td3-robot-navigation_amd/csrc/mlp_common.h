@@ -1,0 +1,123 @@
+// mlp_common.h — the device MLP layout (include/navenv.h nav_mlp) and the fragment helpers
+// shared by the row kernels (mlp_kernels.hip) and the learner kernels (learner_kernels.hip).
+#pragma once
+#include <stdlib.h>
+
+#include "nav_device.h"
+
+using namespace nav;
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kMaxLayers = 9;
+// train_actor keeps the actor's top hidden layer in registers for its dWo partials (1) or writes
+// it to `acts` and reads it back (0; A/B builds)
+#ifndef NAV_ACTOR_TOP_REGS
+#define NAV_ACTOR_TOP_REGS 1
+#endif
+// workgroups hold RT row tiles of 32 rows (RT = 2 or 4; NAV_MLP_RT)
+
+struct MlpDev {
+    const float* params;
+    const float* packed;
+    int d_in, d_out, hp, n_hidden;
+    int64_t count;
+    int64_t w_off[kMaxLayers], b_off[kMaxLayers];
+};
+
+inline int64_t r4(int64_t x) { return (x + 3) & ~(int64_t)3; }
+
+bool make_dev(const nav_mlp* n, MlpDev* d) {
+    if (!n || n->d_in < 1 || n->d_in > 4 || n->d_out < 1 || n->d_out > 2 || n->hidden_pad < 32 ||
+        n->hidden_pad > 256 || (n->hidden_pad & 31) || n->n_hidden < 1 ||
+        n->n_hidden >= kMaxLayers || !n->params || (n->n_hidden > 1 && !n->packed) ||
+        n->hidden < 1 || n->hidden > n->hidden_pad)
+        return false;
+    const int hp = n->hidden_pad;
+    d->params = n->params;
+    d->packed = n->packed;
+    d->d_in = n->d_in;
+    d->d_out = n->d_out;
+    d->hp = hp;
+    d->n_hidden = n->n_hidden;
+    int64_t o = 0;
+    for (int l = 0; l <= n->n_hidden; ++l) {
+        const int64_t in = l == 0 ? n->d_in : hp, out = l == n->n_hidden ? n->d_out : hp;
+        d->w_off[l] = o;
+        o += r4(in * out);
+        d->b_off[l] = o;
+        o += r4(out);
+    }
+    d->count = o;
+    return true;
+}
+
+// Edge-gradient layout: every parameter except the hidden x hidden weights W_1 .. W_{nh-1}, in
+// the flat order with those segments cut out (W0 | b0 | b1 .. b_{nh-1} | Wo | bo). The forward /
+// backward kernels sum these per row block while the operands sit in LDS (edge slabs
+// [blocks][edge_count]); nav_grad_reduce folds them and the weight-gradient slabs into the flat
+// gradient.
+__host__ __device__ inline int64_t hidden_w_count(const MlpDev& d) {
+    return (int64_t)(d.n_hidden - 1) * d.hp * d.hp;
+}
+__host__ __device__ inline int64_t edge_count(const MlpDev& d) { return d.count - hidden_w_count(d); }
+// edge index of b_L (L < n_hidden), of Wo and of bo
+__host__ __device__ inline int64_t e_b(const MlpDev& d, int L) {
+    return d.b_off[L] - (int64_t)L * d.hp * d.hp;
+}
+__host__ __device__ inline int64_t e_wo(const MlpDev& d) { return d.w_off[d.n_hidden] - hidden_w_count(d); }
+__host__ __device__ inline int64_t e_bo(const MlpDev& d) { return d.b_off[d.n_hidden] - hidden_w_count(d); }
+// flat parameter index of edge index e
+__host__ __device__ inline int64_t edge_to_flat(const MlpDev& d, int64_t e) {
+    const int nh = d.n_hidden;
+    if (nh == 1 || e < d.w_off[1]) return e;
+    if (e >= e_wo(d)) return e + hidden_w_count(d);
+    const int64_t L = (e - d.w_off[1]) / d.hp + 1;  // inside the b_L run
+    return e + L * d.hp * d.hp;
+}
+
+inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// One hidden unit of layer 0 (K = d_in <= 4; absent inputs and weights are 0). The forward and the
+// weight-gradient kernel's recompute of h_0 share this fma order, so both produce the same bits.
+NAV_DEV float layer0_unit(float4 x, float w0, float w1, float w2, float w3, float b) {
+    float v = b;
+    v = fmaf(x.x, w0, v);
+    v = fmaf(x.y, w1, v);
+    v = fmaf(x.z, w2, v);
+    v = fmaf(x.w, w3, v);
+    return fmaxf(v, 0.f);
+}
+
+// dL/dz of the top hidden layer before its ReLU mask: dy . Wo[:, n] (d_out <= 2; absent = 0).
+// Shared by the backward and the weight-gradient recompute of dz_{nh-1}.
+NAV_DEV float top_unit(float g0, float g1, float w0, float w1) { return fmaf(g1, w1, g0 * w0); }
+
+NAV_DEV f32x16 mfma(float a, float b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+NAV_DEV int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
+
+// Column tiles of a wave: wave w owns 32-column tiles t = w and w + 4 (when < NT) of every
+// 128-row block, for all 4 row tiles: acc[rt][j] is the 32x32 tile (rows rt*32.., cols t_j*32..).
+// Wave index as a scalar: the compiler then treats per-wave tile ownership as uniform control
+// flow (s_cbranch) instead of exec-masked vector branches with pointer selects.
+NAV_DEV int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
+// ReLU masks: one 16-bit word per (row tile, column tile, lane) holding the lane's 16 C-layout
+// elements' (value > 0) bits; [n_hidden][row tiles][NT][64]. The backward reads 2 bytes per 16
+// elements instead of the 64 bytes of saved activations.
+NAV_DEV size_t mask_idx(int64_t rowtile, int NT_, int t, int lane) {
+    return ((size_t)rowtile * NT_ + t) * 64 + lane;
+}
+
+constexpr int kWaves = kBlock / 64;
+
+// Mask image row-tile count: independent of the workgroup height, so any RT reads what any RT
+// wrote (row tile = global row / 32; layers strided by ceil(M/128)*4 tiles).
+__host__ __device__ inline int64_t mask_rowtiles(int64_t M) { return ((M + 127) / 128) * 4; }
+
+}  // namespace

@@ -9,111 +9,9 @@
 // input layer (K = 2 or 4) and output layer (N = 1 or 2) run on the VALU; ReLU derivatives travel
 // from forward to backward as C-layout bit masks. Weight gradients: one launch per network over
 // row splits writing deterministic partial slabs, reduced in a fixed order.
-#include <stdlib.h>
-
-#include "nav_device.h"
-
-using namespace nav;
+#include "mlp_common.h"
 
 namespace {
-
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-
-constexpr int kMaxLayers = 9;
-// train_actor keeps the actor's top hidden layer in registers for its dWo partials (1) or writes
-// it to `acts` and reads it back (0; A/B builds)
-#ifndef NAV_ACTOR_TOP_REGS
-#define NAV_ACTOR_TOP_REGS 1
-#endif
-// workgroups hold RT row tiles of 32 rows (RT = 2 or 4; NAV_MLP_RT)
-
-struct MlpDev {
-    const float* params;
-    const float* packed;
-    int d_in, d_out, hp, n_hidden;
-    int64_t count;
-    int64_t w_off[kMaxLayers], b_off[kMaxLayers];
-};
-
-inline int64_t r4(int64_t x) { return (x + 3) & ~(int64_t)3; }
-
-bool make_dev(const nav_mlp* n, MlpDev* d) {
-    if (!n || n->d_in < 1 || n->d_in > 4 || n->d_out < 1 || n->d_out > 2 || n->hidden_pad < 32 ||
-        n->hidden_pad > 256 || (n->hidden_pad & 31) || n->n_hidden < 1 ||
-        n->n_hidden >= kMaxLayers || !n->params || (n->n_hidden > 1 && !n->packed) ||
-        n->hidden < 1 || n->hidden > n->hidden_pad)
-        return false;
-    const int hp = n->hidden_pad;
-    d->params = n->params;
-    d->packed = n->packed;
-    d->d_in = n->d_in;
-    d->d_out = n->d_out;
-    d->hp = hp;
-    d->n_hidden = n->n_hidden;
-    int64_t o = 0;
-    for (int l = 0; l <= n->n_hidden; ++l) {
-        const int64_t in = l == 0 ? n->d_in : hp, out = l == n->n_hidden ? n->d_out : hp;
-        d->w_off[l] = o;
-        o += r4(in * out);
-        d->b_off[l] = o;
-        o += r4(out);
-    }
-    d->count = o;
-    return true;
-}
-
-// Edge-gradient layout: every parameter except the hidden x hidden weights W_1 .. W_{nh-1}, in
-// the flat order with those segments cut out (W0 | b0 | b1 .. b_{nh-1} | Wo | bo). The forward /
-// backward kernels sum these per row block while the operands sit in LDS (edge slabs
-// [blocks][edge_count]); nav_grad_reduce folds them and the weight-gradient slabs into the flat
-// gradient.
-__host__ __device__ inline int64_t hidden_w_count(const MlpDev& d) {
-    return (int64_t)(d.n_hidden - 1) * d.hp * d.hp;
-}
-__host__ __device__ inline int64_t edge_count(const MlpDev& d) { return d.count - hidden_w_count(d); }
-// edge index of b_L (L < n_hidden), of Wo and of bo
-__host__ __device__ inline int64_t e_b(const MlpDev& d, int L) {
-    return d.b_off[L] - (int64_t)L * d.hp * d.hp;
-}
-__host__ __device__ inline int64_t e_wo(const MlpDev& d) { return d.w_off[d.n_hidden] - hidden_w_count(d); }
-__host__ __device__ inline int64_t e_bo(const MlpDev& d) { return d.b_off[d.n_hidden] - hidden_w_count(d); }
-// flat parameter index of edge index e
-__host__ __device__ inline int64_t edge_to_flat(const MlpDev& d, int64_t e) {
-    const int nh = d.n_hidden;
-    if (nh == 1 || e < d.w_off[1]) return e;
-    if (e >= e_wo(d)) return e + hidden_w_count(d);
-    const int64_t L = (e - d.w_off[1]) / d.hp + 1;  // inside the b_L run
-    return e + L * d.hp * d.hp;
-}
-
-inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
-
-// One hidden unit of layer 0 (K = d_in <= 4; absent inputs and weights are 0). The forward and the
-// weight-gradient kernel's recompute of h_0 share this fma order, so both produce the same bits.
-NAV_DEV float layer0_unit(float4 x, float w0, float w1, float w2, float w3, float b) {
-    float v = b;
-    v = fmaf(x.x, w0, v);
-    v = fmaf(x.y, w1, v);
-    v = fmaf(x.z, w2, v);
-    v = fmaf(x.w, w3, v);
-    return fmaxf(v, 0.f);
-}
-
-// dL/dz of the top hidden layer before its ReLU mask: dy . Wo[:, n] (d_out <= 2; absent = 0).
-// Shared by the backward and the weight-gradient recompute of dz_{nh-1}.
-NAV_DEV float top_unit(float g0, float g1, float w0, float w1) { return fmaf(g1, w1, g0 * w0); }
-
-NAV_DEV f32x16 mfma(float a, float b, f32x16 c) {
-    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
-}
-
-NAV_DEV int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
-
-// Column tiles of a wave: wave w owns 32-column tiles t = w and w + 4 (when < NT) of every
-// 128-row block, for all 4 row tiles: acc[rt][j] is the 32x32 tile (rows rt*32.., cols t_j*32..).
-// Wave index as a scalar: the compiler then treats per-wave tile ownership as uniform control
-// flow (s_cbranch) instead of exec-masked vector branches with pointer selects.
-NAV_DEV int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
 template <int NT>
 struct WaveCols {
@@ -187,12 +85,6 @@ NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const float* __restr
 enum { IN_F32 = 0, IN_BASELINE = 1 };
 enum { OUT_F32 = 0, OUT_TARGET = 1, OUT_ACT = 2, OUT_LOSS = 3 };
 
-// ReLU masks: one 16-bit word per (row tile, column tile, lane) holding the lane's 16 C-layout
-// elements' (value > 0) bits; [n_hidden][row tiles][NT][64]. The backward reads 2 bytes per 16
-// elements instead of the 64 bytes of saved activations.
-NAV_DEV size_t mask_idx(int64_t rowtile, int NT_, int t, int lane) {
-    return ((size_t)rowtile * NT_ + t) * 64 + lane;
-}
 
 struct FwdArgs {
     MlpDev net[2];
@@ -229,7 +121,6 @@ struct FwdArgs {
 };
 
 // Output-layer partial sums: [d_out <= 2][4 waves][TM rows] (red_floats per block).
-constexpr int kWaves = kBlock / 64;
 __host__ __device__ constexpr int red_floats(int tm) { return 2 * kWaves * tm; }
 
 // rows [tm][hp+4] + input/dy staging [tm][4] + output-layer partial sums
@@ -237,9 +128,6 @@ inline size_t lds_bytes(int hp, int tm) {
     return ((size_t)tm * (hp + 4) + tm * 4 + red_floats(tm)) * 4;
 }
 
-// Mask image row-tile count: independent of the workgroup height, so any RT reads what any RT
-// wrote (row tile = global row / 32; layers strided by ceil(M/128)*4 tiles).
-__host__ __device__ inline int64_t mask_rowtiles(int64_t M) { return ((M + 127) / 128) * 4; }
 
 // Store a layer's C-layout result into the LDS rows (the next layer's A operand) and its ReLU
 // mask bits. Global copies of the rows are written afterwards by copy_rows (coalesced).
@@ -1133,584 +1021,6 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_actor_rows(ActorRowsArgs a) {
 #endif
 }
 
-#if NAV_MLP_PART == 0  // the rest of the learner: main object only
-// ---------------- hidden x hidden weight gradients (split-M partial slabs) ----------------
-// dW_L = dz_L^T h_{L-1} for L = 1 .. nh-1 over the rows of each split. The thin layers' gradients
-// (W0, every bias, Wo, bo) are edge partials of the forward / backward kernels instead.
-struct WgradArgs {
-    MlpDev net[2];          // 1 or 2 networks, same shapes, same input rows
-    int64_t M;
-    const float* in;        // layer-0 input rows: h_0 is recomputed (layer0_unit)
-    int ld_in, in_col;
-    const float* acts[2];   // [nh][M][hp]: saved h_L, 1 <= L <= nh-2
-    const float* dz[2];     // [nh][M][hp]: saved dz_L, 1 <= L <= nh-2
-    const float* dy[2];     // dz_{nh-1} is recomputed: top_unit(dy row, Wo) under the ReLU bit
-    int ld_dy;
-    const uint16_t* masks[2];  // the forward's ReLU bit image
-    float* slabs[2];        // [splits][(nh-1) hp hp]
-    int splits;
-    int TA;                 // 128-wide tiles across hp
-    int n_hid;              // jobs per network = (nh - 1) * TA * TA
-};
-
-constexpr int WG_MC = 32;   // rows per staged chunk
-constexpr int WA_W = 128;   // tile width
-constexpr int WA_LD = 132;  // LDS row stride of the 128-column panels
-#ifndef WG_STAGE0
-#define WG_STAGE0 6         // first MFMA step that stages the next chunk (A/B r01r: 6 over 4, 8)
-#endif
-
-inline size_t wgrad_lds_bytes() { return (size_t)2 * 2 * WG_MC * WA_LD * 4; }
-
-// v if c else 0, per component (a float4-wide select would be lowered through the stack)
-NAV_DEV float4 sel4(bool c, float4 v) {
-    return make_float4(c ? v.x : 0.f, c ? v.y : 0.f, c ? v.z : 0.f, c ? v.w : 0.f);
-}
-
-// One 128x128 tile (tn, tk) of dW_L over the rows of one split: the 4 waves own 64x64 quadrants
-// (2x2 v_mfma_f32_32x32x2_f32 tiles each; the MFMA K dimension is the row index). 32-row chunks
-// of the P (dz_L columns) and Q (h_{L-1} columns) panels are double-buffered in LDS with the next
-// chunk's operands in flight during the current chunk's MFMAs.
-// PR / QR: the panel is recomputed instead of read from a saved [M][hp] tensor — for the top
-// layer dz = top_unit(dy, Wo) under the forward's ReLU bit (8 B of mask words per row and 4
-// columns), for layer 1 h_0 = layer0_unit(x, W0, b0) — the same bits the backward / forward
-// produced, so a 2-hidden-layer network's weight gradient reads no activation tensor at all.
-template <bool FULL, bool PR, bool QR>
-NAV_DEV void wgrad_hidden(const WgradArgs& a, int y, int job, int split, float* smem) {
-    const MlpDev& net = a.net[y];
-    const int hp = net.hp, TA = a.TA, nh = net.n_hidden, d_in = net.d_in, d_out = net.d_out;
-    const int L = job / (TA * TA) + 1;
-    const int tn = (job % (TA * TA)) / TA, tk = job % TA;
-    const int n0 = tn * WA_W, k0 = tk * WA_W;
-    const int64_t M = a.M, MH = M * hp;
-    float* Ps = smem;                      // [2][32][WA_LD]
-    float* Qs = smem + 2 * WG_MC * WA_LD;  // [2][32][WA_LD]
-    const int tid = threadIdx.x, lane = tid & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
-    const int wn = 64 * (wv >> 1), wk = 64 * (wv & 1);
-    // 32x32 sub-tiles inside hp (wave-uniform)
-    const bool n0k = n0 + wn < hp, n1k = n0 + wn + 32 < hp;
-    const bool k0k = k0 + wk < hp, k1k = k0 + wk + 32 < hp;
-    // 32-row aligned splits: a split's mask row tiles start at a tile boundary and every per-row
-    // offset inside the split is a 32-bit product (nav_mlp_wgrad checks the bound); the 64-bit
-    // address math happens once per split
-    const int64_t per = (((M + a.splits - 1) / a.splits) + 31) & ~(int64_t)31;
-    const int64_t m_lo = (int64_t)split * per < M ? (int64_t)split * per : M;
-    const int64_t m_hi = m_lo + per < M ? m_lo + per : M;
-    const int cnt = (int)(m_hi - m_lo);
-    f32x16 acc[2][2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-    // staging: thread = 4 columns from 4*c4 of each panel, rows rr0 + 8 f of the chunk. Every load
-    // comes from a clamped valid address; out-of-range values are zeroed at store time.
-    const int c4 = tid & 31, rr0 = tid >> 5;
-    const int pn = n0 + 4 * c4, qk = k0 + 4 * c4;
-    const bool pc_ok = pn < hp, qc_ok = qk < hp;
-    const int pnc = pc_ok ? pn : 0, qkc = qc_ok ? qk : 0;
-    const float* Pb = a.dz[y] + (PR ? 0 : (int64_t)L * MH + m_lo * hp + pnc);
-    const float* Qb = QR ? a.in + m_lo * a.ld_in + a.in_col
-                         : a.acts[y] + (int64_t)(L - 1) * MH + m_lo * hp + qkc;
-    const int ldp = PR ? a.ld_dy : hp, ldq = QR ? a.ld_in : hp;
-    float wo0[4] = {0.f, 0.f, 0.f, 0.f}, wo1[4] = {0.f, 0.f, 0.f, 0.f};
-    float w0[4][4] = {}, b0[4] = {0.f, 0.f, 0.f, 0.f};
-    const uint16_t* mk = a.masks[y];
-    const int NTm = hp >> 5;
-    if (PR) {
-        const float* Wo = net.params + net.w_off[nh];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            wo0[c] = Wo[pnc + c];
-            wo1[c] = d_out > 1 ? Wo[hp + pnc + c] : 0.f;
-        }
-        mk += (size_t)(nh - 1) * mask_rowtiles(M) * NTm * 64 + mask_idx(m_lo >> 5, NTm, pnc >> 5, pnc & 31);
-        Pb = a.dy[y] + m_lo * a.ld_dy;
-    }
-    if (QR) {
-        const float* W0 = net.params + net.w_off[0];
-        const float* bb = net.params + net.b_off[0];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) w0[c][k] = k < d_in ? W0[(qkc + c) * d_in + k] : 0.f;
-            b0[c] = bb[qkc + c];
-        }
-    }
-    const int g1 = d_out > 1 ? 1 : 0;
-    const int x1 = d_in > 1 ? 1 : 0, x2 = d_in > 2 ? 2 : 0, x3 = d_in > 3 ? 3 : 0;
-    float4 rp[4], rq[4];
-    uint2 rm[4];
-    // r0: the chunk's first row relative to m_lo
-    auto load = [&](int r0) {
-#pragma unroll
-        for (int f = 0; f < 4; ++f) {
-            const int rel = r0 + rr0 + 8 * f;
-            const int rc = rel < cnt ? rel : 0;
-            if (PR) {
-                rm[f] = *reinterpret_cast<const uint2*>(mk + (rc >> 5) * (NTm * 64) +
-                                                        32 * ((rc >> 2) & 1));
-                const float* g = Pb + rc * ldp;
-                rp[f] = make_float4(g[0], g[g1], 0.f, 0.f);
-            } else {
-                rp[f] = *reinterpret_cast<const float4*>(Pb + rc * ldp);
-            }
-            if (QR) {
-                const float* x = Qb + rc * ldq;
-                rq[f] = make_float4(x[0], x[x1], x[x2], x[x3]);
-            } else {
-                rq[f] = *reinterpret_cast<const float4*>(Qb + rc * ldq);
-            }
-        }
-    };
-    // staging of row group f of a chunk into LDS buffer buf, one panel at a time
-    auto storeP = [&](int buf, int r0, int f) {
-        const int r = rr0 + 8 * f;
-        const bool ok = r0 + r < cnt;
-        float4 pv = rp[f];
-        if (PR) {
-            const int rr = ok ? r : 0;  // row within the 32-row tile (r0 is a multiple of 32)
-            const int i = (rr & 3) + 4 * (rr >> 3);  // C-layout element of the row
-            const float gx = rp[f].x, gy = d_out > 1 ? rp[f].y : 0.f;
-            const uint32_t wx = rm[f].x, wy = rm[f].y;
-            pv.x = (wx >> i) & 1u ? top_unit(gx, gy, wo0[0], wo1[0]) : 0.f;
-            pv.y = (wx >> (16 + i)) & 1u ? top_unit(gx, gy, wo0[1], wo1[1]) : 0.f;
-            pv.z = (wy >> i) & 1u ? top_unit(gx, gy, wo0[2], wo1[2]) : 0.f;
-            pv.w = (wy >> (16 + i)) & 1u ? top_unit(gx, gy, wo0[3], wo1[3]) : 0.f;
-        }
-        *reinterpret_cast<float4*>(Ps + (buf * WG_MC + r) * WA_LD + 4 * c4) = sel4(ok && pc_ok, pv);
-    };
-    auto storeQ = [&](int buf, int r0, int f) {
-        const int r = rr0 + 8 * f;
-        const bool ok = r0 + r < cnt;
-        float4 qv = rq[f];
-        if (QR) {
-            float4 x = rq[f];
-            x.y = d_in > 1 ? x.y : 0.f;
-            x.z = d_in > 2 ? x.z : 0.f;
-            x.w = d_in > 3 ? x.w : 0.f;
-            qv.x = layer0_unit(x, w0[0][0], w0[0][1], w0[0][2], w0[0][3], b0[0]);
-            qv.y = layer0_unit(x, w0[1][0], w0[1][1], w0[1][2], w0[1][3], b0[1]);
-            qv.z = layer0_unit(x, w0[2][0], w0[2][1], w0[2][2], w0[2][3], b0[2]);
-            qv.w = layer0_unit(x, w0[3][0], w0[3][1], w0[3][2], w0[3][3], b0[3]);
-        }
-        *reinterpret_cast<float4*>(Qs + (buf * WG_MC + r) * WA_LD + 4 * c4) = sel4(ok && qc_ok, qv);
-    };
-    const int nch = (cnt + WG_MC - 1) / WG_MC;
-    if (nch > 0) {
-        load(0);
-#pragma unroll
-        for (int f = 0; f < 4; ++f) {
-            storeP(0, 0, f);
-            storeQ(0, 0, f);
-        }
-    }
-    __syncthreads();
-    for (int c = 0; c < nch; ++c) {
-        const bool more = c + 1 < nch;
-        const int mn = (c + 1) * WG_MC;
-        if (FULL || more) load(mn);  // rows past m_hi load clamped addresses
-        const int buf = c & 1;
-        const float* pb = Ps + buf * WG_MC * WA_LD;
-        const float* qb = Qs + buf * WG_MC * WA_LD;
-        __builtin_amdgcn_sched_barrier(0);
-        if (FULL) {
-            // branch-free: step s+1's operands are read before step s's 4 MFMAs; steps 4..11 also
-            // stage one (row group, panel) piece of the NEXT chunk into the other buffer, whose
-            // VALU / LDS work issues in the MFMAs' shadow instead of after the chunk
-            const float* pw = pb + h * WA_LD + wn + l32;
-            const float* qw = qb + h * WA_LD + wk + l32;
-            float a0 = pw[0], a1 = pw[32], bq0 = qw[0], bq1 = qw[32];
-#pragma unroll
-            for (int st = 0; st < WG_MC / 2; ++st) {
-                float a0n = 0.f, a1n = 0.f, b0n = 0.f, b1n = 0.f;
-                if (st + 1 < WG_MC / 2) {
-                    const int o = 2 * (st + 1) * WA_LD;
-                    a0n = pw[o];
-                    a1n = pw[o + 32];
-                    b0n = qw[o];
-                    b1n = qw[o + 32];
-                }
-                __builtin_amdgcn_sched_barrier(0);
-                acc[0][0] = mfma(a0, bq0, acc[0][0]);
-                acc[0][1] = mfma(a0, bq1, acc[0][1]);
-                acc[1][0] = mfma(a1, bq0, acc[1][0]);
-                acc[1][1] = mfma(a1, bq1, acc[1][1]);
-                if (st >= WG_STAGE0 && st < WG_STAGE0 + 8) {
-                    // unconditional (the last chunk stages clamped rows into the idle buffer), so
-                    // the piece shares the MFMAs' basic block: MFMA / VALU interleaved
-                    if ((st & 1) == 0) storeP(buf ^ 1, mn, (st - WG_STAGE0) >> 1);
-                    else storeQ(buf ^ 1, mn, (st - WG_STAGE0) >> 1);
-#pragma unroll
-                    for (int g = 0; g < 4; ++g) {
-                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
-                        __builtin_amdgcn_sched_group_barrier(0x002, 12, 0);  // up to 12 VALU
-                    }
-                    __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);       // the ds_write
-                }
-                __builtin_amdgcn_sched_barrier(0);
-                a0 = a0n; a1 = a1n; bq0 = b0n; bq1 = b1n;
-            }
-        } else {
-#pragma unroll
-            for (int st = 0; st < WG_MC / 2; ++st) {
-                const int row = 2 * st + h;
-                const float a0 = pb[row * WA_LD + wn + l32], a1 = pb[row * WA_LD + wn + 32 + l32];
-                const float bq0 = qb[row * WA_LD + wk + l32], bq1 = qb[row * WA_LD + wk + 32 + l32];
-                if (n0k && k0k) acc[0][0] = mfma(a0, bq0, acc[0][0]);
-                if (n0k && k1k) acc[0][1] = mfma(a0, bq1, acc[0][1]);
-                if (n1k && k0k) acc[1][0] = mfma(a1, bq0, acc[1][0]);
-                if (n1k && k1k) acc[1][1] = mfma(a1, bq1, acc[1][1]);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            if (more) {
-#pragma unroll
-                for (int f = 0; f < 4; ++f) {
-                    storeP(buf ^ 1, mn, f);
-                    storeQ(buf ^ 1, mn, f);
-                }
-            }
-        }
-        __syncthreads();
-    }
-    float* o = a.slabs[y] + (int64_t)split * hidden_w_count(net) + (int64_t)(L - 1) * hp * hp;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            if (!((i ? n1k : n0k) && (j ? k1k : k0k))) continue;
-            const int nb = n0 + wn + 32 * i, kb = k0 + wk + 32 * j;
-#pragma unroll
-            for (int e = 0; e < 16; ++e) o[(int64_t)(nb + acc_row(e, h)) * hp + kb + l32] = acc[i][j][e];
-        }
-}
-
-// One launch per network: the 1-D grid lists the hidden-layer 128x128 tiles of every row split.
-// Which operand is recomputed depends on the layer (top: P, layer 1: Q), chosen per block.
-__global__ __launch_bounds__(kBlock) void k_wgrad(WgradArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int per_net = a.n_hid * a.splits;
-    const int y = (int)blockIdx.x / per_net, b = (int)blockIdx.x % per_net;
-    const int job = b % a.n_hid, split = b / a.n_hid;
-    const int TA = a.TA, t = job % (TA * TA);
-    const int L = job / (TA * TA) + 1, nh = a.net[0].n_hidden, hp = a.net[0].hp;
-    // tiles entirely inside hp take the branch-free MFMA body
-    const bool full = (t / TA + 1) * WA_W <= hp && (t % TA + 1) * WA_W <= hp;
-    const bool pr = L == nh - 1, qr = L == 1;
-#define NAV_WG(F)                                                                       \
-    if (pr && qr) wgrad_hidden<F, true, true>(a, y, job, split, smem);                     \
-    else if (pr) wgrad_hidden<F, true, false>(a, y, job, split, smem);                     \
-    else if (qr) wgrad_hidden<F, false, true>(a, y, job, split, smem);                     \
-    else wgrad_hidden<F, false, false>(a, y, job, split, smem);
-    if (full) {
-        NAV_WG(true)
-    } else {
-        NAV_WG(false)
-    }
-#undef NAV_WG
-}
-
-// ---------------- optimizer / target update, refreshing the packed images ----------------
-struct PackInfo {
-    int hp, n_hidden;
-    int64_t w_off[kMaxLayers];
-    float* packed;
-};
-
-NAV_DEV void repack(const PackInfo& pk, int64_t i, float4 v) {
-    // i = flat float index of v.x (multiple of 4)
-    for (int L = 1; L < pk.n_hidden; ++L) {
-        const int64_t off = pk.w_off[L], sz = (int64_t)pk.hp * pk.hp;
-        if (i >= off && i < off + sz) {
-            const int64_t e = i - off;
-            const int n = (int)(e / pk.hp), k = (int)(e % pk.hp);
-            float* Wf = pk.packed + (int64_t)(L - 1) * 2 * sz;
-            float* Wb = Wf + sz;
-            *reinterpret_cast<float4*>(Wf + ((int64_t)(k >> 2) * pk.hp + n) * 4) = v;
-            float* d = Wb + ((int64_t)(n >> 2) * pk.hp + k) * 4 + (n & 3);
-            d[0] = v.x; d[4] = v.y; d[8] = v.z; d[12] = v.w;
-            return;
-        }
-    }
-}
-
-NAV_DEV float adam1(float& p, float g, float& m, float& v, float b1w, float b2, float omb2,
-                    float eps, float step_size, float bc2s) {
-    // torch 2.10 _single_tensor_adam: m.lerp_(g, 1-b1); v.mul_(b2).addcmul_(g, g, 1-b2);
-    // denom = v.sqrt()/bc2_sqrt + eps; p.addcdiv_(m, denom, -step_size)
-    m = fmaf(b1w, g - m, m);
-    v = v * b2 + (omb2 * g) * g;
-    const float denom = sqrtf(v) / bc2s + eps;
-    p = p + (-step_size) * (m / denom);
-    return p;
-}
-
-// ---------------- gradient reduce (+ fused Adam) ----------------
-// grad = hidden-W entries: sum of the weight-gradient split slabs (block = 64 float4 columns x 4
-// split groups, the group sums added in order through LDS); every other entry: sum of the
-// per-row-block edge slabs (one wave per float4, lanes take blocks b = lane, lane + 64, ..., a
-// fixed xor tree adds the lanes). Deterministic: the same order on every run. With ADAM the
-// finished gradient goes straight into torch's Adam update (robot.py:236-239) of the parameter
-// it belongs to and the packed MFMA images are refreshed; up to 2 networks per launch.
-struct RedNet {
-    MlpDev net;
-    const float4* hs;
-    const float4* es;
-    float4* grad;  // nullable with ADAM
-    float4* p;
-    float4* m;
-    float4* v;
-    float step_size, bc2s;
-    PackInfo pk;
-    int nbh, nbe;
-};
-
-struct RedArgs {
-    RedNet n[2];
-    int splits;
-    int64_t nblk;
-    float b1w, b2, omb2, eps;
-};
-
-template <bool ADAM>
-NAV_DEV void red_out(const RedArgs& a, const RedNet& rn, int64_t flat4, float4 g) {
-    if (rn.grad) rn.grad[flat4] = g;
-    if (!ADAM) return;
-    float4 pp = rn.p[flat4], mm = rn.m[flat4], vv = rn.v[flat4];
-    adam1(pp.x, g.x, mm.x, vv.x, a.b1w, a.b2, a.omb2, a.eps, rn.step_size, rn.bc2s);
-    adam1(pp.y, g.y, mm.y, vv.y, a.b1w, a.b2, a.omb2, a.eps, rn.step_size, rn.bc2s);
-    adam1(pp.z, g.z, mm.z, vv.z, a.b1w, a.b2, a.omb2, a.eps, rn.step_size, rn.bc2s);
-    adam1(pp.w, g.w, mm.w, vv.w, a.b1w, a.b2, a.omb2, a.eps, rn.step_size, rn.bc2s);
-    rn.p[flat4] = pp;
-    rn.m[flat4] = mm;
-    rn.v[flat4] = vv;
-    if (rn.pk.packed) repack(rn.pk, flat4 * 4, pp);
-}
-
-template <bool ADAM>
-__global__ __launch_bounds__(kBlock) void k_grad_reduce(RedArgs a) {
-    __shared__ float4 part[4][64];
-    const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
-    int b = blockIdx.x;
-    const bool second = b >= a.n[0].nbh + a.n[0].nbe;
-    const RedNet& rn = second ? a.n[1] : a.n[0];
-    if (second) b -= a.n[0].nbh + a.n[0].nbe;
-    const MlpDev& net = rn.net;
-    if (b < rn.nbh) {
-        const int64_t hw4 = hidden_w_count(net) / 4;
-        const int64_t i = (int64_t)b * 64 + c;
-        float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (i < hw4) {
-#pragma unroll 4
-            for (int k = g; k < a.splits; k += 4) {
-                const float4 v = rn.hs[(int64_t)k * hw4 + i];
-                s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-            }
-        }
-        part[g][c] = s;
-        __syncthreads();
-        if (g != 0 || i >= hw4) return;
-        float4 r = part[0][c];
-#pragma unroll
-        for (int q = 1; q < 4; ++q) {
-            r.x += part[q][c].x; r.y += part[q][c].y; r.z += part[q][c].z; r.w += part[q][c].w;
-        }
-        const int64_t per = (int64_t)net.hp * net.hp / 4;
-        const int L = (int)(i / per) + 1;
-        red_out<ADAM>(a, rn, net.w_off[L] / 4 + i % per, r);
-        return;
-    }
-    const int64_t e4 = edge_count(net) / 4;
-    const int64_t o = (int64_t)(b - rn.nbh) * 4 + g;
-    if (o >= e4) return;  // wave-uniform
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int64_t k = c; k < a.nblk; k += 64) {
-        const float4 v = rn.es[k * e4 + o];
-        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-    }
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) {
-        s.x += __shfl_xor(s.x, d, 64);
-        s.y += __shfl_xor(s.y, d, 64);
-        s.z += __shfl_xor(s.z, d, 64);
-        s.w += __shfl_xor(s.w, d, 64);
-    }
-    if (c == 0) red_out<ADAM>(a, rn, edge_to_flat(net, 4 * o) / 4, s);
-}
-
-// robot.py:293-310 soft update of up to 4 (target, source) pairs in one launch
-struct PolyPair {
-    float4* t;
-    const float4* s;
-    int64_t n4;
-    PackInfo pk;
-};
-struct PolyArgs {
-    PolyPair q[4];
-    int n;
-    int64_t total4;
-    float omt, tau;
-};
-
-__global__ __launch_bounds__(kBlock) void k_adam(float4* __restrict__ p,
-                                                 const float4* __restrict__ g, float4* m,
-                                                 float4* v, int64_t n4, float b1w, float b2,
-                                                 float omb2, float eps, float ss, float bc2s,
-                                                 PackInfo pk) {
-    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n4;
-         i += (int64_t)gridDim.x * kBlock) {
-        float4 pp = p[i], gg = g[i], mm = m[i], vv = v[i];
-        adam1(pp.x, gg.x, mm.x, vv.x, b1w, b2, omb2, eps, ss, bc2s);
-        adam1(pp.y, gg.y, mm.y, vv.y, b1w, b2, omb2, eps, ss, bc2s);
-        adam1(pp.z, gg.z, mm.z, vv.z, b1w, b2, omb2, eps, ss, bc2s);
-        adam1(pp.w, gg.w, mm.w, vv.w, b1w, b2, omb2, eps, ss, bc2s);
-        p[i] = pp; m[i] = mm; v[i] = vv;
-        if (pk.packed) repack(pk, i * 4, pp);
-    }
-}
-
-// torch.optim.Adam of up to 2 networks in one launch from flat gradients that a collective
-// produced (shared policy: the SUM all-reduce of the bucket); g / grad_div is the averaged
-// gradient (grad_div 1: the plain step, bit-identical to k_adam).
-struct AdamNet {
-    float4* p;
-    const float4* g;
-    float4* m;
-    float4* v;
-    int64_t n4;
-    float step_size, bc2s;
-    PackInfo pk;
-};
-struct AdamArgs {
-    AdamNet q[2];
-    int n;
-    int64_t total4;
-    float b1w, b2, omb2, eps, gdiv;
-};
-
-__global__ __launch_bounds__(kBlock) void k_adam_multi(AdamArgs a) {
-    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < a.total4;
-         i += (int64_t)gridDim.x * kBlock) {
-        const bool second = a.n > 1 && i >= a.q[0].n4;
-        const AdamNet& q = second ? a.q[1] : a.q[0];
-        const int64_t j = second ? i - a.q[0].n4 : i;
-        float4 pp = q.p[j], gg = q.g[j], mm = q.m[j], vv = q.v[j];
-        gg.x = gg.x / a.gdiv; gg.y = gg.y / a.gdiv; gg.z = gg.z / a.gdiv; gg.w = gg.w / a.gdiv;
-        adam1(pp.x, gg.x, mm.x, vv.x, a.b1w, a.b2, a.omb2, a.eps, q.step_size, q.bc2s);
-        adam1(pp.y, gg.y, mm.y, vv.y, a.b1w, a.b2, a.omb2, a.eps, q.step_size, q.bc2s);
-        adam1(pp.z, gg.z, mm.z, vv.z, a.b1w, a.b2, a.omb2, a.eps, q.step_size, q.bc2s);
-        adam1(pp.w, gg.w, mm.w, vv.w, a.b1w, a.b2, a.omb2, a.eps, q.step_size, q.bc2s);
-        q.p[j] = pp; q.m[j] = mm; q.v[j] = vv;
-        if (q.pk.packed) repack(q.pk, j * 4, pp);
-    }
-}
-
-__global__ __launch_bounds__(kBlock) void k_polyak(float4* __restrict__ t,
-                                                   const float4* __restrict__ s, int64_t n4,
-                                                   float omt, float tau, PackInfo pk) {
-    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n4;
-         i += (int64_t)gridDim.x * kBlock) {
-        float4 a = t[i];
-        const float4 b = s[i];
-        // robot.py:309 target*(1-tau) + source*tau (two products, one sum)
-        a.x = a.x * omt + b.x * tau;
-        a.y = a.y * omt + b.y * tau;
-        a.z = a.z * omt + b.z * tau;
-        a.w = a.w * omt + b.w * tau;
-        t[i] = a;
-        if (pk.packed) repack(pk, i * 4, a);
-    }
-}
-
-__global__ __launch_bounds__(kBlock) void k_polyak_multi(PolyArgs a) {
-    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < a.total4;
-         i += (int64_t)gridDim.x * kBlock) {
-        int64_t j = i;
-        int k = 0;
-        while (k < a.n - 1 && j >= a.q[k].n4) j -= a.q[k++].n4;
-        const PolyPair& q = a.q[k];
-        float4 t = q.t[j];
-        const float4 s = q.s[j];
-        // robot.py:309 target*(1-tau) + source*tau (two products, one sum)
-        t.x = t.x * a.omt + s.x * a.tau;
-        t.y = t.y * a.omt + s.y * a.tau;
-        t.z = t.z * a.omt + s.z * a.tau;
-        t.w = t.w * a.omt + s.w * a.tau;
-        q.t[j] = t;
-        if (q.pk.packed) repack(q.pk, j * 4, t);
-    }
-}
-
-__global__ __launch_bounds__(kBlock) void k_pack(const float4* __restrict__ p, int64_t n4,
-                                                 PackInfo pk) {
-    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n4;
-         i += (int64_t)gridDim.x * kBlock)
-        repack(pk, i * 4, p[i]);
-}
-
-// ---------------- TD3 glue ----------------
-__global__ __launch_bounds__(kBlock) void k_replay_sample(const float4* __restrict__ rows,
-                                                          int64_t size, int64_t B,
-                                                          const int64_t* __restrict__ idx,
-                                                          uint32_t s0, uint32_t s1, uint32_t ctr,
-                                                          float4* __restrict__ batch) {
-    const int64_t b = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (b >= B) return;
-    int64_t k;
-    if (idx) {
-        k = idx[b];
-    } else {
-        const uint4 w = philox((uint32_t)b, 0u, NAV_TAG_SAMPLE, ctr, s0, s1);
-        k = (int64_t)(((uint64_t)w.x * (uint64_t)size) >> 32);
-    }
-    batch[2 * b] = rows[2 * k];
-    batch[2 * b + 1] = rows[2 * k + 1];
-}
-
-__global__ __launch_bounds__(kBlock) void k_fill(float* x, int64_t n, float v) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i < n) x[i] = v;
-}
-
-__global__ __launch_bounds__(kBlock) void k_strided_copy(const float* __restrict__ src, int lds,
-                                                         int cs, float* __restrict__ dst, int ldd,
-                                                         int cd, int64_t rows, int cols) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= rows * cols) return;
-    const int64_t r = i / cols;
-    const int c = (int)(i % cols);
-    dst[r * ldd + cd + c] = src[r * lds + cs + c];
-}
-
-inline int blocks_for(int64_t n) { return (int)((n + kBlock - 1) / kBlock); }
-inline int grid_stride_blocks(int64_t n) {
-    const int64_t b = (n + kBlock - 1) / kBlock;
-    return (int)(b < 2048 ? (b > 0 ? b : 1) : 2048);
-}
-
-PackInfo pack_info(const MlpDev& d, float* packed) {
-    PackInfo pk;
-    pk.hp = d.hp;
-    pk.n_hidden = d.n_hidden;
-    for (int l = 0; l < kMaxLayers; ++l) pk.w_off[l] = l <= d.n_hidden ? d.w_off[l] : 0;
-    pk.packed = d.n_hidden > 1 ? packed : nullptr;
-    return pk;
-}
-
-bool red_net(const nav_mlp* net, const float* hs, int splits, const float* es, float* grad,
-             RedNet* rn) {
-    if (!make_dev(net, &rn->net)) return false;
-    if (rn->net.n_hidden > 1 && (!hs || splits < 1)) return false;
-    rn->hs = reinterpret_cast<const float4*>(hs);
-    rn->es = reinterpret_cast<const float4*>(es);
-    rn->grad = reinterpret_cast<float4*>(grad);
-    rn->nbh = (int)((hidden_w_count(rn->net) / 4 + 63) / 64);
-    rn->nbe = (int)((edge_count(rn->net) / 4 + 3) / 4);
-    return true;
-}
-
-#endif  // NAV_MLP_PART == 0
 
 // ---- launch helpers (template dispatch on NT = hp / 32 and RT = rows / 32) ----
 // Workgroup height: RT = 4 (128 rows, one workgroup per CU) or RT = 2 (64 rows, two per CU so one
@@ -2147,256 +1457,6 @@ int nav_mlp_backward(const nav_mlp* nets, int32_t n_nets, int64_t M, const float
     a.save_mask = save_mask;
     a.ecount = edge_count(a.net[0]);
     return launch_bwd(a, n_nets, S(stream));
-}
-
-int nav_mlp_wgrad(const nav_mlp* nets, int32_t n_nets, int64_t M, const float* in,
-                  int32_t ld_in, int32_t in_col, const float* const* acts,
-                  const float* const* dz, const float* const* dy, int32_t ld_dy,
-                  const uint16_t* const* masks, float* const* slabs, int32_t splits,
-                  void* stream) {
-    WgradArgs a{};
-    if (!nets || n_nets < 1 || n_nets > 2 || M < 1 || splits < 1 || !in || !dy || ld_dy < 0 ||
-        !masks || !slabs)
-        return NAV_EINVAL;
-    for (int i = 0; i < n_nets; ++i) {
-        if (!make_dev(&nets[i], &a.net[i]) || !dy[i] || !masks[i] || !slabs[i]) return NAV_EINVAL;
-        if (a.net[i].hp != a.net[0].hp || a.net[i].d_in != a.net[0].d_in ||
-            a.net[i].n_hidden != a.net[0].n_hidden || a.net[i].d_out != a.net[0].d_out)
-            return NAV_EINVAL;
-        a.acts[i] = acts ? acts[i] : nullptr;
-        a.dz[i] = dz ? dz[i] : nullptr;
-        if (a.net[i].n_hidden > 2 && (!a.acts[i] || !a.dz[i])) return NAV_EINVAL;
-        a.dy[i] = dy[i];
-        a.masks[i] = masks[i];
-        a.slabs[i] = slabs[i];
-    }
-    if (in_col < 0 || in_col + a.net[0].d_in > ld_in) return NAV_EINVAL;
-    if (a.net[0].n_hidden < 2) return 0;
-    {   // per-split row offsets are 32-bit inside the kernel
-        const int64_t per = (((M + splits - 1) / splits) + 31) & ~(int64_t)31;
-        int64_t ld = ld_in > ld_dy ? ld_in : ld_dy;
-        ld = ld > a.net[0].hp ? ld : a.net[0].hp;
-        if (per * ld >= ((int64_t)1 << 31) || (per / 32) * a.net[0].hp * 2 >= ((int64_t)1 << 31))
-            return NAV_EINVAL;
-    }
-    a.M = M;
-    a.in = in;
-    a.ld_in = ld_in;
-    a.in_col = in_col;
-    a.ld_dy = ld_dy;
-    a.splits = splits;
-    a.TA = (a.net[0].hp + WA_W - 1) / WA_W;
-    a.n_hid = (a.net[0].n_hidden - 1) * a.TA * a.TA;
-    const size_t lds = wgrad_lds_bytes();
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wgrad),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(k_wgrad, dim3((unsigned)(n_nets * a.n_hid * splits)), dim3(kBlock), lds,
-                       S(stream), a);
-    NAV_CHECK_LAUNCH();
-    return 0;
-}
-
-int nav_grad_reduce(const nav_mlp* net, const float* hidden_slabs, int32_t splits,
-                    const float* edge_slabs, int64_t edge_blocks, float* grad, void* stream) {
-    RedArgs a{};
-    if (!grad || !edge_slabs || edge_blocks < 1 || splits < 0 ||
-        !red_net(net, hidden_slabs, splits, edge_slabs, grad, &a.n[0]))
-        return NAV_EINVAL;
-    a.splits = splits;
-    a.nblk = edge_blocks;
-    hipLaunchKernelGGL(k_grad_reduce<false>, dim3((unsigned)(a.n[0].nbh + a.n[0].nbe)),
-                       dim3(kBlock), 0, S(stream), a);
-    NAV_CHECK_LAUNCH();
-    return 0;
-}
-
-int nav_grad_reduce_multi(const nav_mlp* nets, int32_t n_nets, const float* const* hidden_slabs,
-                          int32_t splits, const float* const* edge_slabs, int64_t edge_blocks,
-                          float* const* grads, void* stream) {
-    RedArgs a{};
-    if (!nets || n_nets < 1 || n_nets > 2 || !hidden_slabs || !edge_slabs || edge_blocks < 1 ||
-        splits < 0 || !grads)
-        return NAV_EINVAL;
-    int blocks = 0;
-    for (int i = 0; i < n_nets; ++i) {
-        if (!edge_slabs[i] || !grads[i] ||
-            !red_net(&nets[i], hidden_slabs[i], splits, edge_slabs[i], grads[i], &a.n[i]))
-            return NAV_EINVAL;
-        if (a.n[i].net.hp != a.n[0].net.hp || a.n[i].net.n_hidden != a.n[0].net.n_hidden)
-            return NAV_EINVAL;
-        blocks += a.n[i].nbh + a.n[i].nbe;
-    }
-    a.splits = splits;
-    a.nblk = edge_blocks;
-    hipLaunchKernelGGL(k_grad_reduce<false>, dim3((unsigned)blocks), dim3(kBlock), 0, S(stream),
-                       a);
-    NAV_CHECK_LAUNCH();
-    return 0;
-}
-
-int nav_adam_multi(const nav_mlp* nets, int32_t n_nets, const float* const* grads,
-                   float* const* m, float* const* v, float beta1, float beta2, float eps,
-                   const float* step_size, const float* bc2_sqrt, float grad_div, void* stream) {
-    AdamArgs a{};
-    if (!nets || n_nets < 1 || n_nets > 2 || !grads || !m || !v || !step_size || !bc2_sqrt ||
-        !(grad_div > 0.f))
-        return NAV_EINVAL;
-    for (int i = 0; i < n_nets; ++i) {
-        MlpDev d;
-        if (!make_dev(&nets[i], &d) || !grads[i] || !m[i] || !v[i]) return NAV_EINVAL;
-        AdamNet& q = a.q[i];
-        q.p = reinterpret_cast<float4*>(nets[i].params);
-        q.g = reinterpret_cast<const float4*>(grads[i]);
-        q.m = reinterpret_cast<float4*>(m[i]);
-        q.v = reinterpret_cast<float4*>(v[i]);
-        q.n4 = d.count / 4;
-        q.step_size = step_size[i];
-        q.bc2s = bc2_sqrt[i];
-        q.pk = pack_info(d, nets[i].packed);
-        a.total4 += q.n4;
-    }
-    a.n = n_nets;
-    a.b1w = 1.0f - beta1;
-    a.b2 = beta2;
-    a.omb2 = 1.0f - beta2;
-    a.eps = eps;
-    a.gdiv = grad_div;
-    hipLaunchKernelGGL(k_adam_multi, dim3(grid_stride_blocks(a.total4)), dim3(kBlock), 0,
-                       S(stream), a);
-    NAV_CHECK_LAUNCH();
-    return 0;
-}
-
-int nav_grad_reduce_adam(const nav_mlp* nets, int32_t n_nets, const float* const* hidden_slabs,
-                         int32_t splits, const float* const* edge_slabs, int64_t edge_blocks,
-                         float* const* grads, float* const* m, float* const* v, float beta1,
-                         float beta2, float eps, const float* step_size, const float* bc2_sqrt,
-                         void* stream) {
-    RedArgs a{};
-    if (!nets || n_nets < 1 || n_nets > 2 || !hidden_slabs || !edge_slabs || edge_blocks < 1 ||
-        splits < 0 || !m || !v || !step_size || !bc2_sqrt)
-        return NAV_EINVAL;
-    int blocks = 0;
-    for (int i = 0; i < n_nets; ++i) {
-        RedNet& rn = a.n[i];
-        if (!edge_slabs[i] || !m[i] || !v[i] ||
-            !red_net(&nets[i], hidden_slabs[i], splits, edge_slabs[i], grads ? grads[i] : nullptr,
-                     &rn))
-            return NAV_EINVAL;
-        rn.p = reinterpret_cast<float4*>(nets[i].params);
-        rn.m = reinterpret_cast<float4*>(m[i]);
-        rn.v = reinterpret_cast<float4*>(v[i]);
-        rn.step_size = step_size[i];
-        rn.bc2s = bc2_sqrt[i];
-        rn.pk = pack_info(rn.net, nets[i].packed);
-        blocks += rn.nbh + rn.nbe;
-    }
-    a.splits = splits;
-    a.nblk = edge_blocks;
-    a.b1w = 1.0f - beta1;
-    a.b2 = beta2;
-    a.omb2 = 1.0f - beta2;
-    a.eps = eps;
-    hipLaunchKernelGGL(k_grad_reduce<true>, dim3((unsigned)blocks), dim3(kBlock), 0, S(stream),
-                       a);
-    NAV_CHECK_LAUNCH();
-    return 0;
-}
-
-int nav_polyak_multi(const nav_mlp* targets, const nav_mlp* sources, int32_t n, float tau,
-                     void* stream) {
-    PolyArgs a{};
-    if (!targets || !sources || n < 1 || n > 4) return NAV_EINVAL;
-    for (int i = 0; i < n; ++i) {
-        MlpDev dt, ds;
-        if (!make_dev(&targets[i], &dt) || !make_dev(&sources[i], &ds) || dt.count != ds.count ||
-            dt.hp != ds.hp || dt.n_hidden != ds.n_hidden)
-            return NAV_EINVAL;
-        a.q[i].t = reinterpret_cast<float4*>(targets[i].params);
-        a.q[i].s = reinterpret_cast<const float4*>(sources[i].params);
-        a.q[i].n4 = dt.count / 4;
-        a.q[i].pk = pack_info(dt, targets[i].packed);
-        a.total4 += a.q[i].n4;
-    }
-    a.n = n;
-    a.omt = 1.0f - tau;
-    a.tau = tau;
-    hipLaunchKernelGGL(k_polyak_multi, dim3(grid_stride_blocks(a.total4)), dim3(kBlock), 0,
-                       S(stream), a);
-    NAV_CHECK_LAUNCH();
-    return 0;
-}
-
-int nav_adam(const nav_mlp* net, const float* grad, float* m, float* v, float beta1, float beta2,
-             float eps, float step_size, float bc2_sqrt, void* stream) {
-    MlpDev d;
-    if (!make_dev(net, &d) || !grad || !m || !v) return NAV_EINVAL;
-    const int64_t n4 = d.count / 4;
-    hipLaunchKernelGGL(k_adam, dim3(grid_stride_blocks(n4)), dim3(kBlock), 0, S(stream),
-                       reinterpret_cast<float4*>(net->params),
-                       reinterpret_cast<const float4*>(grad), reinterpret_cast<float4*>(m),
-                       reinterpret_cast<float4*>(v), n4, 1.0f - beta1, beta2, 1.0f - beta2, eps,
-                       step_size, bc2_sqrt, pack_info(d, net->packed));
-    NAV_CHECK_LAUNCH();
-    return 0;
-}
-
-int nav_polyak(const nav_mlp* target, const nav_mlp* source, float tau, void* stream) {
-    MlpDev dt, ds;
-    if (!make_dev(target, &dt) || !make_dev(source, &ds) || dt.count != ds.count ||
-        dt.hp != ds.hp || dt.n_hidden != ds.n_hidden)
-        return NAV_EINVAL;
-    const int64_t n4 = dt.count / 4;
-    hipLaunchKernelGGL(k_polyak, dim3(grid_stride_blocks(n4)), dim3(kBlock), 0, S(stream),
-                       reinterpret_cast<float4*>(target->params),
-                       reinterpret_cast<const float4*>(source->params), n4, 1.0f - tau, tau,
-                       pack_info(dt, target->packed));
-    NAV_CHECK_LAUNCH();
-    return 0;
-}
-
-int nav_mlp_pack(const nav_mlp* net, void* stream) {
-    MlpDev d;
-    if (!make_dev(net, &d)) return NAV_EINVAL;
-    if (d.n_hidden < 2) return 0;
-    const int64_t n4 = d.count / 4;
-    hipLaunchKernelGGL(k_pack, dim3(grid_stride_blocks(n4)), dim3(kBlock), 0, S(stream),
-                       reinterpret_cast<const float4*>(net->params), n4,
-                       pack_info(d, net->packed));
-    NAV_CHECK_LAUNCH();
-    return 0;
-}
-
-int nav_replay_sample(const nav_replay* replay, int64_t size, int64_t B, const int64_t* idx,
-                      uint32_t seed_lo, uint32_t seed_hi, uint32_t counter, float* batch,
-                      void* stream) {
-    if (!replay || !replay->rows || size < 1 || size > replay->capacity ||
-        size > ((int64_t)1 << 32) || B < 0 || !batch)
-        return NAV_EINVAL;
-    if (B == 0) return 0;
-    hipLaunchKernelGGL(k_replay_sample, dim3(blocks_for(B)), dim3(kBlock), 0, S(stream),
-                       reinterpret_cast<const float4*>(replay->rows), size, B, idx, seed_lo,
-                       seed_hi, counter, reinterpret_cast<float4*>(batch));
-    NAV_CHECK_LAUNCH();
-    return 0;
-}
-
-int nav_fill(float* x, int64_t n, float value, void* stream) {
-    if (n < 0 || (n && !x)) return NAV_EINVAL;
-    if (n == 0) return 0;
-    hipLaunchKernelGGL(k_fill, dim3(blocks_for(n)), dim3(kBlock), 0, S(stream), x, n, value);
-    NAV_CHECK_LAUNCH();
-    return 0;
-}
-
-int nav_strided_copy(const float* src, int32_t ld_src, int32_t col_src, float* dst,
-                     int32_t ld_dst, int32_t col_dst, int64_t rows, int32_t cols, void* stream) {
-    if (rows < 0 || cols < 0 || (rows && cols && (!src || !dst))) return NAV_EINVAL;
-    if (rows == 0 || cols == 0) return 0;
-    hipLaunchKernelGGL(k_strided_copy, dim3(blocks_for(rows * cols)), dim3(kBlock), 0, S(stream),
-                       src, ld_src, col_src, dst, ld_dst, col_dst, rows, cols);
-    NAV_CHECK_LAUNCH();
-    return 0;
 }
 
 }  // extern "C"

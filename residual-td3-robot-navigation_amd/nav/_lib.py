@@ -116,6 +116,7 @@ SIGNATURES = [
     ("nav_mlp_wgrad", C.c_int, [_P(NavMlp), C.c_int32, C.c_int64, _vp, C.c_int32, C.c_int32,
                                 _P(_vp), _P(_vp), _P(_vp), C.c_int32, _P(_vp), _P(_vp), C.c_int32,
                                 _vp]),
+    ("nav_mlp_wgrad_splits", C.c_int32, [C.c_int32, C.c_int32, C.c_int32, C.c_int64]),
     ("nav_grad_reduce", C.c_int, [_P(NavMlp), _vp, C.c_int32, _vp, C.c_int64, _vp, _vp]),
     ("nav_grad_reduce_adam", C.c_int, [_P(NavMlp), C.c_int32, _P(_vp), C.c_int32, _P(_vp),
                                        C.c_int64, _P(_vp), _P(_vp), _P(_vp), C.c_float, C.c_float,
@@ -143,7 +144,8 @@ SIGNATURES = [
 
 # Entry points that return int64 counts (negative = error) rather than a status code.
 _COUNT_FNS = {"nav_mlp_param_count", "nav_mlp_packed_count", "nav_mlp_mask_count",
-              "nav_mlp_row_blocks", "nav_mlp_edge_count", "nav_mlp_hidden_count"}
+              "nav_mlp_row_blocks", "nav_mlp_edge_count", "nav_mlp_hidden_count",
+              "nav_mlp_wgrad_splits"}
 
 
 class NavError(RuntimeError):
@@ -156,11 +158,12 @@ class _Checked:
 
     def __call__(self, *args):
         r = self.fn(*args)
-        if self.fn.restype is C.c_int and r != 0 and self.name != "nav_abi_version":
+        if self.name in _COUNT_FNS:
+            if r < 0:
+                raise NavError(f"{self.name}: invalid argument")
+        elif self.fn.restype is C.c_int and r != 0 and self.name != "nav_abi_version":
             what = "invalid argument" if r == NAV_EINVAL else f"HIP error {-r}"
             raise NavError(f"{self.name} failed: {what}")
-        if self.name in _COUNT_FNS and r < 0:
-            raise NavError(f"{self.name}: invalid argument")
         return r
 
 

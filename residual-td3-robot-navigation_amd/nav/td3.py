@@ -104,8 +104,10 @@ class TD3:
         self.eslab1, self.eslab2 = f(self.nblk, ec), f(self.nblk, ec)
         self.eslab_a = f(self.nblk, L.nav_mlp_edge_count(2, 2, hp, nh))
         # row splits of the weight-gradient launch (partial slabs): critic twins and actor
-        # separately (NAV_WGRAD_SPLITS="critic,actor" overrides; tuning only)
-        sc = sa = max(1, min(64, B // 512))
+        # separately, as many as fill the chip (NAV_WGRAD_SPLITS="critic,actor" overrides;
+        # tuning only)
+        sc = L.nav_mlp_wgrad_splits(2, hp, nh, B)
+        sa = L.nav_mlp_wgrad_splits(1, hp, nh, B)
         env = os.environ.get("NAV_WGRAD_SPLITS")
         if env:
             sc, sa = (max(1, min(int(v), max(1, B // 32))) for v in env.split(","))

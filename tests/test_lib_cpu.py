@@ -17,7 +17,7 @@ LIB = os.path.join(PKG, "nav", "libnavenv.so")
 def header_functions():
     src = open(HEADER).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"^\s*(?:int|int64_t|void)\s+(nav_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int32_t|int64_t|void)\s+(nav_\w+)\s*\(", src, re.M)))
 
 
 @pytest.fixture(scope="module")

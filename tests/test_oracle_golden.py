@@ -139,3 +139,22 @@ def test_td3_oracle_vs_reference():
             assert (ix == g[name + "_idx"][k]).all()
             np.testing.assert_allclose(v, g[name + "_val"][k], rtol=0, atol=1e-7)
             np.testing.assert_allclose(s, g[name + "_sum"][k], rtol=1e-6, atol=1e-5)
+
+
+def test_cpu_demo_index_equals_brute_force(orc):
+    """The CPU port's exact demo index (cpu_baseline leg) returns the brute-force minimum bit for
+    bit: the reference's demo set (incl. augmented points off the world), shifted copies, queries
+    on cell corners, on demo points, off the world."""
+    from conftest import golden
+    demo = golden("trace.npz")["demo_set"]
+    rng = np.random.default_rng(21)
+    for shift in (0.0, 7.3, -3.1):
+        d = np.ascontiguousarray(demo + shift)
+        ix = orc.DemoIndexCPU(d)
+        assert ix.total < 60 * 10000  # sublinear: tens of candidates per cell, not 11 355
+        q = rng.uniform(-2, 101, (3000, 2))
+        q[:300] = np.floor(q[:300])
+        q[300:600] = d[rng.integers(0, len(d), 300)]
+        for x, y in q:
+            want = orc.lib().orc_demo_min(orc.ptr(d, orc._dp), len(d), float(x), float(y))
+            assert ix.min(float(x), float(y)) == want

@@ -1,0 +1,23 @@
+#!/bin/bash
+# Build an A/B variant of libnavenv.so with extra -D flags on one translation unit (tuning only):
+#   tools/build_variant.sh NAME learner|env|mlp0 "-DFOO=1 ..."
+# -> abl/libnavenv_NAME.so (load it with NAV_LIB=abl/libnavenv_NAME.so)
+set -eu
+cd "$(dirname "$0")/.."
+name=$1; unit=$2; flags=$3
+P=residual-td3-robot-navigation_amd
+B=$P/build
+make -s -C $P
+mkdir -p abl
+FL="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function -Iinclude -I$P/csrc"
+objs="$B/env_kernels.o $B/learner_kernels.o $B/mlp_kernels.o"
+for n in 1 2 3 4 5 6 7 8; do objs="$objs $B/mlp_nt$n.o"; done
+case $unit in
+  learner) /opt/rocm/bin/hipcc $FL $flags -c $P/csrc/learner_kernels.hip -o abl/$name.o
+           objs=${objs/$B\/learner_kernels.o/abl\/$name.o} ;;
+  env) /opt/rocm/bin/hipcc $FL $flags -c $P/csrc/env_kernels.hip -o abl/$name.o
+       objs=${objs/$B\/env_kernels.o/abl\/$name.o} ;;
+  *) echo "unit?"; exit 2 ;;
+esac
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o abl/libnavenv_$name.so $objs
+echo abl/libnavenv_$name.so

@@ -1,0 +1,53 @@
+"""Summarise a rocprofv3 --pmc run's rocpd database (run_results.db): per kernel (short name),
+dispatch count, mean of each counter per dispatch, and the derived MFMA busy fraction
+SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs * 1024 SIMDs) when both were collected.
+
+python tools/pmc_db.py gpurun_out/<dir>/run_results.db [name-substring ...]
+"""
+import re
+import sqlite3
+import sys
+from collections import defaultdict
+
+
+def short(name):
+    m = re.search(r"(k_[a-z_0-9]+)", name)
+    if not m:
+        return name[:40]
+    t = re.search(r"ILi(\d+)ELi(\d+)E(?:Li(\d+)ELi(\d+)E)?", name)
+    return m.group(1) + ("<%s>" % ",".join(g for g in t.groups() if g) if t else "")
+
+
+def summarise(path, filt=()):
+    c = sqlite3.connect(path)
+    acc = defaultdict(lambda: defaultdict(list))
+    dur = defaultdict(dict)
+    for name, counter, value, disp, d in c.execute(
+            "select kernel_name, counter_name, value, dispatch_id, duration "
+            "from counters_collection"):
+        k = short(name)
+        if filt and not any(s in k for s in filt):
+            continue
+        acc[k][counter].append(value)
+        dur[k][disp] = d
+    out = {}
+    for k, cs in sorted(acc.items()):
+        row = {c: sum(v) / len(v) for c, v in cs.items()}
+        row["dispatches"] = len(dur[k])
+        row["duration_us"] = sum(dur[k].values()) / max(1, len(dur[k])) / 1e3
+        g, m = row.get("GRBM_GUI_ACTIVE"), row.get("SQ_VALU_MFMA_BUSY_CYCLES")
+        if g and m is not None:
+            row["mfma_busy"] = m / (g / 8 * 1024)
+        out[k] = row
+    return out
+
+
+def main():
+    res = summarise(sys.argv[1], sys.argv[2:])
+    for k, row in res.items():
+        parts = " ".join("%s=%.4g" % (c, v) for c, v in sorted(row.items()))
+        print("%-36s %s" % (k, parts))
+
+
+if __name__ == "__main__":
+    main()
