@@ -2,11 +2,12 @@
 """bench.py — env-steps/s of the vectorised residual-TD3 loop on MI355X (BASELINE.json metric).
 
 Workload (BASELINE.json config 3): 65 536 parallel envs per GPU, full residual-TD3 update with
-2 x 256 actor/critic MLPs. One bench step = one vector tick of every env (nav_act ->
-nav_agent_step_indexed: tick + demo reward) followed by `--updates` TD3 epochs (critic every epoch, actor + Polyak every
-2nd) at batch `--batch` sampled from the device replay ring. Synthetic seeded start/goal pairs
-(Philox, 64 tasks of 1 024 envs), synthetic Perlin-style fields and straight-line demonstration
-sets, random-init networks (no datasets or checkpoints exist offline).
+2 x 256 actor/critic MLPs. One bench step = one vector tick of every env (nav_act_tick: actor
+forward + tick + indexed demo reward in one launch) followed by `--updates` TD3 epochs (critic
+every epoch, actor + Polyak every 2nd) at batch `--batch` sampled from the device replay ring. Synthetic seeded start/goal pairs
+(Philox, 64 tasks of 1 024 envs), synthetic Perlin-style fields, per-task demonstration sets from
+the batched GPU CEM demonstrator (3 demos + augmentations each, as the reference's robot builds
+them), random-init networks (no datasets or checkpoints exist offline).
 
 N > 1 (torch.distributed.run, one process per GPU): independent env blocks per rank (seed +
 rank), no data-path collective ("scaling": "weak"); `--shared-policy` adds the RCCL all-reduce of
@@ -14,7 +15,8 @@ flat actor/critic gradients (BASELINE config 5). Rank 0 prints one JSON line.
 
 Besides `value`, the line carries `roofline` for the dominant kernel (HIP-event timed inside the
 timed region on the launch stream), the step kernel's HBM figure on a large-N sweep
-(`step_kernel`, the 2^24-env point; `tick_in_loop` = the fused tick's time in the loop), and
+(`step_kernel`, the 2^24-env point), the per-tick time at 65 536 envs in both launch forms
+(`tick_forms`: nav_act + nav_agent_step_indexed vs the fused nav_act_tick), and
 `cpu_baseline` (the oracle CPU port of the same loop, rank 0 only, bounded sample).
 """
 import argparse
@@ -38,6 +40,7 @@ PMC_TRAFFIC = os.path.join(HERE, "profiles", "pmc_traffic.json")
 REGION_KERNEL = {"critic_rows": "k_td3_critic_rows", "actor_rows": "k_td3_actor_rows",
                  "mlp_bwd": "k_mlp_bwd", "mlp_wgrad": "k_wgrad", "act": "k_mlp_fwd",
                  "agent_step": "k_agent_step", "env_step": "k_env_step",
+                 "act_tick": "k_mlp_fwd<tick>", "env_step_k": "k_env_step_k",
                  "grad_reduce": "k_grad_reduce", "demo_reward": "k_demo_reward_idx"}
 
 
@@ -101,9 +104,10 @@ def barrier(ws):
         torch.distributed.barrier()
 
 
-def step_kernel_sweep(field, sizes, reps=20):
-    """Step-kernel HBM figure: nav_agent_step (fused tick) and nav_env_step (pure
-    Environment.step) alone at growing N, HIP-event timed on the launch stream."""
+def step_kernel_sweep(field, sizes, reps=20, K=16):
+    """Step-kernel HBM figure: nav_agent_step (fused tick), nav_env_step (pure
+    Environment.step) and nav_env_step_k (K Environment.steps per launch, state in registers)
+    alone at growing N, HIP-event timed on the launch stream; per-env-step figures."""
     from nav import prof
     from nav.vec_env import ReplayRing, VecEnv
     out = []
@@ -114,7 +118,8 @@ def step_kernel_sweep(field, sizes, reps=20):
         for _ in range(6):  # fill the 5-deep stuck history: steady-state traffic
             env.agent_step(act, rep)
             env.step(act)
-        t = prof.KernelTimer(["agent_step", "env_step"])
+        acts = (torch.rand(K, n, 2, dtype=torch.float64, device="cuda") - 0.5) * 14
+        t = prof.KernelTimer(["agent_step", "env_step", "env_step_k"])
         # each kernel back to back, as a training loop / a pure Environment.step loop runs it
         # (interleaved, env_step paid the write-back of agent_step's dirty lines: PMC r01p)
         with prof.timing(t):
@@ -122,17 +127,48 @@ def step_kernel_sweep(field, sizes, reps=20):
                 env.agent_step(act, rep)
             for _ in range(reps):
                 env.step(act)
+            for _ in range(max(1, reps // 4)):
+                env.step_k(acts)
         s = t.summary()
         row = {"n_envs": n}
-        for k, bpe in (("agent_step", prof.AGENT_STEP_BYTES), ("env_step", prof.ENV_STEP_BYTES)):
+        for k, bpe, steps in (("agent_step", prof.AGENT_STEP_BYTES, 1),
+                              ("env_step", prof.ENV_STEP_BYTES, 1),
+                              ("env_step_k", prof.env_step_k_bytes(K, False), K)):
             us = s[k]["avg_us"]
-            row[k] = {"avg_us": round(us, 2), "bytes_per_env": bpe,
-                      "GBps": round(bpe * n / (us * 1e-6) / 1e9, 1),
-                      "env_steps_per_s": n / (us * 1e-6)}
+            row[k] = {"avg_us": round(us, 2), "env_steps_per_launch": steps,
+                      "bytes_per_env_step": bpe,
+                      "GBps": round(bpe * n * steps / (us * 1e-6) / 1e9, 1),
+                      "env_steps_per_s": n * steps / (us * 1e-6)}
         out.append(row)
-        del env, rep, act
+        del env, rep, act, acts
         torch.cuda.empty_cache()
     return out
+
+
+def tick_forms(tr, reps=50):
+    """Per-tick time of the collect half of a step at the trainer's env count, in both launch
+    forms: nav_act + nav_agent_step_indexed (two launches) and nav_act_tick (one), HIP events on
+    the launch stream. Runs the trainer's own envs (after the timed regions)."""
+    from nav import prof
+    fuse = tr.fuse_tick
+    res = {"n_envs": tr.n}
+    for form in ("two_launch", "fused"):
+        tr.fuse_tick = form == "fused"
+        t = prof.KernelTimer(["act", "agent_step", "act_tick"])
+        torch.cuda.synchronize()
+        w0 = time.perf_counter()
+        with prof.timing(t):
+            for _ in range(reps):
+                tr.collect()
+        torch.cuda.synchronize()
+        wall = (time.perf_counter() - w0) / reps
+        s = t.summary()
+        ks = ("act", "agent_step") if form == "two_launch" else ("act_tick",)
+        res[form] = {k: round(s[k]["avg_us"], 2) for k in ks}
+        res[form]["per_tick_us"] = round(sum(s[k]["avg_us"] for k in ks), 2)
+        res[form]["wall_per_tick_us"] = round(1e6 * wall, 2)
+    tr.fuse_tick = fuse
+    return res
 
 
 def cpu_info():
@@ -254,7 +290,7 @@ def main():
     dominant = max(breakdown, key=lambda k: breakdown[k]["total_ms"])
 
     # ---- timed region
-    timer = prof.KernelTimer([] if args.no_timed_events else [dominant, "agent_step"])
+    timer = prof.KernelTimer([] if args.no_timed_events else [dominant])
     barrier(ws)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -301,22 +337,16 @@ def main():
                     "traffic_source": traffic_src,
                     "flop_per_launch": d["work_per_launch"], "avg_us": round(d["avg_us"], 2),
                     "launches": d["launches"]}
-        a = ksum.get("agent_step")
-        # in the training loop the tick launch also carries the indexed demo reward
-        # (nav_agent_step_indexed: ~16 candidate points per flagged env from L2), so its time is
-        # reported as is; the HBM figure of the step kernel is the plain tick on the sweep
-        tick = None
-        if a:
-            tick = {"kernel": "nav_agent_step_indexed (tick + demo reward)", "n_envs": args.envs,
-                    "avg_us": round(a["avg_us"], 2)}
+        forms = None if ws > 1 else tick_forms(tr)
         sweep = None if (args.no_sweep or ws > 1) else step_kernel_sweep(
             tr.field, [65536, 1 << 20, 1 << 22, 1 << 24])
         step_k = None
         if sweep:
             big = sweep[-1]["agent_step"]
             step_k = {"kernel": "nav_agent_step", "n_envs": sweep[-1]["n_envs"],
-                      "avg_us": big["avg_us"], "bytes_per_env": prof.AGENT_STEP_BYTES,
+                      "avg_us": big["avg_us"], "bytes_per_env_step": prof.AGENT_STEP_BYTES,
                       "GBps": big["GBps"], "frac": round(big["GBps"] / HBM_PEAK_GBS, 4),
+                      "env_step_k": sweep[-1]["env_step_k"],
                       "at_65536": sweep[0]["agent_step"]}
         # CPU baseline: rank 0 at N = 1 only (a reported baseline, not part of the scaling runs)
         cpu = None if (args.no_cpu_baseline or ws > 1) else cpu_baseline(args, tr)
@@ -327,7 +357,7 @@ def main():
             "warmup": args.warmup, "ms_per_step": 1e3 * dt / args.steps,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "fp32 MLP (MFMA) / fp64 env state",
-            "data": "synthetic (Philox start/goal pairs, generated fields, straight-line demos)",
+            "data": "synthetic (Philox start/goal pairs, generated fields, batched-CEM demo sets)",
             "config": {"workload": "config3: 65536 envs + residual-TD3 (2x256 MLPs)",
                        "envs_per_gpu": args.envs, "envs_per_group": args.envs_per_group,
                        "hidden": args.hidden, "layers": args.layers, "batch": args.batch,
@@ -338,7 +368,7 @@ def main():
                                        else "independent-env-blocks x%d" % ws)},
             "roofline": roof,
             "step_kernel": step_k,
-            "tick_in_loop": tick,
+            "tick_forms": forms,
             "step_kernel_sweep": sweep,
             "kernels": {k: {"avg_us": round(v["avg_us"], 2), "launches_per_step":
                             v["launches"] / 2, "ms_per_step": v["total_ms"] / 2}

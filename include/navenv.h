@@ -217,6 +217,22 @@ int nav_compute_reward(const nav_params* p, int64_t n, const double* next_state,
 int nav_rollout(const float* field, int64_t P, int32_t T, const double* start,
                 const double* actions, double* paths, const double* goal, double* reward,
                 void* stream);
+/* The CEM demonstrator batched over n_prob independent problems (environment.py:140-179; one per
+ * (group, demonstration)), P paths x T steps each. nav_cem_rollout runs CEM iteration `iter` for
+ * every path of every problem: start = region_sample(region[prob], uniforms[prob]) (environment.py:
+ * 150, 136), actions a0 [n][P][T][2] (iteration 0, the +-5 np.random.choice draws) or
+ * mean[prob][t] + std[prob][t] * z [n][P][T][2] in f64 (np.random.normal's loc + scale * gauss),
+ * written as float32 to actions [n][P][T][2] (planning_actions); paths (nullable) [n][P][T+1][2]
+ * float32 (planning_paths); reward [n][P] = -||f32(s_T) - goal|| (environment.py:164, 182-183).
+ * nav_cem_elite: per problem the E best paths (ascending reward order, ties by path index), their
+ * float32 action mean / std [n][T][2] (numpy float32 reductions over the elites in that order);
+ * best (nullable) [n] = first argmax of the rewards (environment.py:166-175). P <= 256. */
+int nav_cem_rollout(const float* field, int32_t n_prob, int32_t P, int32_t T, int32_t iter,
+                    const double* region, const double* uniforms, const double* goal,
+                    const double* a0, const double* z, const float* mean, const float* stdv,
+                    float* actions, float* paths, double* reward, void* stream);
+int nav_cem_elite(int32_t n_prob, int32_t P, int32_t T, int32_t E, const double* reward,
+                  const float* actions, float* mean, float* stdv, int32_t* best, void* stream);
 /* ReplayBuffer.push (robot.py:79-96) of n transitions (f64 in, float32 rows), slots
  * (base + i) % capacity. */
 int nav_replay_push(const nav_replay* replay, int64_t base, int64_t n, const double* state,
@@ -233,6 +249,18 @@ int nav_act(const nav_params* p, const nav_mlp* actor, int64_t n, const double* 
             const double* goal, const double* noise_scale, const double* noise_z,
             uint32_t step, int32_t mode, double* action_out, float* residual_out, void* stream);
 
+/* nav_act (training or testing mode, noise from noise_z or Philox) and nav_agent_step_indexed
+ * (demo_xy given) / nav_agent_step with demo_pending 0 (demo_xy NULL) in ONE launch: the actor's
+ * action epilogue hands each env's action to that env's training tick in the same workgroup, so
+ * the action never round-trips through memory (action_out nullable). Same results as the two
+ * launches, bit for bit (robot.py:541-569 then the tick of nav_agent_step; the robot-learning.py
+ * 'step' tick, robot-learning.py:95-101). */
+int nav_act_tick(const nav_params* p, const nav_mlp* actor, const nav_env_soa* env,
+                 const float* field, const double* noise_z, uint32_t step, int32_t mode,
+                 const nav_replay* replay, int64_t replay_base, const nav_step_out* out,
+                 const double* demo_xy, const int64_t* demo_off, int32_t envs_per_group,
+                 const int64_t* cell_start, const int32_t* cand, double* action_out,
+                 double* reward_out, void* stream);
 /* Generic forward of up to 2 networks sharing one input (twin critics), rows [M]:
  * x = in[m*ld_in + in_col + 0..d_in) (f32). out_mode 0: out[m*ld_out + out_col + j] = y;
  * out_mode 1 (target policy smoothing, robot.py:336-339): out = clamp(y + clamp(policy_noise*eps,

@@ -274,6 +274,100 @@ __global__ __launch_bounds__(kBlock) void k_rollout(const float2* __restrict__ f
     }
 }
 
+// ---------------- batched CEM demonstrator (environment.py:140-179) ----------------
+// n_prob independent CEM problems (one per group and demonstration), each P paths x T steps. One
+// rollout launch per CEM iteration over every problem's paths (lane = path, state in f64 as the
+// reference's planning_state), then one elite launch per iteration (workgroup = problem).
+// Iteration 0 takes the +-5 actions drawn by np.random.choice, later ones
+// a = mean[t] + std[t] * z in f64 (legacy normal = loc + scale * gauss) with z the standard
+// normal draws; both are drawn on the host from each problem's numpy stream, in the reference's
+// order, so the plans equal nav.Environment.get_demonstration's on the same stream.
+__global__ __launch_bounds__(kBlock) void k_cem_rollout(const float2* __restrict__ field,
+                                                        int32_t n_prob, int32_t P, int32_t T,
+                                                        int32_t iter,
+                                                        const double* __restrict__ region,
+                                                        const double2* __restrict__ uni,
+                                                        const double2* __restrict__ goal,
+                                                        const double2* __restrict__ a0,
+                                                        const double2* __restrict__ z,
+                                                        const float2* __restrict__ mean,
+                                                        const float2* __restrict__ stdv,
+                                                        float2* __restrict__ actions,
+                                                        float2* __restrict__ paths,
+                                                        double* __restrict__ reward) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;  // problem * P + path
+    if (i >= (int64_t)n_prob * P) return;
+    const int64_t prob = i / P;
+    // environment.py:150 get_random_robot_init_state (the same formula as nav_env_reset)
+    const double* rg = region + 4 * prob;
+    const double reg[4] = {rg[0], rg[1], rg[2], rg[3]};
+    const double2 u = uni[prob];
+    double2 s = region_sample(reg, u.x, u.y);
+    const int64_t base = i * T;
+    if (paths) paths[i * (T + 1)] = make_float2((float)s.x, (float)s.y);
+    for (int t = 0; t < T; ++t) {
+        double2 a;
+        if (iter == 0) {
+            a = a0[base + t];
+        } else {
+            const float2 m = mean[prob * T + t], sd = stdv[prob * T + t];
+            const double2 zz = z[base + t];
+            a = make_double2((double)m.x + (double)sd.x * zz.x, (double)m.y + (double)sd.y * zz.y);
+        }
+        actions[base + t] = make_float2((float)a.x, (float)a.y);  // planning_actions (float32)
+        s = dynamics(field, s, a);
+        if (paths) paths[i * (T + 1) + t + 1] = make_float2((float)s.x, (float)s.y);
+    }
+    // environment.py:164, 182-183 on the float32 planning_paths row
+    const double2 g = goal[prob];
+    reward[i] = -norm2((double)(float)s.x - g.x, (double)(float)s.y - g.y);
+}
+
+// environment.py:166-171: the E best paths (np.argsort ascending, last E; ties by path index, a
+// stable order), their float32 action mean and std over the elites in that order (numpy's float32
+// reductions: sequential sums, / E, sqrt); best [n] = argmax of the rewards (first maximum,
+// environment.py:173). Workgroup = problem; P <= kBlock.
+__global__ __launch_bounds__(kBlock) void k_cem_elite(int32_t P, int32_t T, int32_t E,
+                                                      const double* __restrict__ reward,
+                                                      const float* __restrict__ actions,
+                                                      float* __restrict__ mean,
+                                                      float* __restrict__ stdv,
+                                                      int32_t* __restrict__ best) {
+    __shared__ double r[kBlock];
+    __shared__ int order[kBlock];
+    const int prob = blockIdx.x, tid = threadIdx.x;
+    if (tid < P) r[tid] = reward[(int64_t)prob * P + tid];
+    __syncthreads();
+    if (tid < P) {
+        const double v = r[tid];
+        int rank = 0;
+        for (int q = 0; q < P; ++q) rank += (r[q] < v || (r[q] == v && q < tid)) ? 1 : 0;
+        order[rank] = tid;
+    }
+    __syncthreads();
+    if (best && tid == 0) {
+        int b = 0;
+        for (int q = 1; q < P; ++q)
+            if (r[q] > r[b]) b = q;
+        best[prob] = b;
+    }
+    const float* acts = actions + (int64_t)prob * P * T * 2;
+    const float inv_n = (float)E;
+    for (int k = tid; k < T * 2; k += kBlock) {
+        float sum = acts[(int64_t)order[P - E] * T * 2 + k];
+        for (int e = 1; e < E; ++e) sum = sum + acts[(int64_t)order[P - E + e] * T * 2 + k];
+        const float mu = sum / inv_n;
+        float d0 = acts[(int64_t)order[P - E] * T * 2 + k] - mu;
+        float sq = d0 * d0;
+        for (int e = 1; e < E; ++e) {
+            const float d = acts[(int64_t)order[P - E + e] * T * 2 + k] - mu;
+            sq = sq + d * d;
+        }
+        mean[(int64_t)prob * T * 2 + k] = mu;
+        stdv[(int64_t)prob * T * 2 + k] = sqrtf(sq / inv_n);
+    }
+}
+
 // ReplayBuffer.push (robot.py:79-96) of n transitions given as f64 arrays.
 __global__ __launch_bounds__(kBlock) void k_replay_push(int64_t n, const double2* __restrict__ s,
                                                         const double2* __restrict__ a,
@@ -733,6 +827,39 @@ int nav_rollout(const float* field, int64_t P, int32_t T, const double* start,
                        reinterpret_cast<const double2*>(start),
                        reinterpret_cast<const double2*>(actions),
                        reinterpret_cast<double2*>(paths), goal, reward);
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_cem_rollout(const float* field, int32_t n_prob, int32_t P, int32_t T, int32_t iter,
+                    const double* region, const double* uniforms, const double* goal,
+                    const double* a0, const double* z, const float* mean, const float* stdv,
+                    float* actions, float* paths, double* reward, void* stream) {
+    if (!field || n_prob < 0 || P < 1 || T < 1 || iter < 0 || !region || !uniforms || !goal ||
+        !actions || !reward || (iter == 0 && !a0) || (iter > 0 && (!z || !mean || !stdv)) ||
+        (int64_t)n_prob * P * (T + 1) > ((int64_t)1 << 40))
+        return NAV_EINVAL;
+    if (n_prob == 0) return 0;
+    hipLaunchKernelGGL(k_cem_rollout, dim3(blocks_for((int64_t)n_prob * P)), dim3(kBlock), 0,
+                       S(stream), reinterpret_cast<const float2*>(field), n_prob, P, T, iter,
+                       region, reinterpret_cast<const double2*>(uniforms),
+                       reinterpret_cast<const double2*>(goal),
+                       reinterpret_cast<const double2*>(a0), reinterpret_cast<const double2*>(z),
+                       reinterpret_cast<const float2*>(mean), reinterpret_cast<const float2*>(stdv),
+                       reinterpret_cast<float2*>(actions), reinterpret_cast<float2*>(paths),
+                       reward);
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_cem_elite(int32_t n_prob, int32_t P, int32_t T, int32_t E, const double* reward,
+                  const float* actions, float* mean, float* stdv, int32_t* best, void* stream) {
+    if (n_prob < 0 || P < 1 || P > kBlock || T < 1 || E < 1 || E > P || !reward || !actions ||
+        !mean || !stdv)
+        return NAV_EINVAL;
+    if (n_prob == 0) return 0;
+    hipLaunchKernelGGL(k_cem_elite, dim3(n_prob), dim3(kBlock), 0, S(stream), P, T, E, reward,
+                       actions, mean, stdv, best);
     NAV_CHECK_LAUNCH();
     return 0;
 }

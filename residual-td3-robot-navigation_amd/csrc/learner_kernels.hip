@@ -399,23 +399,44 @@ NAV_DEV void wgrad_rows_mfma(const WgradArgs& a, int y, int n0, int k0, int64_t 
     const int ld_dy = a.ld_dy, ld_in = a.ld_in;
     const float* xin = a.in + a.in_col;
     // raw loads of a 32-row tile (A operands: lane l32 = row, h = k; the lane's 2 mask words),
-    // from clamped in-bounds addresses; what does not exist is zeroed where it is used
+    // in tile order through running per-lane pointers (a 64-bit add per stream and tile: the
+    // address math is VALU, which the f32 MFMA waits for); a partial last tile reads clamped rows,
+    // and what does not exist is zeroed where it is used
     const int gk = h < d_out ? h : 0, xk0 = h < d_in ? h : 0, xk1 = 2 + h < d_in ? 2 + h : 0;
     struct Raw {
         float g, x0, x1;
         uint32_t m0, m1;
     };
-    auto load = [&](int64_t rt) {
-        const int64_t r = rt + l32;
-        const int64_t rc = r < r_hi ? r : r_lo;
+    const float* gp = dyp + (r_lo + l32) * ld_dy + gk;
+    const float* xp = xin + (r_lo + l32) * ld_in;
+    const uint16_t* mp = mk + (size_t)(r_lo >> 5) * mstride;
+    const int64_t gstep = 32 * (int64_t)ld_dy, xstep = 32 * (int64_t)ld_in;
+    int64_t rl = r_lo;  // first row of the next tile to load
+    auto load = [&](int64_t) {
         Raw v;
-        v.g = dyp[rc * ld_dy + gk];
-        const float* x = xin + rc * ld_in;
-        v.x0 = x[xk0];
-        v.x1 = x[xk1];
-        const uint16_t* w = mk + (size_t)(rt >> 5) * mstride;
-        v.m0 = w[0];
-        v.m1 = w[64];
+        if (NAV_WG_EXP == 5) {  // tuning probe: no global loads in the row loop
+            v.g = wob[0] + (float)rl; v.x0 = w0b[0][0]; v.x1 = w0b[1][1];
+            v.m0 = (uint32_t)rl * 2654435761u; v.m1 = v.m0 >> 7;
+        } else if (rl + 32 <= r_hi) {
+            v.g = *gp;
+            v.x0 = xp[xk0];
+            v.x1 = xp[xk1];
+            v.m0 = mp[0];
+            v.m1 = mp[64];
+        } else {  // rows past r_hi read row r_lo (the values are not used)
+            const bool ok = rl + l32 < r_hi;
+            const float* g = ok ? gp : dyp + r_lo * ld_dy + gk;
+            const float* x = ok ? xp : xin + r_lo * ld_in;
+            v.g = *g;
+            v.x0 = x[xk0];
+            v.x1 = x[xk1];
+            v.m0 = mp[0];
+            v.m1 = mp[64];
+        }
+        gp += gstep;
+        xp += xstep;
+        mp += mstride;
+        rl += 32;
         return v;
     };
     // operand MFMAs of one tile (results in the C layout, masked later by finish())
@@ -446,7 +467,7 @@ NAV_DEV void wgrad_rows_mfma(const WgradArgs& a, int y, int n0, int k0, int64_t 
             Q[1][e] = __int_as_float(max(__float_as_int(Q[1][e]), 0));
         }
     };
-    if (r_lo >= r_hi) return;
+    if (r_lo >= r_hi || NAV_WG_EXP == 4) return;  // 4: tuning probe, no row loop
     // ping-pong operand buffers (a loop-carried copy would cost 64 v_mov per tile, and the VALU
     // shares the SIMD's issue with the f32 MFMA): tile t uses buffer t & 1 while the operand
     // MFMAs of tile t + 1 fill the other
@@ -459,10 +480,13 @@ NAV_DEV void wgrad_rows_mfma(const WgradArgs& a, int y, int n0, int k0, int64_t 
     auto step = [&](int64_t rt, f32x16 (&P)[2], f32x16 (&Q)[2], f32x16 (&Pn)[2],
                     f32x16 (&Qn)[2]) {
         const bool more = rt + 32 < r_hi;
-        // the next tile's operand MFMAs go first: done long before finish() reads them
-        if (more) issue(rt + 32, nxt, Pn, Qn);
+        // the loads of tile t + 2 are issued first and fenced there, so the wait for tile t + 1's
+        // raw data (loaded a step ago) below leaves them in flight (vmcnt counts in order)
         Raw nn = nxt;
         if (rt + 64 < r_hi) nn = load(rt + 64);
+        __builtin_amdgcn_sched_barrier(0);
+        // the next tile's operand MFMAs next: done long before finish() reads them
+        if (more) issue(rt + 32, nxt, Pn, Qn);
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
             acc[0][0] = mfma(P[0][e], Q[0][e], acc[0][0]);

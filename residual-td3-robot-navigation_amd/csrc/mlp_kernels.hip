@@ -10,6 +10,7 @@
 // from forward to backward as C-layout bit masks. Weight gradients: one launch per network over
 // row splits writing deterministic partial slabs, reduced in a fixed order.
 #include "mlp_common.h"
+#include "nav_tick.h"
 
 namespace {
 
@@ -83,7 +84,7 @@ NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const float* __restr
 }
 
 enum { IN_F32 = 0, IN_BASELINE = 1 };
-enum { OUT_F32 = 0, OUT_TARGET = 1, OUT_ACT = 2, OUT_LOSS = 3 };
+enum { OUT_F32 = 0, OUT_TARGET = 1, OUT_ACT = 2, OUT_LOSS = 3, OUT_TICK = 4 };
 
 
 struct FwdArgs {
@@ -118,6 +119,16 @@ struct FwdArgs {
     int act_mode;
     double max_action_d;
     double* action_out;
+    // OUT_TICK: the training tick of every row's env with the action just formed (one launch:
+    // nav_act + nav_agent_step(_indexed); nav_act_tick)
+    nav_params p;
+    nav_env_soa env;
+    const float2* field;
+    float4* rows;
+    int64_t cap, base;
+    nav_step_out sout;
+    DemoIdx demo;
+    double* reward_out;
 };
 
 // Output-layer partial sums: [d_out <= 2][4 waves][TM rows] (red_floats per block).
@@ -534,6 +545,43 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
         loss_epilogue<NT, RT>(net, top, red, row0, M, yt, a.norm, a.dq[q],
                               a.loss_part[q] + blockIdx.x,
                               a.eslab[q] ? a.eslab[q] + (int64_t)blockIdx.x * a.ecount : nullptr);
+        return;
+    }
+    if (OUT_MODE == OUT_TICK) {
+        // robot.py:556-567 as OUT_ACT, the action parked in LDS (the input rows are done with),
+        // then the tick of env row0 + t by thread t < TM: nav_agent_step's device code
+        double* act_lds = reinterpret_cast<double*>(xin);  // [TM][2]
+        if (tid < 2 * TM && r < M) {
+            const float y = out_y<RT>(net, red, rloc, j);
+            const double s = a.state[r * 2 + j], g = a.goal[r * 2 + j];
+            double c = (s - g) + (double)y;
+            if (a.act_mode == 0) {
+                double z;
+                if (a.noise_z) {
+                    z = a.noise_z[r * 2 + j];
+                } else {
+                    const double2 zz = gauss_pair(philox(0u, (uint32_t)r, NAV_TAG_NOISE, a.step,
+                                                         a.p.seed_lo, a.p.seed_hi));
+                    z = j == 0 ? zz.x : zz.y;
+                }
+                c = c + (a.noise_scale[r] * a.max_action_d) * z;
+            }
+            const double v = clipd(c, -a.max_action_d, a.max_action_d);
+            act_lds[rloc * 2 + j] = v;
+            if (a.action_out) a.action_out[r * 2 + j] = v;
+        }
+        __syncthreads();
+        if (tid < TM) {
+            TickStats st{0.f, 0.f, 0.f, 0.f, 0.f};
+            if (r < M) {
+                const double2 av = make_double2(act_lds[tid * 2], act_lds[tid * 2 + 1]);
+                st = a.demo.cand ? agent_tick<true>(a.p, a.env, a.field, r, av, a.rows, a.cap,
+                                                    a.base, a.sout, a.demo, true, a.reward_out)
+                                 : agent_tick<false>(a.p, a.env, a.field, r, av, a.rows, a.cap,
+                                                     a.base, a.sout, a.demo, false, a.reward_out);
+            }
+            if (a.sout.block_stats && row0 + (tid & ~63) < M) wave_stats(st, a.sout.block_stats, r);
+        }
         return;
     }
     if (r >= M || j >= d_out) return;
@@ -1100,6 +1148,8 @@ int rows_rt(int fam, int in_mode, int out_mode, const void* args, int n_nets, hi
             const FwdArgs& a = *static_cast<const FwdArgs*>(args);
             if (in_mode == IN_BASELINE && out_mode == OUT_ACT)
                 launch_fwd_k<NT, RT, IN_BASELINE, OUT_ACT>(a, n_nets, st);
+            else if (in_mode == IN_BASELINE && out_mode == OUT_TICK)
+                launch_fwd_k<NT, RT, IN_BASELINE, OUT_TICK>(a, n_nets, st);
             else if (in_mode == IN_F32 && out_mode == OUT_F32)
                 launch_fwd_k<NT, RT, IN_F32, OUT_F32>(a, n_nets, st);
             else if (in_mode == IN_F32 && out_mode == OUT_TARGET)
@@ -1218,6 +1268,47 @@ int nav_act(const nav_params* p, const nav_mlp* actor, int64_t n, const double* 
     a.seed_lo = p->seed_lo;
     a.seed_hi = p->seed_hi;
     return launch_fwd<IN_BASELINE, OUT_ACT>(a, 1, S(stream));
+}
+
+int nav_act_tick(const nav_params* p, const nav_mlp* actor, const nav_env_soa* env,
+                 const float* field, const double* noise_z, uint32_t step, int32_t mode,
+                 const nav_replay* replay, int64_t replay_base, const nav_step_out* out,
+                 const double* demo_xy, const int64_t* demo_off, int32_t envs_per_group,
+                 const int64_t* cell_start, const int32_t* cand, double* action_out,
+                 double* reward_out, void* stream) {
+    FwdArgs a{};
+    if (!p || !env || !make_dev(actor, &a.net[0]) || actor->d_in != 2 || actor->d_out != 2 ||
+        (mode != 0 && mode != 1) || !field || !replay || !replay->rows || !out ||
+        env->n < 0 || env->n >= ((int64_t)1 << 31) || replay->capacity < env->n ||
+        replay->capacity <= 0 || replay_base < 0 || (demo_off && envs_per_group <= 0))
+        return NAV_EINVAL;
+    if (env->n == 0) return 0;
+    if (!env->state || !env->goal || !env->region || !env->hist || !env->meta ||
+        !env->plan_index || !env->path_length || !env->episodes || !env->noise_scale)
+        return NAV_EINVAL;
+    const bool demo = demo_xy != nullptr;
+    if (demo && (!cell_start || !cand)) return NAV_EINVAL;
+    a.M = env->n;
+    a.state = env->state;
+    a.goal = env->goal;
+    a.noise_scale = env->noise_scale;
+    a.noise_z = noise_z;
+    a.step = step;
+    a.act_mode = mode;
+    a.max_action_d = p->max_action;
+    a.action_out = action_out;
+    a.p = *p;
+    a.env = *env;
+    a.field = reinterpret_cast<const float2*>(field);
+    a.rows = reinterpret_cast<float4*>(replay->rows);
+    a.cap = replay->capacity;
+    a.base = replay_base % replay->capacity;
+    a.sout = *out;
+    if (demo)
+        a.demo = DemoIdx{reinterpret_cast<const double2*>(demo_xy), demo_off,
+                         envs_per_group > 0 ? envs_per_group : 1, cell_start, cand};
+    a.reward_out = reward_out;
+    return launch_fwd<IN_BASELINE, OUT_TICK>(a, 1, S(stream));
 }
 
 int nav_mlp_forward(const nav_mlp* nets, int32_t n_nets, int64_t M, const float* in,

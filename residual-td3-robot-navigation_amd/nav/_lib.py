@@ -74,6 +74,10 @@ SIGNATURES = [
                                  C.c_int64, _P(NavStepOut), C.c_int32, _vp]),
     ("nav_check_if_stuck", C.c_int, [_P(NavParams), _P(NavEnvSoa), _vp, _vp, _vp]),
     ("nav_rollout", C.c_int, [_vp, C.c_int64, C.c_int32, _vp, _vp, _vp, _vp, _vp, _vp]),
+    ("nav_cem_rollout", C.c_int, [_vp, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _vp, _vp, _vp,
+                                  _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    ("nav_cem_elite", C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, _vp, _vp, _vp, _vp,
+                                _vp, _vp]),
     ("nav_replay_push", C.c_int, [_P(NavReplay), C.c_int64, C.c_int64, _vp, _vp, _vp, _vp, _vp,
                                   _vp]),
     ("nav_demo_index_plan", C.c_int, [_vp, _vp, C.c_int32, C.c_int64, _vp, _vp, _vp]),
@@ -90,6 +94,9 @@ SIGNATURES = [
                                      C.c_int32, _vp, _vp, _vp]),
     ("nav_act", C.c_int, [_P(NavParams), _P(NavMlp), C.c_int64, _vp, _vp, _vp, _vp, C.c_uint32,
                           C.c_int32, _vp, _vp, _vp]),
+    ("nav_act_tick", C.c_int, [_P(NavParams), _P(NavMlp), _P(NavEnvSoa), _vp, _vp, C.c_uint32,
+                               C.c_int32, _P(NavReplay), C.c_int64, _P(NavStepOut), _vp, _vp,
+                               C.c_int32, _vp, _vp, _vp, _vp, _vp]),
     ("nav_mlp_forward", C.c_int, [_P(NavMlp), C.c_int32, C.c_int64, _vp, C.c_int32, C.c_int32,
                                   _P(_vp), C.c_int32, C.c_int32, C.c_int32, _vp, C.c_float,
                                   C.c_float, C.c_float, C.c_uint32, C.c_uint32, C.c_uint32,

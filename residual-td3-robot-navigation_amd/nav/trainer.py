@@ -2,14 +2,15 @@
 training mode, robot-learning.py:54-101, for n independent envs at once).
 
 One `step()` = one vector tick: every env selects an action (actor MLP + baseline + exploration
-noise, nav_act), takes one environment step with the fused reward / stuck / done / replay-push /
-auto-reset tick (nav_agent_step + nav_demo_reward), then the learner runs `updates_per_step`
+noise) and takes one environment step with the fused reward / stuck / done / replay-push /
+auto-reset tick, both in ONE launch (nav_act_tick), then the learner runs `updates_per_step`
 TD3 epochs (robot.py:272-285: critic every epoch, actor + Polyak every `policy_update_delay`-th)
 on batches sampled from the device replay ring. The reference's schedule (100 epochs of batch
 100 at every episode end) does not map onto 65 536 asynchronous envs; the update-to-data ratio
 here is updates_per_step * batch / n_envs sampled transitions per collected transition.
 """
 import ctypes as C
+import os
 
 import numpy as np
 import torch
@@ -17,7 +18,7 @@ import torch
 from . import config as K
 from . import prof
 from ._lib import lib, ptr, stream_handle
-from .demos import synthetic_group_demo_sets
+from .cem import cem_group_demo_sets
 from .fields import make_fields
 from .td3 import TD3
 from .vec_env import ReplayRing, VecEnv, make_field
@@ -42,7 +43,10 @@ class VecTrainer:
             firsts = torch.arange(G, device=self.device) * epg
             regions = self.env.region[firsts].cpu().numpy()
             goals = self.env.goal[firsts].cpu().numpy()
-            pts, off = synthetic_group_demo_sets(regions, goals, self.seed)
+            # each group's 3 demonstrations from the batched GPU CEM (environment.py:140-179) +
+            # their augmentations (robot.py:771-824), as the reference's robot acquires them
+            pts, off = cem_group_demo_sets(self.field, regions, goals, self.seed,
+                                           device=self.device)
             self.env.set_demo(pts, off if G > 1 else None)
         cfg = K.TD3Config(batch_size=int(batch), num_epochs=int(updates_per_step),
                           net=K.NetConfig(hidden=hidden, n_hidden=n_hidden))
@@ -52,6 +56,9 @@ class VecTrainer:
         self.action = torch.zeros(self.n, 2, dtype=torch.float64, device=self.device)
         self.steps = 0
         self.updates_per_step = int(updates_per_step)
+        # act + tick fused into one launch (NAV_FUSE_TICK=0: the two launches; A/B and the
+        # fused-vs-unfused parity test)
+        self.fuse_tick = os.environ.get("NAV_FUSE_TICK", "1") != "0"
 
     # robot.py:541-569 for every env
     def act(self, training=True, stream=None):
@@ -64,8 +71,13 @@ class VecTrainer:
         return self.action
 
     def collect(self, stream=None):
-        self.act(True, stream)
-        self.env.agent_step(self.action, self.replay, stream)
+        if self.fuse_tick and (self.env.demo_xy is None or self.env.demo_index is not None):
+            # one launch: action selection + the tick (nav_act_tick)
+            self.env.act_tick(self.td3.actor_network, self.steps, self.replay,
+                              action_out=self.action, stream=stream)
+        else:
+            self.act(True, stream)
+            self.env.agent_step(self.action, self.replay, stream)
         self.steps += 1
 
     def learn(self, stream=None):

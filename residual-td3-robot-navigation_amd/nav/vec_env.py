@@ -199,6 +199,28 @@ class VecEnv:
         replay.advance(self.n)
         return base
 
+    # robot.py:541-569 + the training tick above, one launch (nav_act_tick): the actor's action
+    # epilogue runs each env's tick in the same workgroup
+    def act_tick(self, actor, step, replay, training=True, action_out=None, reward_out=None,
+                 noise_z=None, stream=None):
+        base = replay.position
+        rd = replay.desc()
+        a = actor.desc()
+        ix = self.demo_index if (self.demo_xy is not None and self.demo_xy.shape[0] > 0) else None
+        if self.demo_xy is not None and self.demo_xy.shape[0] > 0 and ix is None:
+            raise ValueError("act_tick needs the demo index (set_demo(index=True))")
+        flops = prof.mlp_fwd_flops(2, 2, actor.hidden, actor.n_hidden, self.n)
+        with prof.region("act_tick", flops):
+            lib().nav_act_tick(
+                C.byref(self.p), C.byref(a), C.byref(self.soa), ptr(self.field), ptr(noise_z),
+                int(step) & 0xFFFFFFFF, 0 if training else 1, C.byref(rd), base,
+                C.byref(self.out), ptr(self.demo_xy) if ix else None,
+                ptr(self.demo_off) if ix else None, self.envs_per_group,
+                ptr(ix.cell_start) if ix else None, ptr(ix.cand) if ix else None,
+                ptr(action_out), ptr(reward_out), stream_handle(stream))
+        replay.advance(self.n)
+        return base
+
     def stats(self):
         """Sum of the per-block rows: reward (w/o demo term), done, goal, stuck, ended."""
         return self.block_stats.sum(0)[:5].tolist()

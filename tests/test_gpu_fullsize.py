@@ -116,6 +116,45 @@ def test_fused_demo_reward_is_bit_identical():
         assert torch.equal(net.params, b.td3.networks()[k].params), k
 
 
+@pytest.mark.parametrize("n,demos", [(8192, True), (5000, True), (1000, False)])
+def test_fused_act_tick_is_bit_identical(n, demos):
+    """nav_act_tick (actor forward + the env tick in one launch) vs nav_act followed by
+    nav_agent_step_indexed: same actions, replay rows, env state, flags, next states, rewards,
+    block stats and learner, bit for bit, over ragged env counts and with / without demo sets."""
+    from nav.trainer import VecTrainer
+    runs = []
+    for fused in (True, False):
+        tr = VecTrainer(n_envs=n, hidden=256, n_hidden=2, batch=2048, updates_per_step=2,
+                        envs_per_group=1024, demos=demos, device=DEV)
+        got = []
+        for _ in range(6):
+            r = torch.full((tr.n,), float("nan"), dtype=torch.float64, device=DEV)
+            if fused:
+                tr.env.act_tick(tr.td3.actor_network, tr.steps, tr.replay, action_out=tr.action,
+                                reward_out=r)
+            else:
+                tr.act()
+                tr.env.agent_step(tr.action, tr.replay, reward_out=r)
+            tr.steps += 1
+            tr.learn()
+            got.append((tr.action.clone(), r, tr.env.next_state.clone(), tr.env.goal_term.clone(),
+                        tr.env.block_stats.clone()))
+        torch.cuda.synchronize()
+        runs.append((tr, got))
+    (a, ga), (b, gb) = runs
+    assert torch.equal(a.replay.rows, b.replay.rows)
+    assert torch.equal(a.env.state, b.env.state)
+    assert torch.equal(a.env.flags, b.env.flags)
+    for t, (x, y) in enumerate(zip(ga, gb)):
+        for i, (u, v) in enumerate(zip(x, y)):
+            assert torch.equal(u.isnan(), v.isnan()), (t, i)
+            assert torch.equal(u.nan_to_num(), v.nan_to_num()), (t, i)
+    if demos:
+        assert any((~g[1].isnan()).any() for g in ga)  # some envs took the demo term
+    for k, net in a.td3.networks().items():
+        assert torch.equal(net.params, b.td3.networks()[k].params), k
+
+
 def test_td3_update_at_bench_config_vs_oracle():
     """The learner pinned at the bench configuration (2x256 actor/critics, batch 32 768, the
     bench's 2 epochs per step: critic, actor + Polyak, critic): TD3.td3_update with injected batch
