@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define NAV_ABI_VERSION 5
+#define NAV_ABI_VERSION 6
 #define NAV_EINVAL (-100000)
 
 #define NAV_WORLD_CELLS 100 /* field = float32 [100][100][2] (speed, angle), x-major: cell cx*100+cy
@@ -172,11 +172,18 @@ int nav_demo_reward(const nav_params* p, int64_t n, const double* next_state,
                     const int64_t* demo_off, int64_t m, int32_t envs_per_group,
                     const nav_replay* replay, int64_t replay_base, double* reward_out,
                     void* stream);
-/* Exact bucketed nearest-demo index over the 100 x 100 dynamics cells (robot.py:753 made
- * sublinear, result bit-identical to the brute force): for each (group, cell) the bound
- * U^2 = min_q maxdist^2(q, cell) and the candidate count (plan), an exclusive scan into
+/* Exact bucketed nearest-demo index (robot.py:753 made sublinear, result bit-identical to the
+ * brute force), built in two levels.
+ * Level 1, the 100 x 100 dynamics cells over all points of each group: for each (group, cell) the
+ * bound U^2 = min_q maxdist^2(q, cell) and the candidate count (plan), an exclusive scan into
  * cell_start [n_groups*10000 + 1] (scan), then ascending group-relative point indices (fill).
- * cell_bound f64 / cell_count i32: [n_groups][10000]; cand: cell_start[last] int32 entries. */
+ * cell_bound f64 / cell_count i32: [n_groups][10000]; cand: cell_start[last] int32 entries.
+ * Level 2, the query index: every dynamics cell split into R x R index cells (R =
+ * nav_demo_index_res(), a power of 2; index cell of s = ((int)(s.x*R), (int)(s.y*R)) on a
+ * 100R x 100R grid, x-major), each cell's list taken from its level-1 parent's list (subplan),
+ * scanned (subscan) and filled (subfill). sub_bound f64 / sub_count i32: [n_groups][(100R)^2];
+ * sub_start [n_groups*(100R)^2 + 1]; sub_cand: sub_start[last] int32 entries. The reward entry
+ * points below take (sub_start, sub_cand) as their (cell_start, cand). */
 int nav_demo_index_plan(const double* demo_xy, const int64_t* demo_off, int32_t n_groups,
                         int64_t m, double* cell_bound, int32_t* cell_count, void* stream);
 int nav_demo_index_scan(const int32_t* cell_count, int32_t n_groups, int64_t* cell_start,
@@ -184,7 +191,18 @@ int nav_demo_index_scan(const int32_t* cell_count, int32_t n_groups, int64_t* ce
 int nav_demo_index_fill(const double* demo_xy, const int64_t* demo_off, int32_t n_groups,
                         int64_t m, const double* cell_bound, const int64_t* cell_start,
                         int32_t* cand, void* stream);
-/* nav_demo_reward through the index (same result, ~11 instead of 11 355 points per env). */
+int32_t nav_demo_index_res(void);
+int nav_demo_index_subplan(const double* demo_xy, const int64_t* demo_off, int32_t n_groups,
+                           const int64_t* cell_start, const int32_t* cand, double* sub_bound,
+                           int32_t* sub_count, void* stream);
+int nav_demo_index_subscan(const int32_t* sub_count, int32_t n_groups, int64_t* sub_start,
+                           void* stream);
+int nav_demo_index_subfill(const double* demo_xy, const int64_t* demo_off, int32_t n_groups,
+                           const int64_t* cell_start, const int32_t* cand,
+                           const double* sub_bound, const int64_t* sub_start, int32_t* sub_cand,
+                           void* stream);
+/* nav_demo_reward through the level-2 index (same result, a few instead of 11 355 points per
+ * env). */
 int nav_demo_reward_indexed(const nav_params* p, int64_t n, const double* next_state,
                             const double* goal_term, const uint8_t* flags, const double* demo_xy,
                             const int64_t* demo_off, int32_t envs_per_group,

@@ -337,20 +337,22 @@ void orc_act_epilogue(const double* s, const double* g, const float* res, double
 }
 
 /* ---- exact nearest-demo index for the CPU port (the cpu_baseline leg does the GPU's algorithm):
- * per dynamics cell C a candidate list holding, for every query in C, its nearest demo point.
+ * per cell C a candidate list holding, for every query in C, its nearest demo point.
  * Any demo point q bounds the nearest distance of every x in C by U = maxdist(q, C), and the
  * nearest point p* has mindist(p*, C) <= U, so {p : mindist^2(p, C) <= U^2} suffices; the min over
- * it is the same f64 value as over all points (tests/test_oracle_golden.py checks it). The
- * construction buckets the points into the 1 x 1 cells and searches rings of buckets. */
-static double cell_maxd2(double px, double py, double lx, double ly) {
-    double fx = fmax(fabs(px - lx), fabs(px - (lx + 1.0)));
-    double fy = fmax(fabs(py - ly), fabs(py - (ly + 1.0)));
+ * it is the same f64 value as over all points (tests/test_oracle_golden.py checks it).
+ * Two levels, as nav_demo_index_*: the 1 x 1 dynamics cells (points bucketed into those cells,
+ * rings of buckets searched), then ORC_DEMO_RES x ORC_DEMO_RES index cells per dynamics cell whose
+ * lists come from the parent's list (a subcell's candidates are candidates of its parent). */
+static double cell_maxd2(double px, double py, double lx, double ly, double w) {
+    double fx = fmax(fabs(px - lx), fabs(px - (lx + w)));
+    double fy = fmax(fabs(py - ly), fabs(py - (ly + w)));
     return fx * fx + fy * fy;
 }
 
-static double cell_mind2(double px, double py, double lx, double ly) {
-    double nx = fmax(0.0, fmax(lx - px, px - (lx + 1.0)));
-    double ny = fmax(0.0, fmax(ly - py, py - (ly + 1.0)));
+static double cell_mind2(double px, double py, double lx, double ly, double w) {
+    double nx = fmax(0.0, fmax(lx - px, px - (lx + w)));
+    double ny = fmax(0.0, fmax(ly - py, py - (ly + w)));
     return nx * nx + ny * ny;
 }
 
@@ -359,8 +361,11 @@ static int bucket_of(double v) {
     return b < 0 ? 0 : (b > 99 ? 99 : b);
 }
 
-int64_t orc_demo_index_build(const double* demo, int64_t m, int64_t* cell_start, int32_t* cand,
-                             int64_t cap) {
+int32_t orc_demo_index_res(void) { return ORC_DEMO_RES; }
+
+/* level 1 over the 100 x 100 dynamics cells: cell_start [10001]; cand NULL = count only */
+static int64_t index_level1(const double* demo, int64_t m, int64_t* cell_start, int32_t* cand,
+                            int64_t cap) {
     /* buckets (CSR) of the in-world points; points outside [0,100)^2 go to a side list that
      * every cell checks (augmentation noise can push a demo point off the world) */
     int64_t* bstart = (int64_t*)calloc(10001, sizeof(int64_t));
@@ -389,7 +394,7 @@ int64_t orc_demo_index_build(const double* demo, int64_t m, int64_t* cell_start,
         const double lx = (double)cx, ly = (double)cy;
         double u = INFINITY;
         for (int64_t o = 0; o < n_out; ++o)
-            u = fmin(u, cell_maxd2(demo[2 * outside[o]], demo[2 * outside[o] + 1], lx, ly));
+            u = fmin(u, cell_maxd2(demo[2 * outside[o]], demo[2 * outside[o] + 1], lx, ly, 1.0));
         /* rings of buckets around the cell until one ring past the first non-empty one */
         int hit = -1;
         for (int r = 0; r < 100; ++r) {
@@ -402,7 +407,7 @@ int64_t orc_demo_index_build(const double* demo, int64_t m, int64_t* cell_start,
                     const int b = bx * 100 + by;
                     for (int64_t t = bstart[b]; t < bstart[b + 1]; ++t) {
                         const int32_t j = bpts[t];
-                        u = fmin(u, cell_maxd2(demo[2 * j], demo[2 * j + 1], lx, ly));
+                        u = fmin(u, cell_maxd2(demo[2 * j], demo[2 * j + 1], lx, ly, 1.0));
                         any = 1;
                     }
                 }
@@ -421,7 +426,7 @@ int64_t orc_demo_index_build(const double* demo, int64_t m, int64_t* cell_start,
                 const int b = bx * 100 + by;
                 for (int64_t t = bstart[b]; t < bstart[b + 1]; ++t) {
                     const int32_t j = bpts[t];
-                    if (cell_mind2(demo[2 * j], demo[2 * j + 1], lx, ly) <= lim) {
+                    if (cell_mind2(demo[2 * j], demo[2 * j + 1], lx, ly, 1.0) <= lim) {
                         if (cand && total < cap) cand[total] = j;
                         ++total;
                     }
@@ -430,15 +435,13 @@ int64_t orc_demo_index_build(const double* demo, int64_t m, int64_t* cell_start,
         }
         for (int64_t o = 0; o < n_out; ++o) {
             const int32_t j = outside[o];
-            if (cell_mind2(demo[2 * j], demo[2 * j + 1], lx, ly) <= lim) {
+            if (cell_mind2(demo[2 * j], demo[2 * j + 1], lx, ly, 1.0) <= lim) {
                 if (cand && total < cap) cand[total] = j;
                 ++total;
             }
         }
-        if (cell_start) {
-            cell_start[cell] = first;
-            cell_start[cell + 1] = total;
-        }
+        cell_start[cell] = first;
+        cell_start[cell + 1] = total;
     }
     free(bstart);
     free(bpts);
@@ -446,11 +449,49 @@ int64_t orc_demo_index_build(const double* demo, int64_t m, int64_t* cell_start,
     return total;
 }
 
+/* the query index: cell_start [(100 R)^2 + 1] (nullable), cand [cap] (nullable = count only) */
+int64_t orc_demo_index_build(const double* demo, int64_t m, int64_t* cell_start, int32_t* cand,
+                             int64_t cap) {
+    int64_t* s1 = (int64_t*)malloc(10001 * sizeof(int64_t));
+    const int64_t t1 = index_level1(demo, m, s1, NULL, 0);
+    int32_t* c1 = (int32_t*)malloc((size_t)(t1 > 0 ? t1 : 1) * sizeof(int32_t));
+    index_level1(demo, m, s1, c1, t1);
+    const int R = ORC_DEMO_RES, side = 100 * ORC_DEMO_RES;
+    const double w = 1.0 / R;
+    int64_t total = 0;
+    for (int ix = 0; ix < side; ++ix) {
+        for (int iy = 0; iy < side; ++iy) {
+            const int k1 = (ix / R) * 100 + iy / R;
+            const double lx = (double)(ix / R) + (ix % R) * w, ly = (double)(iy / R) + (iy % R) * w;
+            double u = INFINITY;
+            for (int64_t t = s1[k1]; t < s1[k1 + 1]; ++t)
+                u = fmin(u, cell_maxd2(demo[2 * c1[t]], demo[2 * c1[t] + 1], lx, ly, w));
+            const double lim = u * (1.0 + 1e-12) + 1e-12;
+            const int64_t first = total;
+            for (int64_t t = s1[k1]; t < s1[k1 + 1]; ++t) {
+                const int32_t j = c1[t];
+                if (cell_mind2(demo[2 * j], demo[2 * j + 1], lx, ly, w) <= lim) {
+                    if (cand && total < cap) cand[total] = j;
+                    ++total;
+                }
+            }
+            if (cell_start) {
+                cell_start[(int64_t)ix * side + iy] = first;
+                cell_start[(int64_t)ix * side + iy + 1] = total;
+            }
+        }
+    }
+    free(s1);
+    free(c1);
+    return total;
+}
+
 /* robot.py:753 min distance through the index (brute force off the indexed world) */
 double orc_demo_min_idx(const double* demo, int64_t m, const int64_t* cell_start,
                         const int32_t* cand, double x, double y) {
     if (!(x >= 0.0 && x < 100.0 && y >= 0.0 && y < 100.0)) return orc_demo_min(demo, m, x, y);
-    const int k = (int)x * 100 + (int)y;
+    const int64_t k = (int64_t)(int)(x * ORC_DEMO_RES) * (100 * ORC_DEMO_RES) +
+                      (int)(y * ORC_DEMO_RES);
     double best = INFINITY;
     for (int64_t t = cell_start[k]; t < cell_start[k + 1]; ++t) {
         const int32_t j = cand[t];

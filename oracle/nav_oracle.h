@@ -115,9 +115,15 @@ void orc_vec_agent_step_batch(const orc_params_t* p, const float* speed, const f
                               int64_t replay_base, int64_t env0 /* global index of env 0 */,
                               const int64_t* idx_start, const int32_t* idx_cand /* nullable */);
 
-/* Exact nearest-demo index (per 1 x 1 dynamics cell, the candidates that can be nearest to any
- * query in the cell): cell_start [10001], cand [returned total]; call with cand = NULL (cap 0) to
- * size. orc_demo_min_idx = orc_demo_min through it, the same f64 value. */
+/* Exact nearest-demo index (per index cell of width 1/ORC_DEMO_RES, the candidates that can be
+ * nearest to any query in the cell; built from the 1 x 1 dynamics cells' lists):
+ * cell_start [(100 ORC_DEMO_RES)^2 + 1], cand [returned total]; call with cand = NULL (cap 0) to
+ * size. orc_demo_min_idx = orc_demo_min through it, the same f64 value.
+ * ORC_DEMO_RES: index cells per dynamics cell side (= libnavenv's nav_demo_index_res) */
+#ifndef ORC_DEMO_RES
+#define ORC_DEMO_RES 4
+#endif
+int32_t orc_demo_index_res(void);
 int64_t orc_demo_index_build(const double* demo_xy, int64_t m, int64_t* cell_start, int32_t* cand,
                              int64_t cap);
 double orc_demo_min_idx(const double* demo_xy, int64_t m, const int64_t* cell_start,

@@ -10,7 +10,8 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liborc.so")
+# ORC_LIB: another build of the same restatement (make asan-test: the sanitized one)
+LIB_PATH = os.environ.get("ORC_LIB") or os.path.join(HERE, "liborc.so")
 
 _dp = C.POINTER(C.c_double)
 _fp = C.POINTER(C.c_float)
@@ -87,6 +88,7 @@ def lib():
                                                C.c_int64, _dp, _dp, _dp, _dp, _u32p, _i32p, _i32p,
                                                _i32p, _dp, _dp, _dp, _fp, C.c_int64, C.c_int64,
                                                C.c_int64, _i64p, _i32p]
+        L.orc_demo_index_res.restype = C.c_int32
         L.orc_demo_index_build.restype = C.c_int64
         L.orc_demo_index_build.argtypes = [_dp, C.c_int64, _i64p, _i32p, C.c_int64]
         L.orc_single_env_run.restype = C.c_double
@@ -111,7 +113,8 @@ class DemoIndexCPU:
     def __init__(self, demo):
         self.demo = np.ascontiguousarray(demo, np.float64).reshape(-1, 2)
         m = len(self.demo)
-        self.start = np.zeros(10001, np.int64)
+        side = 100 * int(lib().orc_demo_index_res())
+        self.start = np.zeros(side * side + 1, np.int64)
         total = lib().orc_demo_index_build(ptr(self.demo, _dp), m, ptr(self.start, _i64p), None, 0)
         self.cand = np.zeros(max(total, 1), np.int32)
         lib().orc_demo_index_build(ptr(self.demo, _dp), m, ptr(self.start, _i64p),

@@ -394,21 +394,26 @@ __global__ __launch_bounds__(kBlock) void k_demo_min(const double2* __restrict__
     out[i] = sqrt(demo_min_global(demo, m, s.x, s.y));
 }
 
-// ---------------- exact bucketed nearest-demo index (1 x 1 cells = the dynamics cells) --------
-// For cell C = [i, i+1) x [j, j+1): U(C)^2 = min_q maxdist^2(q, C) bounds the nearest-demo
-// distance of every query inside C, so the nearest point p* satisfies mindist(p*, C) <= U(C).
-// The candidate list of C = { p : mindist^2(p, C) <= U^2 (1 + 1e-12) + 1e-12 } contains p* for
-// every query in C; the kernel then takes the same f64 minimum over it as over all points, so the
-// result is bit-identical to the brute force (tests/test_gpu_env.py checks it).
-NAV_DEV double cell_maxd2(double px, double py, double lx, double ly) {
-    const double fx = fmax(fabs(px - lx), fabs(px - (lx + 1.0)));
-    const double fy = fmax(fabs(py - ly), fabs(py - (ly + 1.0)));
+// ---------------- exact bucketed nearest-demo index ----------------
+// For a cell C of width w: U(C)^2 = min_q maxdist^2(q, C) bounds the nearest-demo distance of
+// every query inside C, so the nearest point p* satisfies mindist(p*, C) <= U(C). The candidate
+// list of C = { p : mindist^2(p, C) <= U^2 (1 + 1e-12) + 1e-12 } contains p* for every query in C;
+// the query takes the same f64 minimum over it as over all points, so the result is
+// bit-identical to the brute force (tests/test_gpu_env.py checks it).
+// Two levels: the 1 x 1 dynamics cells over all points of the group (plan / scan / fill), then
+// each dynamics cell's kRes x kRes index cells over its parent's list only (subplan / subscan /
+// subfill): a subcell S of C has mindist(p, C) <= mindist(p, S) and U(S) <= U(C), so every
+// candidate of S is a candidate of C, and U(S) taken over C's list is still a real point's
+// maxdist, i.e. a valid bound. The queries use the index-cell lists.
+NAV_DEV double cell_maxd2(double px, double py, double lx, double ly, double w = 1.0) {
+    const double fx = fmax(fabs(px - lx), fabs(px - (lx + w)));
+    const double fy = fmax(fabs(py - ly), fabs(py - (ly + w)));
     return fx * fx + fy * fy;
 }
 
-NAV_DEV double cell_mind2(double px, double py, double lx, double ly) {
-    const double nx = fmax(0.0, fmax(lx - px, px - (lx + 1.0)));
-    const double ny = fmax(0.0, fmax(ly - py, py - (ly + 1.0)));
+NAV_DEV double cell_mind2(double px, double py, double lx, double ly, double w = 1.0) {
+    const double nx = fmax(0.0, fmax(lx - px, px - (lx + w)));
+    const double ny = fmax(0.0, fmax(ly - py, py - (ly + w)));
     return nx * nx + ny * ny;
 }
 
@@ -460,31 +465,45 @@ __global__ __launch_bounds__(kBlock) void k_demo_index_plan(const double2* __res
     }
 }
 
-// exclusive scan of counts [n] into start [n + 1] (one workgroup; set-up time only)
-__global__ __launch_bounds__(kBlock) void k_scan_counts(const int32_t* __restrict__ count,
-                                                        int64_t n, int64_t* __restrict__ start) {
-    __shared__ int64_t part[kBlock];
-    const int64_t per = (n + kBlock - 1) / kBlock;
-    const int64_t a = threadIdx.x * per, b = a + per < n ? a + per : n;
-    int64_t s = 0;
-    for (int64_t i = a; i < b; ++i) s += count[i];
-    part[threadIdx.x] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int64_t run = 0;
-        for (int t = 0; t < kBlock; ++t) {
-            const int64_t v = part[t];
-            part[t] = run;
-            run += v;
+// exclusive scan of counts [n] into start [n + 1] (set-up time only): one 1024-thread workgroup
+// walks the array in coalesced tiles of 4096 (4 per thread), a wave scan + wave-total scan per
+// tile, carrying the running total (n = 10.24 M index cells at the bench config: ~2 500 tiles).
+constexpr int kScanThreads = 1024;
+__global__ __launch_bounds__(kScanThreads) void k_scan_counts(const int32_t* __restrict__ count,
+                                                              int64_t n,
+                                                              int64_t* __restrict__ start) {
+    __shared__ int64_t wtot[kScanThreads / 64];
+    __shared__ int64_t carry_s;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    int64_t carry = 0;
+    for (int64_t t0 = 0; t0 < n; t0 += 4 * kScanThreads) {
+        const int64_t i0 = t0 + 4 * (int64_t)tid;
+        int64_t c[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) c[u] = i0 + u < n ? count[i0 + u] : 0;
+        const int64_t mine = c[0] + c[1] + c[2] + c[3];
+        int64_t v = mine;  // inclusive scan within the wave
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int64_t up = __shfl_up(v, o, 64);
+            if (lane >= o) v += up;
         }
-        start[n] = run;
+        if (lane == 63) wtot[wv] = v;
+        __syncthreads();
+        int64_t before = carry;
+        for (int w = 0; w < wv; ++w) before += wtot[w];
+        int64_t run = before + v - mine;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (i0 + u < n) start[i0 + u] = run;
+            run += c[u];
+        }
+        if (tid == kScanThreads - 1) carry_s = run;
+        __syncthreads();
+        carry = carry_s;
+        __syncthreads();
     }
-    __syncthreads();
-    int64_t run = part[threadIdx.x];
-    for (int64_t i = a; i < b; ++i) {
-        start[i] = run;
-        run += count[i];
-    }
+    if (tid == 0) start[n] = carry;
 }
 
 // grid = (cells, groups): write the cell's candidate indices (group-relative, ascending)
@@ -527,7 +546,90 @@ __global__ __launch_bounds__(kBlock) void k_demo_index_fill(const double2* __res
     }
 }
 
-// The demo-proximity term through the index: lane = env, its cell = the dynamics cell of s'.
+NAV_DEV double wave_min(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// grid = (dynamics cells, groups), 4 waves: wave w takes index subcells w, w + 4, ... of its
+// dynamics cell; bound and count of each from the parent's candidate list (lane-strided).
+__global__ __launch_bounds__(kBlock) void k_demo_index_subplan(const double2* __restrict__ demo,
+                                                               const int64_t* __restrict__ off,
+                                                               const int64_t* __restrict__ start1,
+                                                               const int32_t* __restrict__ cand1,
+                                                               double* __restrict__ bound,
+                                                               int32_t* __restrict__ count) {
+    const int cell = blockIdx.x, g = blockIdx.y, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const double2* pts = demo + (off ? off[g] : 0);
+    const int64_t k1 = (int64_t)g * kCells + cell;
+    const int64_t a = start1[k1], b = start1[k1 + 1];
+    const int cx = cell / NAV_WORLD_CELLS, cy = cell % NAV_WORLD_CELLS;
+    constexpr double w = 1.0 / kRes;
+    for (int sc = wv; sc < kRes * kRes; sc += kBlock / 64) {
+        const int sx = sc / kRes, sy = sc % kRes;
+        const double lx = cx + sx * w, ly = cy + sy * w;
+        double u = __builtin_inf();
+        for (int64_t t = a + lane; t < b; t += 64) {
+            const double2 q = pts[cand1[t]];
+            u = fmin(u, cell_maxd2(q.x, q.y, lx, ly, w));
+        }
+        u = wave_min(u);
+        const double lim = u * (1.0 + 1e-12) + 1e-12;
+        int c = 0;
+        for (int64_t t = a + lane; t < b; t += 64) {
+            const double2 q = pts[cand1[t]];
+            c += cell_mind2(q.x, q.y, lx, ly, w) <= lim ? 1 : 0;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+        if (lane == 0) {
+            const int64_t k = (int64_t)g * kIdxCells + (int64_t)(cx * kRes + sx) * kSide +
+                              (cy * kRes + sy);
+            bound[k] = lim;
+            count[k] = c;
+        }
+    }
+}
+
+// the index cells' candidate lists, in their parent list's (ascending) order
+__global__ __launch_bounds__(kBlock) void k_demo_index_subfill(const double2* __restrict__ demo,
+                                                               const int64_t* __restrict__ off,
+                                                               const int64_t* __restrict__ start1,
+                                                               const int32_t* __restrict__ cand1,
+                                                               const double* __restrict__ bound,
+                                                               const int64_t* __restrict__ start,
+                                                               int32_t* __restrict__ cand) {
+    const int cell = blockIdx.x, g = blockIdx.y, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const double2* pts = demo + (off ? off[g] : 0);
+    const int64_t k1 = (int64_t)g * kCells + cell;
+    const int64_t a = start1[k1], b = start1[k1 + 1];
+    const int cx = cell / NAV_WORLD_CELLS, cy = cell % NAV_WORLD_CELLS;
+    constexpr double w = 1.0 / kRes;
+    for (int sc = wv; sc < kRes * kRes; sc += kBlock / 64) {
+        const int sx = sc / kRes, sy = sc % kRes;
+        const double lx = cx + sx * w, ly = cy + sy * w;
+        const int64_t k = (int64_t)g * kIdxCells + (int64_t)(cx * kRes + sx) * kSide +
+                          (cy * kRes + sy);
+        const double lim = bound[k];
+        int64_t run = start[k];
+        for (int64_t t0 = a; t0 < b; t0 += 64) {
+            const int64_t t = t0 + lane;
+            bool take = false;
+            int32_t j = 0;
+            if (t < b) {
+                j = cand1[t];
+                const double2 q = pts[j];
+                take = cell_mind2(q.x, q.y, lx, ly, w) <= lim;
+            }
+            const unsigned long long bal = __ballot(take);
+            if (take) cand[run + __popcll(bal & ((1ull << lane) - 1ull))] = j;
+            run += __popcll(bal);
+        }
+    }
+}
+
+// The demo-proximity term through the index: lane = env, its cell = the index cell of s'.
 __global__ __launch_bounds__(kBlock) void k_demo_reward_idx(nav_params p, int64_t n,
                                                             const double2* __restrict__ ns,
                                                             const double* __restrict__ gterm,
@@ -546,8 +648,8 @@ __global__ __launch_bounds__(kBlock) void k_demo_reward_idx(nav_params p, int64_
 }
 
 // One training tick per env (see navenv.h nav_agent_step). DEMO: the demo-proximity reward of
-// flagged envs through the index in the same launch (nav_agent_step_indexed), so the replay row
-// is written once, with the final reward. One statistics row per wave (64 envs).
+// flagged envs through the index in the same launch (nav_agent_step_indexed): the block's demo
+// pass walks all its flagged envs' candidate lists together. One statistics row per wave.
 template <bool DEMO>
 __global__ __launch_bounds__(kBlock) void k_agent_step(nav_params p, nav_env_soa env,
                                                        const float2* __restrict__ field,
@@ -558,9 +660,15 @@ __global__ __launch_bounds__(kBlock) void k_agent_step(nav_params p, nav_env_soa
                                                        double* __restrict__ reward_out) {
     const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     TickStats st{0.f, 0.f, 0.f, 0.f, 0.f};
+    DemoPend pend{false, false, 0.0, make_double2(0.0, 0.0)};
     if (e < env.n)
-        st = agent_tick<DEMO>(p, env, field, e, action[e], rows, cap, base, out, d,
-                              demo_pending != 0, reward_out);
+        st = agent_tick<DEMO>(p, env, field, e, action[e], rows, cap, base, out,
+                              demo_pending != 0, pend);
+    if (DEMO) {
+        __shared__ DemoScratch<kBlock, kBlock> scratch;
+        demo_pass<kBlock, kBlock>(p, d, scratch, pend, e, reinterpret_cast<float*>(rows), cap,
+                                  base, reward_out);
+    }
     if (out.block_stats && e - (threadIdx.x & 63) < env.n) wave_stats(st, out.block_stats, e);
 }
 
@@ -927,7 +1035,7 @@ int nav_demo_index_plan(const double* demo_xy, const int64_t* demo_off, int32_t 
 int nav_demo_index_scan(const int32_t* cell_count, int32_t n_groups, int64_t* cell_start,
                         void* stream) {
     if (!cell_count || !cell_start || n_groups < 1) return NAV_EINVAL;
-    hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(kBlock), 0, S(stream), cell_count,
+    hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(kScanThreads), 0, S(stream), cell_count,
                        (int64_t)n_groups * kCells, cell_start);
     NAV_CHECK_LAUNCH();
     return 0;
@@ -942,6 +1050,44 @@ int nav_demo_index_fill(const double* demo_xy, const int64_t* demo_off, int32_t 
     hipLaunchKernelGGL(k_demo_index_fill, dim3(kCells, n_groups), dim3(kBlock), 0, S(stream),
                        reinterpret_cast<const double2*>(demo_xy), demo_off, m, cell_bound,
                        cell_start, cand);
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int32_t nav_demo_index_res(void) { return kRes; }
+
+int nav_demo_index_subplan(const double* demo_xy, const int64_t* demo_off, int32_t n_groups,
+                           const int64_t* cell_start, const int32_t* cand, double* sub_bound,
+                           int32_t* sub_count, void* stream) {
+    if (!demo_xy || n_groups < 1 || (!demo_off && n_groups != 1) || !cell_start || !cand ||
+        !sub_bound || !sub_count)
+        return NAV_EINVAL;
+    hipLaunchKernelGGL(k_demo_index_subplan, dim3(kCells, n_groups), dim3(kBlock), 0, S(stream),
+                       reinterpret_cast<const double2*>(demo_xy), demo_off, cell_start, cand,
+                       sub_bound, sub_count);
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_demo_index_subscan(const int32_t* sub_count, int32_t n_groups, int64_t* sub_start,
+                           void* stream) {
+    if (!sub_count || !sub_start || n_groups < 1) return NAV_EINVAL;
+    hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(kScanThreads), 0, S(stream), sub_count,
+                       (int64_t)n_groups * kIdxCells, sub_start);
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_demo_index_subfill(const double* demo_xy, const int64_t* demo_off, int32_t n_groups,
+                           const int64_t* cell_start, const int32_t* cand,
+                           const double* sub_bound, const int64_t* sub_start, int32_t* sub_cand,
+                           void* stream) {
+    if (!demo_xy || n_groups < 1 || (!demo_off && n_groups != 1) || !cell_start || !cand ||
+        !sub_bound || !sub_start || !sub_cand)
+        return NAV_EINVAL;
+    hipLaunchKernelGGL(k_demo_index_subfill, dim3(kCells, n_groups), dim3(kBlock), 0, S(stream),
+                       reinterpret_cast<const double2*>(demo_xy), demo_off, cell_start, cand,
+                       sub_bound, sub_start, sub_cand);
     NAV_CHECK_LAUNCH();
     return 0;
 }

@@ -571,16 +571,23 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
             if (a.action_out) a.action_out[r * 2 + j] = v;
         }
         __syncthreads();
+        DemoPend pend{false, false, 0.0, make_double2(0.0, 0.0)};
         if (tid < TM) {
             TickStats st{0.f, 0.f, 0.f, 0.f, 0.f};
             if (r < M) {
                 const double2 av = make_double2(act_lds[tid * 2], act_lds[tid * 2 + 1]);
                 st = a.demo.cand ? agent_tick<true>(a.p, a.env, a.field, r, av, a.rows, a.cap,
-                                                    a.base, a.sout, a.demo, true, a.reward_out)
+                                                    a.base, a.sout, true, pend)
                                  : agent_tick<false>(a.p, a.env, a.field, r, av, a.rows, a.cap,
-                                                     a.base, a.sout, a.demo, false, a.reward_out);
+                                                     a.base, a.sout, false, pend);
             }
             if (a.sout.block_stats && row0 + (tid & ~63) < M) wave_stats(st, a.sout.block_stats, r);
+        }
+        if (a.demo.cand) {  // block-uniform: the demo pass of the block's envs, all threads
+            // the LDS rows are done with (the actions live in xin)
+            auto* scratch = reinterpret_cast<DemoScratch<TM, kBlock>*>(act);
+            demo_pass<TM, kBlock>(a.p, a.demo, *scratch, pend, r, reinterpret_cast<float*>(a.rows),
+                                  a.cap, a.base, a.reward_out);
         }
         return;
     }

@@ -13,6 +13,21 @@ constexpr int kCells = NAV_WORLD_CELLS * NAV_WORLD_CELLS;
 #define NAV_DEMO_BATCH 16
 #endif
 constexpr int kDemoBatch = NAV_DEMO_BATCH;  // candidates per dependent-load trip (indexed reward)
+// Resolution of the nearest-demo index: kRes x kRes index cells per dynamics cell (a power of 2,
+// so s * kRes and the cell edges are exact). The query cell of s is (int)(s.x * kRes),
+// (int)(s.y * kRes); kIdxCells index cells per group.
+#ifndef NAV_DEMO_RES
+#define NAV_DEMO_RES 4
+#endif
+constexpr int kRes = NAV_DEMO_RES;
+static_assert(kRes >= 1 && (kRes & (kRes - 1)) == 0, "index resolution: a power of 2");
+constexpr int kSide = NAV_WORLD_CELLS * kRes;
+constexpr int64_t kIdxCells = (int64_t)kSide * kSide;
+
+NAV_DEV bool in_index(double2 s) { return s.x >= 0.0 && s.x < 100.0 && s.y >= 0.0 && s.y < 100.0; }
+NAV_DEV int64_t index_cell(int64_t g, double2 s) {
+    return g * kIdxCells + (int64_t)(int)(s.x * kRes) * kSide + (int)(s.y * kRes);
+}
 
 // Robot.process_transition (robot.py:645-675) for env e given (s, a, s'): reward without the
 // demo term (robot.py:727-762; the term is added by the demo pass for flagged envs),
@@ -109,8 +124,8 @@ NAV_DEV double sqd(double x, double y, double px, double py) {
 }
 
 // The demo set of env e through the exact bucketed index (nav_demo_index_*): squared distance to
-// the nearest demonstration point of its group (robot.py:753), the candidates of the dynamics
-// cell of s' (brute force outside the indexed cells).
+// the nearest demonstration point of its group (robot.py:753), the candidates of the index cell
+// of s' (brute force outside the indexed world).
 struct DemoIdx {
     const double2* demo;
     const int64_t* off;
@@ -123,8 +138,8 @@ NAV_DEV double demo_min2_idx(const DemoIdx& d, int64_t e, double2 s) {
     const int64_t g = d.off ? e / d.epg : 0;
     const double2* pts = d.demo + (d.off ? d.off[g] : 0);
     double best = __builtin_inf();
-    if (s.x >= 0.0 && s.x < 100.0 && s.y >= 0.0 && s.y < 100.0) {
-        const int64_t k = g * kCells + (int64_t)((int)s.x * NAV_WORLD_CELLS + (int)s.y);
+    if (in_index(s)) {
+        const int64_t k = index_cell(g, s);
         const int64_t a = d.start[k], b = d.start[k + 1];
         // kDemoBatch candidates per trip: their indices, then their points, are independent loads
         // (two dependent round trips per batch instead of per candidate; a wave runs as many
@@ -159,11 +174,20 @@ NAV_DEV double demo_reward_of(const nav_params& p, double gterm, double min2, bo
     return r;
 }
 
+// The demo term of one env, deferred by the tick to the block's demo pass (its replay row is
+// written with the goal-term reward first; the pass overwrites the reward word).
+struct DemoPend {
+    bool need, stuck;
+    double gt;
+    double2 ns;
+};
+
 // Everything one training tick does for env e given its action (see navenv.h nav_agent_step):
-// Environment.step (environment.py:122-127) -> Robot.process_transition (robot.py:645-675, the
-// demo term through the index when DEMO) -> replay push -> the next tick's end-of-episode check
-// and Robot.reset + Environment.reset (robot.py:479-506, environment.py:130-137). Returns the
-// per-env statistics (reward w/o demo term, done, goal, stuck, ended) for the block reduction.
+// Environment.step (environment.py:122-127) -> Robot.process_transition (robot.py:645-675) ->
+// replay push -> the next tick's end-of-episode check and Robot.reset + Environment.reset
+// (robot.py:479-506, environment.py:130-137). DEMO: a demo pass follows in the same launch; the
+// env's demo term (robot.py:749-757) is returned in `pend` for it. Returns the per-env statistics
+// (reward w/o demo term, done, goal, stuck, ended) for the block reduction.
 struct TickStats {
     float r, done, goal, stuck, ended;
 };
@@ -172,8 +196,7 @@ template <bool DEMO>
 NAV_DEV TickStats agent_tick(const nav_params& p, const nav_env_soa& env,
                              const float2* __restrict__ field, int64_t e, double2 a,
                              float4* __restrict__ rows, int64_t cap, int64_t base,
-                             const nav_step_out& out, const DemoIdx& d, bool demo_pending,
-                             double* __restrict__ reward_out) {
+                             const nav_step_out& out, bool demo_pending, DemoPend& pend) {
     double2* state = reinterpret_cast<double2*>(env.state);
     const double2 s = state[e];
     const uint32_t meta = env.meta[e];
@@ -184,12 +207,13 @@ NAV_DEV TickStats agent_tick(const nav_params& p, const nav_env_soa& env,
     double2 ns = dynamics(field, s, a);
     if (!in_world(ns)) ns = s;
     TransOut t = transition(p, env, e, s, a, ns, meta, plan, path, DEMO || demo_pending);
-    double r = t.r;
-    if (DEMO && t.demo_term) {
-        r = demo_reward_of(p, t.gt, demo_min2_idx(d, e, ns), t.stuck);
-        if (reward_out) reward_out[e] = r;
+    if (DEMO) {
+        pend.need = t.demo_term;
+        pend.stuck = t.stuck;
+        pend.gt = t.gt;
+        pend.ns = ns;
     }
-    push_row(rows, (base + e) % cap, s, a, r, ns, t.done);
+    push_row(rows, (base + e) % cap, s, a, t.r, ns, t.done);
 
     // next tick: robot.py:479-487 end check -> Robot.reset (492-506) + Environment.reset
     const bool ended = t.done || (t.meta & (M_GOAL | M_STUCK));
@@ -221,6 +245,142 @@ NAV_DEV TickStats agent_tick(const nav_params& p, const nav_env_soa& env,
     st.stuck = t.stuck ? 1.f : 0.f;
     st.ended = ended ? 1.f : 0.f;
     return st;
+}
+
+// ---- block-cooperative demo pass (the indexed demo term of a block's flagged envs) ----
+// One lane per env walking its own candidate list makes a wave as slow as its longest list (the
+// CEM demo sets: mean 36 candidates per flagged env, per-wave max ~175, p90 350, cells up to 992).
+// Here the block's candidate lists are concatenated (inclusive prefix of the lengths in LDS) and
+// every thread of the block takes kDemoFlat consecutive entries per trip, whichever envs they
+// belong to: a block's time is its total candidate count / block size. Per-env minima are combined
+// with LDS 64-bit atomic min on the bit patterns (non-negative doubles order as unsigned
+// integers), so the result is the same f64 minimum over the same candidate set, bit for bit.
+#ifndef NAV_DEMO_FLAT
+#define NAV_DEMO_FLAT 8
+#endif
+constexpr int kDemoFlat = NAV_DEMO_FLAT;
+
+template <int NE, int NT>
+struct DemoScratch {
+    int32_t incl[NE];       // inclusive prefix of the candidate-list lengths
+    int32_t wsum[NE / 64];  // per-wave totals of the scan
+    int64_t first[NE];      // index into cand of the env's first candidate
+    int64_t pbase[NE];      // demo offset of the env's group
+    double sx[NE], sy[NE];  // the env's s'
+    unsigned long long best[NE];
+};
+
+// All NT threads of the block call this (it synchronises). Threads 0..NE-1 own env slots; `pend`
+// of a non-owner or an env past n has need = false. Writes the final reward of every flagged env
+// into its replay row (word 4) and reward_out.
+template <int NE, int NT>
+NAV_DEV void demo_pass(const nav_params& p, const DemoIdx& d, DemoScratch<NE, NT>& S,
+                       const DemoPend& pend, int64_t e, float* __restrict__ rows, int64_t cap,
+                       int64_t base, double* __restrict__ reward_out) {
+    static_assert(NE % 64 == 0 && NE <= NT, "env slots: whole waves, at most one per thread");
+    const int tid = threadIdx.x, lane = tid & 63;
+    const bool owner = tid < NE;
+    bool brute = false;
+    int len = 0;
+    int64_t g = 0;
+    if (owner) {
+        int64_t first = 0;
+        if (pend.need) {
+            g = d.off ? e / d.epg : 0;
+            const double2 s = pend.ns;
+            if (in_index(s)) {
+                const int64_t k = index_cell(g, s);
+                first = d.start[k];
+                len = (int)(d.start[k + 1] - first);
+            } else {
+                brute = true;  // outside the indexed cells
+            }
+        }
+        S.first[tid] = first;
+        S.pbase[tid] = d.off ? d.off[g] : 0;
+        S.sx[tid] = pend.ns.x;
+        S.sy[tid] = pend.ns.y;
+        S.best[tid] = 0x7ff0000000000000ull;  // +inf
+        // inclusive scan of len within the wave
+        int v = len;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int u = __shfl_up(v, o, 64);
+            if (lane >= o) v += u;
+        }
+        if (lane == 63) S.wsum[tid >> 6] = v;
+        len = v;  // wave-inclusive prefix
+    }
+    __syncthreads();
+    if (owner) {
+        int add = 0;
+        for (int w = 0; w < (tid >> 6); ++w) add += S.wsum[w];
+        S.incl[tid] = len + add;
+    }
+    __syncthreads();
+    const int T = S.incl[NE - 1];
+    for (int t0 = tid * kDemoFlat; t0 < T; t0 += NT * kDemoFlat) {
+        // owner slot of entry t0: the first slot whose inclusive prefix exceeds it
+        int lo = 0, hi = NE - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (S.incl[mid] > t0) hi = mid;
+            else lo = mid + 1;
+        }
+        int o = lo;
+        int lo_b = o ? S.incl[o - 1] : 0, hi_b = S.incl[o];
+        int ow[kDemoFlat];
+        int64_t ci[kDemoFlat];
+#pragma unroll
+        for (int u = 0; u < kDemoFlat; ++u) {
+            const int t = t0 + u;
+            if (t < T) {
+                while (t >= hi_b) {
+                    lo_b = hi_b;
+                    ++o;
+                    hi_b = S.incl[o];
+                }
+                ow[u] = o;
+                ci[u] = S.first[o] + (t - lo_b);
+            } else {  // past the end: repeat the previous entry (a duplicate cannot change a min)
+                ow[u] = ow[u > 0 ? u - 1 : 0];
+                ci[u] = ci[u > 0 ? u - 1 : 0];
+            }
+        }
+        int32_t c[kDemoFlat];
+#pragma unroll
+        for (int u = 0; u < kDemoFlat; ++u) c[u] = d.cand[ci[u]];
+        double2 q[kDemoFlat];
+#pragma unroll
+        for (int u = 0; u < kDemoFlat; ++u) q[u] = d.demo[S.pbase[ow[u]] + c[u]];
+        int cur_o = ow[0];
+        double cur = sqd(S.sx[cur_o], S.sy[cur_o], q[0].x, q[0].y);
+#pragma unroll
+        for (int u = 1; u < kDemoFlat; ++u) {
+            const double v = sqd(S.sx[ow[u]], S.sy[ow[u]], q[u].x, q[u].y);
+            if (ow[u] == cur_o) {
+                cur = fmin(cur, v);
+            } else {
+                atomicMin(&S.best[cur_o], (unsigned long long)__double_as_longlong(cur));
+                cur_o = ow[u];
+                cur = v;
+            }
+        }
+        atomicMin(&S.best[cur_o], (unsigned long long)__double_as_longlong(cur));
+    }
+    __syncthreads();
+    if (owner && pend.need) {
+        double m2;
+        if (brute) {
+            const double2* pts = d.demo + S.pbase[tid];
+            m2 = demo_min_global(pts, d.off ? d.off[g + 1] - d.off[g] : 0, pend.ns.x, pend.ns.y);
+        } else {
+            m2 = __longlong_as_double((long long)S.best[tid]);
+        }
+        const double r = demo_reward_of(p, pend.gt, m2, pend.stuck);
+        rows[((base + e) % cap) * NAV_ROW + 4] = (float)r;
+        if (reward_out) reward_out[e] = r;
+    }
 }
 
 // Per-64-env statistics row (one wave = 64 consecutive envs): wave shuffles, lane 0 writes row

@@ -13,7 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # NAV_LIB: load another build of the same ABI instead (A/B timing of kernel variants only)
 LIB_PATH = os.environ.get("NAV_LIB") or os.path.join(HERE, "libnavenv.so")
 NAV_EINVAL = -100000
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 _dp = C.POINTER(C.c_double)
 _vp = C.c_void_p
@@ -83,6 +83,10 @@ SIGNATURES = [
     ("nav_demo_index_plan", C.c_int, [_vp, _vp, C.c_int32, C.c_int64, _vp, _vp, _vp]),
     ("nav_demo_index_scan", C.c_int, [_vp, C.c_int32, _vp, _vp]),
     ("nav_demo_index_fill", C.c_int, [_vp, _vp, C.c_int32, C.c_int64, _vp, _vp, _vp, _vp]),
+    ("nav_demo_index_res", C.c_int32, []),
+    ("nav_demo_index_subplan", C.c_int, [_vp, _vp, C.c_int32, _vp, _vp, _vp, _vp, _vp]),
+    ("nav_demo_index_subscan", C.c_int, [_vp, C.c_int32, _vp, _vp]),
+    ("nav_demo_index_subfill", C.c_int, [_vp, _vp, C.c_int32, _vp, _vp, _vp, _vp, _vp, _vp]),
     ("nav_demo_reward_indexed", C.c_int, [_P(NavParams), C.c_int64, _vp, _vp, _vp, _vp, _vp,
                                           C.c_int32, _vp, _vp, _P(NavReplay), C.c_int64, _vp,
                                           _vp]),
@@ -152,7 +156,7 @@ SIGNATURES = [
 # Entry points that return int64 counts (negative = error) rather than a status code.
 _COUNT_FNS = {"nav_mlp_param_count", "nav_mlp_packed_count", "nav_mlp_mask_count",
               "nav_mlp_row_blocks", "nav_mlp_edge_count", "nav_mlp_hidden_count",
-              "nav_mlp_wgrad_splits"}
+              "nav_mlp_wgrad_splits", "nav_demo_index_res"}
 
 
 class NavError(RuntimeError):

@@ -24,29 +24,52 @@ def make_field(speed, angle, device="cuda"):
 
 
 class DemoIndex:
-    """Exact bucketed nearest-demo index (nav_demo_index_*): per (group, dynamics cell) the
-    ascending list of demonstration points that can be nearest to any state in the cell. The
-    indexed reward equals the brute-force one bit for bit; it visits ~11 points instead of
-    11 355 for the reference's demo sets (tests/test_gpu_env.py)."""
+    """Exact bucketed nearest-demo index (nav_demo_index_*): per (group, index cell) the list of
+    demonstration points that can be nearest to any state in the cell. Two levels: the 1 x 1
+    dynamics cells over every point of the group, then R x R index cells per dynamics cell
+    (R = nav_demo_index_res()) over their parent's list. `cell_start` / `cand` are the index-cell
+    lists the reward kernels walk. The indexed reward equals the brute-force one bit for bit
+    (tests/test_gpu_env.py)."""
 
-    CELLS = 100 * 100
+    L1_CELLS = 100 * 100
 
     def __init__(self, demo_xy, demo_off=None, stream=None):
         dev = demo_xy.device
         G = 1 if demo_off is None else demo_off.shape[0] - 1
         m = demo_xy.shape[0] if demo_off is None else 0
         s = stream_handle(stream)
+        L = lib()
+        self.res = int(L.nav_demo_index_res())
+        self.side = 100 * self.res
+        self.CELLS = self.side * self.side
+        # level 1: dynamics cells over all points
+        bound1 = torch.zeros(G * self.L1_CELLS, dtype=torch.float64, device=dev)
+        count1 = torch.zeros(G * self.L1_CELLS, dtype=torch.int32, device=dev)
+        start1 = torch.zeros(G * self.L1_CELLS + 1, dtype=torch.int64, device=dev)
+        L.nav_demo_index_plan(ptr(demo_xy), ptr(demo_off), G, m, ptr(bound1), ptr(count1), s)
+        L.nav_demo_index_scan(ptr(count1), G, ptr(start1), s)
+        total1 = int(start1[-1].item())
+        cand1 = torch.zeros(max(total1, 1), dtype=torch.int32, device=dev)
+        L.nav_demo_index_fill(ptr(demo_xy), ptr(demo_off), G, m, ptr(bound1), ptr(start1),
+                              ptr(cand1), s)
+        # level 2: the query index
         bound = torch.zeros(G * self.CELLS, dtype=torch.float64, device=dev)
         count = torch.zeros(G * self.CELLS, dtype=torch.int32, device=dev)
         self.cell_start = torch.zeros(G * self.CELLS + 1, dtype=torch.int64, device=dev)
-        lib().nav_demo_index_plan(ptr(demo_xy), ptr(demo_off), G, m, ptr(bound), ptr(count), s)
-        lib().nav_demo_index_scan(ptr(count), G, ptr(self.cell_start), s)
+        L.nav_demo_index_subplan(ptr(demo_xy), ptr(demo_off), G, ptr(start1), ptr(cand1),
+                                 ptr(bound), ptr(count), s)
+        L.nav_demo_index_subscan(ptr(count), G, ptr(self.cell_start), s)
         total = int(self.cell_start[-1].item())
         self.cand = torch.zeros(max(total, 1), dtype=torch.int32, device=dev)
-        lib().nav_demo_index_fill(ptr(demo_xy), ptr(demo_off), G, m, ptr(bound),
-                                  ptr(self.cell_start), ptr(self.cand), s)
+        L.nav_demo_index_subfill(ptr(demo_xy), ptr(demo_off), G, ptr(start1), ptr(cand1),
+                                 ptr(bound), ptr(self.cell_start), ptr(self.cand), s)
         self.total = total
+        self.total_l1 = total1
         self.mean_candidates = total / float(G * self.CELLS)
+
+    def cell_of(self, g, x, y):
+        """index cell of state (x, y) of group g (torch tensors), as the kernels compute it"""
+        return g * self.CELLS + (x * self.res).long() * self.side + (y * self.res).long()
 
 
 class ReplayRing:

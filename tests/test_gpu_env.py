@@ -338,8 +338,11 @@ def test_agent_step_replays_reference_trace(nav):
 
 
 def test_demo_index_bit_exact_vs_brute_force(nav, orc):
-    """The bucketed demo index returns the brute-force minimum bit for bit (same f64 values)."""
-    from nav.vec_env import DemoIndex, ReplayRing, VecEnv
+    """The two-level demo index returns the brute-force minimum bit for bit (same f64 values),
+    through the tick's block-cooperative demo pass (nav_agent_step_indexed) and the per-env
+    indexed pass (nav_demo_reward_indexed), on states at dynamics-cell and index-cell corners, on
+    demo points, and packed around the demo path (the longest candidate lists)."""
+    from nav.vec_env import ReplayRing, VecEnv
     t = golden("trace.npz")
     demo = t["demo_set"]
     n, epg = 4096, 1024
@@ -347,26 +350,35 @@ def test_demo_index_bit_exact_vs_brute_force(nav, orc):
     pts = np.concatenate([demo + 3.0 * k for k in range(G)])
     off = np.arange(G + 1, dtype=np.int64) * len(demo)
     rng = np.random.default_rng(9)
+    s = rng.uniform(0, 99, (n, 2))
+    s[:512] = np.floor(s[:512])  # exactly on dynamics-cell corners
+    s[512:1024] = demo[rng.integers(0, len(demo), 512)].clip(0, 98.99)  # on demo points
+    s[1024:1536] = np.floor(s[1024:1536] * 4) / 4  # on index-cell corners
+    near = demo[rng.integers(0, len(demo), 1536)] + rng.uniform(-0.4, 0.4, (1536, 2))
+    s[1536:3072] = near.clip(0, 98.99)  # packed around the demo path
+    # envs of group g query demo set g = the trace's demo shifted by 3 g
+    shift = 3.0 * (np.arange(n) // epg)
+    for lo, hi in ((512, 1024), (1536, 3072)):
+        s[lo:hi] += shift[lo:hi, None]
+    s = s.clip(0, 99.99)
     rewards = []
-    for use_index in (True, False):
+    for mode in ("fused", "per_env", "brute"):
         env = VecEnv(n, field_of(t["speed"], t["angle"]), seed=5, envs_per_group=epg)
-        env.set_demo(pts, off, index=use_index)
-        s = rng.uniform(0, 99, (n, 2))
-        s[:512] = np.floor(s[:512])  # exactly on cell corners
-        s[512:1024] = demo[rng.integers(0, len(demo), 512)].clip(0, 98.99)  # on demo points
-        rng = np.random.default_rng(9)  # same states for both passes
+        env.set_demo(pts, off, index=mode != "brute")
+        env.fuse_demo = mode == "fused"
         env.state.copy_(torch.tensor(s))
         rep = ReplayRing(n, DEV)
         r = torch.zeros(n, dtype=torch.float64, device=DEV)
         env.agent_step(torch.zeros(n, 2, dtype=torch.float64, device=DEV), rep, reward_out=r)
-        rewards.append((r.cpu().numpy(), env.flags.cpu().numpy()))
-        if use_index:
+        rewards.append((r.cpu().numpy(), env.flags.cpu().numpy(), rep.rows.cpu().numpy()))
+        if mode != "brute":
             assert env.demo_index.mean_candidates < 200
-    (ri, fi), (rb, fb) = rewards
-    assert np.array_equal(fi, fb)
+    (ri, fi, wi), (rp, fp, wp), (rb, fb, wb) = rewards
+    assert np.array_equal(fi, fb) and np.array_equal(fp, fb)
     m = (fi & 16) != 0
     assert m.sum() > n // 2
-    assert np.array_equal(ri[m], rb[m])
+    assert np.array_equal(ri[m], rb[m]) and np.array_equal(rp[m], rb[m])
+    assert np.array_equal(wi, wb) and np.array_equal(wp, wb)
 
 
 def test_compute_reward_kernel_vs_oracle(nav, orc):

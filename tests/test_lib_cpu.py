@@ -56,7 +56,11 @@ def test_gfx950_code_object_present(navlib):
 def test_abi_and_layout(navlib):
     from nav.mlp import layer_offsets
     from nav._lib import NavMlp
-    assert navlib.nav_abi_version() == 5
+    assert navlib.nav_abi_version() == 6
+    assert navlib.nav_demo_index_res() in (1, 2, 4, 8)
+    # the CPU port's index (cpu_baseline) is built at the same resolution
+    from oracle import oracle as O
+    assert O.lib().orc_demo_index_res() == navlib.nav_demo_index_res()
     for d_in, d_out, hidden, nh in ((2, 2, 200, 3), (4, 1, 200, 3), (2, 2, 256, 2),
                                     (4, 1, 256, 2), (4, 1, 32, 1)):
         hp = (hidden + 31) // 32 * 32
