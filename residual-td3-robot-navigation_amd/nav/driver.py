@@ -14,7 +14,10 @@ from . import config as K
 
 
 def run(environment_cls=None, robot_cls=None, seed=K.RANDOM_SEED, max_ticks=None,
-        budget=True, test_timeout=K.TEST_TIMEOUT, tick_rate=None, verbose=True, env_kwargs=None):
+        budget=True, test_timeout=K.TEST_TIMEOUT, tick_rate=None, verbose=True, env_kwargs=None,
+        max_episodes=None):
+    """max_episodes: end the run (in training mode) once robot.num_episodes reaches it — the
+    SURVEY §6 config-1 timing ("200 episodes, budget disabled")."""
     if environment_cls is None:
         from .environment import Environment as environment_cls
     if robot_cls is None:
@@ -43,6 +46,8 @@ def run(environment_cls=None, robot_cls=None, seed=K.RANDOM_SEED, max_ticks=None
         t0 = time.time()
         ticks += 1
         if mode == "training":
+            if max_episodes is not None and robot.num_episodes >= max_episodes:
+                break
             money = remaining()
             action_type = robot.get_next_action_type(state, money)
             money = remaining()
@@ -106,7 +111,8 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser(description="headless robot-learning.py on MI355X")
     ap.add_argument("--seed", type=int, default=K.RANDOM_SEED)
     ap.add_argument("--ticks", type=int, default=None)
+    ap.add_argument("--episodes", type=int, default=None)
     ap.add_argument("--no-budget", action="store_true")
     a = ap.parse_args()
-    r = run(seed=a.seed, max_ticks=a.ticks, budget=not a.no_budget)
+    r = run(seed=a.seed, max_ticks=a.ticks, budget=not a.no_budget, max_episodes=a.episodes)
     print({k: v for k, v in r.items() if k not in ("robot", "environment")})

@@ -112,19 +112,26 @@ class TD3(_GpuTD3):
 
     def td3_update(self, replay_buffer):
         """robot.py:258-285: the replay sampling permutations come from np.random exactly as
-        ReplayBuffer.sample draws them (robot.py:111); the smoothing noise from torch.randn."""
+        ReplayBuffer.sample draws them (robot.py:111), one per train_critic and one per
+        train_actor, in epoch order; the smoothing noise from torch.randn(B, 2) per critic epoch.
+        Both generators are independent of the device work, so every epoch's draws are taken up
+        front (the same streams, the same order) and uploaded in one copy; the 100 epochs then
+        run as launches only, with no host round trip between them."""
         B, dev = self.batch_size, self.device
-
-        def idx_fn():
-            if len(replay_buffer) < B:
-                raise TypeError("cannot unpack non-iterable NoneType object")  # robot.py:326
-            s = np.random.choice(len(replay_buffer), B, replace=False)
-            return torch.as_tensor(s, dtype=torch.int64, device=dev)
-
-        def eps_fn():
-            return torch.randn(B, 2).to(dev)
-
-        super().td3_update(replay_buffer, self.num_epochs, idx_fn=idx_fn, eps_fn=eps_fn)
+        if len(replay_buffer) < B:
+            raise TypeError("cannot unpack non-iterable NoneType object")  # robot.py:326
+        L = len(replay_buffer)
+        draws, eps = [], []
+        for epoch in range(self.num_epochs):
+            draws.append(np.random.choice(L, B, replace=False))  # train_critic's sample
+            eps.append(torch.randn(B, 2))                         # train_critic's noise
+            if epoch % self.policy_update_delay == 0:
+                draws.append(np.random.choice(L, B, replace=False))  # train_actor's sample
+        idx = torch.as_tensor(np.stack(draws), dtype=torch.int64).to(dev)
+        noise = torch.stack(eps).to(dev)
+        it_idx, it_eps = iter(idx), iter(noise)
+        super().td3_update(replay_buffer, self.num_epochs, idx_fn=lambda: next(it_idx),
+                           eps_fn=lambda: next(it_eps))
 
 
 class Robot:

@@ -140,9 +140,79 @@ def test_td3_update_dropin_runs(navmods):
     assert st[0].shape == (100, 2) and st[4].dtype == bool
 
 
+def test_td3_update_predrawn_equals_per_epoch_draws(navmods):
+    """The drop-in's td3_update takes every epoch's np.random.choice / torch.randn draws up
+    front; the parameters equal an update that draws them lazily at each train_critic /
+    train_actor call, as robot.py:300-333 / 386-390 do, bit for bit."""
+    from nav.td3 import TD3 as GpuTD3
+    environment, robot = navmods
+    rng = np.random.default_rng(0)
+    rows = [(s, rng.uniform(-5, 5, 2), rng.uniform(-100, 0), s + 1, False)
+            for s in rng.uniform(0, 100, (400, 2))]
+    robots = []
+    for _ in range(2):
+        rb = robot.Robot(np.array([60.0, 40.0]))
+        for r in rows:
+            rb.memory.push(*r)
+        robots.append(rb)
+    a, b = robots
+    for k, net in a.td3_agent.networks().items():  # same initial networks
+        b.td3_agent.networks()[k].params.copy_(net.params)
+        b.td3_agent.networks()[k].pack()
+    np.random.seed(11)
+    torch.manual_seed(12)
+    a.td3_agent.td3_update(a.memory)
+    np.random.seed(11)
+    torch.manual_seed(12)
+    B, mem = 100, b.memory
+
+    def idx_fn():
+        return torch.as_tensor(np.random.choice(len(mem), B, replace=False), dtype=torch.int64,
+                               device="cuda")
+    GpuTD3.td3_update(b.td3_agent, mem, 100, idx_fn=idx_fn,
+                      eps_fn=lambda: torch.randn(B, 2).to("cuda"))
+    torch.cuda.synchronize()
+    for k, net in a.td3_agent.networks().items():
+        assert torch.equal(net.params, b.td3_agent.networks()[k].params), k
+
+
 def test_headless_driver_short_run(navmods):
     from nav import driver
     d = golden("dynamics.npz")
     r = driver.run(seed=5, max_ticks=40, budget=False, verbose=False,
                    env_kwargs={"speed": d["speed"], "angle": d["angle"]})
     assert r["demos"] == 3 and r["steps"] > 0 and r["ticks"] == 40
+
+
+def test_headless_driver_with_learner(navmods):
+    """config 1 in small: the loop through the demos into training episodes, td3_update (100
+    epochs of batch 100, robot.py:258-285) running at every episode end, budget off."""
+    import torch
+    from nav import driver
+    from nav.robot import Robot
+    d = golden("dynamics.npz")
+    updates = []
+
+    class CountingRobot(Robot):
+        def __init__(self, *a, **k):
+            super().__init__(*a, **k)
+            self.init_actor = self.td3_agent.actor_network.params.clone()
+            inner = self.td3_agent.td3_update
+
+            def counted(buf):
+                inner(buf)
+                updates.append(len(buf))
+            self.td3_agent.td3_update = counted
+
+    r = driver.run(robot_cls=CountingRobot, seed=5, budget=False, verbose=False,
+                   max_episodes=8, env_kwargs={"speed": d["speed"], "angle": d["angle"]})
+    robot = r["robot"]
+    assert r["demos"] == 3 and robot.num_episodes == 8 and r["mode"] == "training"
+    assert len(updates) >= 3  # an update at every training episode end
+    # the replay holds the demos' transitions and every training step
+    assert len(robot.memory) == 3 * 199 + r["steps"]
+    assert updates == sorted(updates) and updates[0] >= 3 * 199
+    nets = robot.td3_agent.networks()
+    assert all(torch.isfinite(n.params).all() for n in nets.values())
+    # the actor moved away from its initial parameters
+    assert not torch.equal(robot.init_actor, nets["actor"].params)
