@@ -31,6 +31,8 @@ sys.path.insert(0, os.path.join(HERE, "residual-td3-robot-navigation_amd"))
 
 import torch  # noqa: E402
 
+from nav import prof  # noqa: E402
+
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP32_MFMA_PEAK_TFS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
 FP64_VALU_PEAK_TFS = 78.6    # MI355X spec FP64 vector
@@ -107,34 +109,37 @@ def barrier(ws):
 def step_kernel_sweep(field, sizes, reps=20, K=16):
     """Step-kernel HBM figure: nav_agent_step (fused tick), nav_env_step (pure
     Environment.step) and nav_env_step_k (K Environment.steps per launch, state in registers)
-    alone at growing N, HIP-event timed on the launch stream; per-env-step figures."""
-    from nav import prof
+    alone at growing N; per-env-step figures. Each kernel runs `reps` times back to back between
+    one event pair on the launch stream (avg = span / reps): per-launch event pairs add a fixed
+    ~4-6 us at 65 536 envs, where the kernels themselves run 4-7 us (kernel trace,
+    profiles/r02r_sweep_65536_kernel_trace.txt)."""
     from nav.vec_env import ReplayRing, VecEnv
     out = []
     for n in sizes:
         env = VecEnv(n, field, seed=11, envs_per_group=n, demo_flag=False)
         rep = ReplayRing(n, "cuda")
         act = (torch.rand(n, 2, dtype=torch.float64, device="cuda") - 0.5) * 14
+        acts = (torch.rand(K, n, 2, dtype=torch.float64, device="cuda") - 0.5) * 14
         for _ in range(6):  # fill the 5-deep stuck history: steady-state traffic
             env.agent_step(act, rep)
             env.step(act)
-        acts = (torch.rand(K, n, 2, dtype=torch.float64, device="cuda") - 0.5) * 14
-        t = prof.KernelTimer(["agent_step", "env_step", "env_step_k"])
+        env.step_k(acts)
+        row = {"n_envs": n}
         # each kernel back to back, as a training loop / a pure Environment.step loop runs it
         # (interleaved, env_step paid the write-back of agent_step's dirty lines: PMC r01p)
-        with prof.timing(t):
-            for _ in range(reps):
-                env.agent_step(act, rep)
-            for _ in range(reps):
-                env.step(act)
-            for _ in range(max(1, reps // 4)):
-                env.step_k(acts)
-        s = t.summary()
-        row = {"n_envs": n}
-        for k, bpe, steps in (("agent_step", prof.AGENT_STEP_BYTES, 1),
-                              ("env_step", prof.ENV_STEP_BYTES, 1),
-                              ("env_step_k", prof.env_step_k_bytes(K, False), K)):
-            us = s[k]["avg_us"]
+        for k, bpe, steps, fn, r in (
+                ("agent_step", prof.AGENT_STEP_BYTES, 1, lambda: env.agent_step(act, rep), reps),
+                ("env_step", prof.ENV_STEP_BYTES, 1, lambda: env.step(act), reps),
+                ("env_step_k", prof.env_step_k_bytes(K, False), K, lambda: env.step_k(acts),
+                 max(2, reps // 4))):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            e0.record()
+            for _ in range(r):
+                fn()
+            e1.record()
+            e1.synchronize()
+            us = 1e3 * e0.elapsed_time(e1) / r
             row[k] = {"avg_us": round(us, 2), "env_steps_per_launch": steps,
                       "bytes_per_env_step": bpe,
                       "GBps": round(bpe * n * steps / (us * 1e-6) / 1e9, 1),

@@ -1,9 +1,11 @@
-"""Summarise a rocprofv3 --pmc run's rocpd database (run_results.db): per kernel (short name),
+"""Summarise a rocprofv3 --pmc run (rocpd database run_results.db, or the counter_collection.csv
+of --output-format csv): per kernel (short name),
 dispatch count, mean of each counter per dispatch, and the derived MFMA busy fraction
 SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs * 1024 SIMDs) when both were collected.
 
-python tools/pmc_db.py gpurun_out/<dir>/run_results.db [name-substring ...]
+python tools/pmc_db.py gpurun_out/<dir>/run_results.db|run_counter_collection.csv [substr ...]
 """
+import csv
 import re
 import sqlite3
 import sys
@@ -19,12 +21,18 @@ def short(name):
 
 
 def summarise(path, filt=()):
-    c = sqlite3.connect(path)
     acc = defaultdict(lambda: defaultdict(list))
     dur = defaultdict(dict)
-    for name, counter, value, disp, d in c.execute(
+    if path.endswith(".csv"):
+        with open(path) as f:
+            rows = [(r["Kernel_Name"], r["Counter_Name"], float(r["Counter_Value"]),
+                     r["Dispatch_Id"], int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+                    for r in csv.DictReader(f)]
+    else:
+        rows = sqlite3.connect(path).execute(
             "select kernel_name, counter_name, value, dispatch_id, duration "
-            "from counters_collection"):
+            "from counters_collection")
+    for name, counter, value, disp, d in rows:
         k = short(name)
         if filt and not any(s in k for s in filt):
             continue
