@@ -46,6 +46,17 @@ def test_library_exports_every_declared_symbol(navlib):
     assert set(header_functions()) == bound
 
 
+def test_integration_table_names_the_abi():
+    """INTEGRATION.md's entry-point table names every declared entry point, and no name that
+    the header does not declare (stale docs)."""
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    table = doc[doc.index("Entry points and the reference interface"):doc.index("## 3.")]
+    named = set(re.findall(r"`(nav_\w+)`", table))
+    fns = set(header_functions())
+    assert fns - named == set(), sorted(fns - named)
+    assert named - fns == set(), sorted(named - fns)
+
+
 def test_gfx950_code_object_present(navlib):
     # the offload bundle carries a gfx950 code object (and no other GPU target)
     blob = open(LIB, "rb").read()
