@@ -91,13 +91,21 @@ def parse():
 
 
 def dist_setup(args):
+    """One process per GPU over RCCL ("nccl"). NAV_DIST_REHEARSAL=1 (rehearsal of the N > 1
+    code path on a one-GPU box only): every rank on cuda:0 and gloo collectives, since RCCL refuses
+    two ranks on one device; the timing of such a run means nothing."""
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if ws > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if os.environ.get("NAV_DIST_REHEARSAL") == "1":
+            local = 0
+            torch.cuda.set_device(0)
+            torch.distributed.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
     return ws, rank, local
 
 

@@ -251,6 +251,20 @@ int nav_cem_rollout(const float* field, int32_t n_prob, int32_t P, int32_t T, in
                     float* actions, float* paths, double* reward, void* stream);
 int nav_cem_elite(int32_t n_prob, int32_t P, int32_t T, int32_t E, const double* reward,
                   const float* actions, float* mean, float* stdv, int32_t* best, void* stream);
+/* environment.py:59-95 set_dynamics as nav.fields restates it (perlin_noise is absent: the field
+ * values are parity unpinned against the reference): unit gradient tables g5 [6][6][2],
+ * g10 [11][11][2], g20 [21][21][2] (speed octaves) and ga5 [6][6][2] (angle), f64, from the
+ * host's seeded draws; field out [100][100][2] float32 (speed, angle) x-major, the table every
+ * dynamics kernel reads. Same f32 values as nav.fields.make_fields (speed within 4 ulp: numpy's f32 exp). */
+int nav_fields_generate(const double* g5, const double* g10, const double* g20,
+                        const double* ga5, float* field, void* stream);
+/* Robot.process_demonstration's demonstration set for n_demo demonstrations (robot.py:694-698,
+ * 771-824): per demo its T states [T][2] (f32, the CEM output) followed by n_aug augmentations
+ * of (T-1)*(steps+1) + 1 states each, f64 out [n_demo][T + n_aug*((T-1)(steps+1)+1)][2];
+ * noise [n_demo][n_aug][(T-1)(steps+1)*4 + 4] = each augmentation's np.random.normal draws in the
+ * reference's order. Bit-identical to the numpy restatement nav.demos.demo_set_from. */
+int nav_demo_augment(int32_t n_demo, int32_t T, int32_t steps, int32_t n_aug,
+                     const float* states, const double* noise, double* out, void* stream);
 /* ReplayBuffer.push (robot.py:79-96) of n transitions (f64 in, float32 rows), slots
  * (base + i) % capacity. */
 int nav_replay_push(const nav_replay* replay, int64_t base, int64_t n, const double* state,

@@ -323,6 +323,140 @@ __global__ __launch_bounds__(kBlock) void k_cem_rollout(const float2* __restrict
     reward[i] = -norm2((double)(float)s.x - g.x, (double)(float)s.y - g.y);
 }
 
+// ---------------- dynamics fields (environment.py:59-95 set_dynamics; nav.fields) ----------------
+// nav.fields' construction on the device: per cell (i, j) of the x-major 100 x 100 grid the f64
+// gradient noise of octave o at (i/100*o, j/100*o) from the unit gradient table g_o [o+1][o+1][2]
+// (quintic fade, bilinear blend), speed cells = f32((n5 + .5 n10) + .25 n20), angle cells =
+// f32(n5'), each min-max normalised in f32 and the speed stretched by 1/(1 + exp(-10 (x - .5)))
+// in f32 (the exp rounded from f64) — numpy's operation order, -ffp-contract=off. One 1024-thread workgroup (10 000 cells,
+// block min / max in LDS); field out [100][100][2] (speed, angle) interleaved, the kernels'
+// table layout.
+constexpr int kFieldThreads = 1024;
+NAV_DEV double grad_noise(const double* __restrict__ g, int oct, int i, int j) {
+    const double x = ((double)i / 100.0) * oct, y = ((double)j / 100.0) * oct;
+    const double xf = floor(x), yf = floor(y);
+    const int x0 = (int)xf, y0 = (int)yf;
+    const double fx = x - xf, fy = y - yf;
+    const int w = oct + 1;
+    auto dot = [&](int ix, int iy, double dx, double dy) {
+        const double* v = g + ((int64_t)ix * w + iy) * 2;
+        return v[0] * dx + v[1] * dy;
+    };
+    auto fade = [](double t) { return t * t * t * (t * (t * 6.0 - 15.0) + 10.0); };
+    const double n00 = dot(x0, y0, fx, fy);
+    const double n10 = dot(x0 + 1, y0, fx - 1.0, fy);
+    const double n01 = dot(x0, y0 + 1, fx, fy - 1.0);
+    const double n11 = dot(x0 + 1, y0 + 1, fx - 1.0, fy - 1.0);
+    const double wx = fade(fx), wy = fade(fy);
+    return (n00 * (1.0 - wx) + n10 * wx) * (1.0 - wy) + (n01 * (1.0 - wx) + n11 * wx) * wy;
+}
+
+NAV_DEV void block_minmax(float& mn, float& mx, float* red) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        mn = fminf(mn, __shfl_xor(mn, o, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    }
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) {
+        red[2 * wv] = mn;
+        red[2 * wv + 1] = mx;
+    }
+    __syncthreads();
+    mn = red[0];
+    mx = red[1];
+    for (int w = 1; w < kFieldThreads / 64; ++w) {
+        mn = fminf(mn, red[2 * w]);
+        mx = fmaxf(mx, red[2 * w + 1]);
+    }
+}
+
+__global__ __launch_bounds__(kFieldThreads) void k_fields(const double* __restrict__ g5,
+                                                          const double* __restrict__ g10,
+                                                          const double* __restrict__ g20,
+                                                          const double* __restrict__ ga,
+                                                          float2* __restrict__ field) {
+    constexpr int N = NAV_WORLD_CELLS * NAV_WORLD_CELLS;
+    __shared__ float sp[N];
+    __shared__ float an[N];
+    __shared__ float red[2 * kFieldThreads / 64];
+    float smn = __builtin_inff(), smx = -__builtin_inff(), amn = smn, amx = smx;
+    for (int c = threadIdx.x; c < N; c += kFieldThreads) {
+        const int i = c / NAV_WORLD_CELLS, j = c % NAV_WORLD_CELLS;
+        const double v = (grad_noise(g5, 5, i, j) + 0.5 * grad_noise(g10, 10, i, j)) +
+                         0.25 * grad_noise(g20, 20, i, j);
+        const float fs = (float)v, fa = (float)grad_noise(ga, 5, i, j);
+        sp[c] = fs;
+        an[c] = fa;
+        smn = fminf(smn, fs);
+        smx = fmaxf(smx, fs);
+        amn = fminf(amn, fa);
+        amx = fmaxf(amx, fa);
+    }
+    block_minmax(smn, smx, red);
+    block_minmax(amn, amx, red);
+    const float sr = smx - smn, ar = amx - amn;
+    for (int c = threadIdx.x; c < N; c += kFieldThreads) {
+        const float nrm = (sp[c] - smn) / sr;
+        const float t = -10.0f * (nrm - 0.5f);
+        // numpy's float32 exp is within an ulp of the correctly rounded value; the f64 exp
+        // rounded to f32 is the correctly rounded value but for double-rounding cases
+        const float speed = 1.0f / (1.0f + (float)exp((double)t));
+        field[c] = make_float2(speed, (an[c] - amn) / ar);
+    }
+}
+
+// Robot.process_demonstration's demonstration set (robot.py:694-698) with the augmentation of
+// robot.py:771-824, one output point per thread: demo d's block is its T original states (f64 of
+// the f32 CEM states), then per augmentation k the (T-1)*(steps+1) + 1 augmented states: for
+// transition i and sub-step s < steps the float32 interpolation cur + f32(s+1)/(steps+1)*(nxt-cur)
+// (numpy NEP 50: a python-float fraction times a float32 array stays float32, no fma) plus the
+// state noise, at s = steps the current state plus noise, and finally the last state plus noise.
+// noise [n_demo][n_aug][D], D = (T-1)(steps+1)*4 + 4: the augmentation's normal draws in the
+// reference's order (per (i, s): state 2, action 2; then the last state 2, last action 2).
+__global__ __launch_bounds__(kBlock) void k_demo_augment(int32_t n_demo, int32_t T, int32_t steps,
+                                                         int32_t n_aug,
+                                                         const float2* __restrict__ states,
+                                                         const double* __restrict__ noise,
+                                                         double2* __restrict__ out) {
+    const int64_t per = steps + 1, A = (int64_t)(T - 1) * per + 1, Lp = T + n_aug * A;
+    const int64_t D = (int64_t)(T - 1) * per * 4 + 4;
+    const int64_t idx = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (idx >= (int64_t)n_demo * Lp) return;
+    const int64_t d = idx / Lp;
+    int64_t j = idx % Lp;
+    const float2* st = states + d * T;
+    double2 v;
+    if (j < T) {
+        const float2 q = st[j];
+        v = make_double2((double)q.x, (double)q.y);
+    } else {
+        j -= T;
+        const int64_t k = j / A, r = j % A;
+        const double* g = noise + (d * n_aug + k) * D;
+        if (r == A - 1) {
+            const float2 q = st[T - 1];
+            v = make_double2((double)q.x + g[D - 4], (double)q.y + g[D - 3]);
+        } else {
+            const int64_t i = r / per, sub = r % per;
+            const float2 cur = st[i];
+            double bx = cur.x, by = cur.y;
+            if (sub < steps) {
+                const float2 nxt = st[i + 1];
+                const float f = (float)((double)(sub + 1) / (double)(steps + 1));
+                const float dx = nxt.x - cur.x, dy = nxt.y - cur.y;
+                const float tx = f * dx, ty = f * dy;
+                bx = (double)(cur.x + tx);
+                by = (double)(cur.y + ty);
+            }
+            const double* gn = g + (i * per + sub) * 4;
+            v = make_double2(bx + gn[0], by + gn[1]);
+        }
+    }
+    out[idx] = v;
+}
+
 // environment.py:166-171: the E best paths (np.argsort ascending, last E; ties by path index, a
 // stable order), their float32 action mean and std over the elites in that order (numpy's float32
 // reductions: sequential sums, / E, sqrt); best [n] = argmax of the rewards (first maximum,
@@ -968,6 +1102,29 @@ int nav_cem_elite(int32_t n_prob, int32_t P, int32_t T, int32_t E, const double*
     if (n_prob == 0) return 0;
     hipLaunchKernelGGL(k_cem_elite, dim3(n_prob), dim3(kBlock), 0, S(stream), P, T, E, reward,
                        actions, mean, stdv, best);
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_fields_generate(const double* g5, const double* g10, const double* g20,
+                        const double* ga5, float* field, void* stream) {
+    if (!g5 || !g10 || !g20 || !ga5 || !field) return NAV_EINVAL;
+    hipLaunchKernelGGL(k_fields, dim3(1), dim3(kFieldThreads), 0, S(stream), g5, g10, g20, ga5,
+                       reinterpret_cast<float2*>(field));
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_demo_augment(int32_t n_demo, int32_t T, int32_t steps, int32_t n_aug,
+                     const float* states, const double* noise, double* out, void* stream) {
+    if (n_demo < 0 || T < 2 || steps < 0 || n_aug < 0 || (n_demo && (!states || !out)) ||
+        (n_demo && n_aug && !noise))
+        return NAV_EINVAL;
+    const int64_t n = (int64_t)n_demo * (T + (int64_t)n_aug * ((int64_t)(T - 1) * (steps + 1) + 1));
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_demo_augment, dim3(blocks_for(n)), dim3(kBlock), 0, S(stream), n_demo, T,
+                       steps, n_aug, reinterpret_cast<const float2*>(states), noise,
+                       reinterpret_cast<double2*>(out));
     NAV_CHECK_LAUNCH();
     return 0;
 }

@@ -47,6 +47,9 @@ struct WgradArgs {
 #ifndef NAV_WG_WAVES
 #define NAV_WG_WAVES 8
 #endif
+#ifndef NAV_WG_TOTAL
+#define NAV_WG_TOTAL 256
+#endif
 #ifndef NAV_WG_EXP
 #define NAV_WG_EXP 0  // tuning probes: 1 = operands without VALU math, 2 = without LDS reads
 #endif
@@ -874,8 +877,8 @@ int32_t nav_mlp_wgrad_splits(int32_t n_nets, int32_t hidden_pad, int32_t n_hidde
     if (n_hidden < 2) return 1;
     const int TT = (hidden_pad + WG_TILE - 1) / WG_TILE;
     const int64_t jobs = (int64_t)n_nets * (n_hidden - 1) * TT * TT;
-    // one 8-wave workgroup per CU (256 CUs), at least 512 rows (64 per wave) per split
-    int64_t s = 256 / jobs;
+    // NAV_WG_TOTAL workgroups (256: one 8-wave workgroup per CU), at least 512 rows per split
+    int64_t s = NAV_WG_TOTAL / jobs;
     const int64_t by_rows = (M + 511) / 512;
     if (s > by_rows) s = by_rows;
     return (int32_t)(s < 1 ? 1 : s);

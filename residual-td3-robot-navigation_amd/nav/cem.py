@@ -69,11 +69,32 @@ def batched_demonstrations(field, regions, goals, uniforms, a0, z, device="cuda"
     return paths[ar, idx, :T].contiguous(), acts[ar, idx].contiguous()
 
 
-def cem_group_demo_sets(field, regions, goals, seed, n_demos=K.NUM_DEMO, device="cuda"):
+def device_demo_sets(states, draws, n_demos=K.NUM_DEMO, stream=None,
+                     interpolation_steps=K.AUG_INTERPOLATION):
+    """Group demo sets on the device (nav_demo_augment): states [G*n_demos][T][2] float32 device
+    tensor (CEM output, group-major), draws[g][d] = that demonstration's augmentation draws
+    (augment_draws). Returns (points [sum m_g][2] f64 device tensor, offsets [G+1] int64 numpy);
+    the same values as demo_set_from per group, bit for bit (tests/test_gpu_cem.py)."""
+    n, T = states.shape[0], states.shape[1]
+    G = n // n_demos
+    n_aug = len(draws[0][0])
+    noise = np.stack([np.stack(draws[g][d]) for g in range(G) for d in range(n_demos)])
+    noise_d = torch.as_tensor(noise, dtype=torch.float64).to(states.device)
+    per_demo = T + n_aug * ((T - 1) * (interpolation_steps + 1) + 1)
+    out = torch.empty(n * per_demo, 2, dtype=torch.float64, device=states.device)
+    lib().nav_demo_augment(n, T, interpolation_steps, n_aug, ptr(states.contiguous()),
+                           ptr(noise_d), ptr(out), stream_handle(stream))
+    off = np.arange(G + 1, dtype=np.int64) * n_demos * per_demo
+    return out, off
+
+
+def cem_group_demo_sets(field, regions, goals, seed, n_demos=K.NUM_DEMO, device="cuda",
+                        on_device=True):
     """Per-group demonstration sets (CSR: points [sum m_g][2] f64, offsets [G+1] int64) built the
     way the reference builds one robot's: n_demos CEM demonstrations from the group's start region
     towards its goal, each with its 3 augmentations (robot.py:679-718, 771-824). Group g draws from
-    numpy RandomState((seed + g) mod 2^32)."""
+    numpy RandomState((seed + g) mod 2^32). on_device: the augmentation runs as nav_demo_augment
+    and the points stay on the device; else the numpy restatement (demo_set_from) on the host."""
     G = len(regions)
     per_group = [group_stream_draws(np.random.RandomState((seed + g) & 0xFFFFFFFF), n_demos=n_demos)
                  for g in range(G)]
@@ -83,11 +104,14 @@ def cem_group_demo_sets(field, regions, goals, seed, n_demos=K.NUM_DEMO, device=
     a0 = np.stack([d[1] for grp in per_group for d in grp])
     z = np.stack([d[2] for grp in per_group for d in grp])
     st, ac = batched_demonstrations(field, rg, gl, uni, a0, z, device)
+    draws = [[per_group[g][d][3] for d in range(n_demos)] for g in range(G)]
+    if on_device:
+        return device_demo_sets(st, draws, n_demos)
     st, ac = st.cpu().numpy(), ac.cpu().numpy()
     pts, off = [], [0]
     for g in range(G):
         demos = [(st[g * n_demos + d], ac[g * n_demos + d]) for d in range(n_demos)]
-        dset = demo_set_from(demos, draws=[per_group[g][d][3] for d in range(n_demos)])
+        dset = demo_set_from(demos, draws=draws[g])
         pts.append(dset)
         off.append(off[-1] + len(dset))
     return np.concatenate(pts, 0), np.array(off, np.int64)

@@ -11,10 +11,23 @@ Fields are an input of every kernel; tests inject fixed fields.
 import numpy as np
 
 
-def _gradient_noise(rng, octaves, n=100):
-    """Classic 2-D Perlin gradient noise with `octaves` lattice cells across [0,1)."""
+def _gradient_table(rng, octaves):
+    """the unit lattice gradients [octaves+1][octaves+1][2] of one noise function"""
     g = rng.standard_normal((octaves + 1, octaves + 1, 2))
     g /= np.linalg.norm(g, axis=-1, keepdims=True) + 1e-12
+    return g
+
+
+def gradient_tables(seed):
+    """(g5, g10, g20, ga5): make_fields' gradient tables, drawn in its order."""
+    rng = np.random.default_rng(seed)
+    return tuple(_gradient_table(rng, o) for o in (5, 10, 20, 5))
+
+
+def _gradient_noise(rng, octaves, n=100, g=None):
+    """Classic 2-D Perlin gradient noise with `octaves` lattice cells across [0,1)."""
+    if g is None:
+        g = _gradient_table(rng, octaves)
     u = np.arange(n) / n * octaves
     x, y = np.meshgrid(u, u, indexing="ij")  # [col][row] like environment.py:69-75
     x0, y0 = np.floor(x).astype(int), np.floor(y).astype(int)
@@ -45,3 +58,15 @@ def make_fields(seed):
     mn, mx = np.min(cells), np.max(cells)
     angle = ((cells - mn) / (mx - mn)).astype(np.float32)
     return speed, angle
+
+
+def make_field_device(seed, device="cuda", stream=None):
+    """make_fields on the device (nav_fields_generate): the [100][100][2] (speed, angle) float32
+    table the kernels read, from the same gradient tables (tests/test_gpu_env.py compares)."""
+    import torch
+    from ._lib import lib, ptr, stream_handle
+    g = [torch.as_tensor(np.ascontiguousarray(t), dtype=torch.float64).to(device)
+         for t in gradient_tables(seed)]
+    field = torch.empty(100, 100, 2, dtype=torch.float32, device=device)
+    lib().nav_fields_generate(*[ptr(t) for t in g], ptr(field), stream_handle(stream))
+    return field

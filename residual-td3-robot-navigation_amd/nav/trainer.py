@@ -19,9 +19,9 @@ from . import config as K
 from . import prof
 from ._lib import lib, ptr, stream_handle
 from .cem import cem_group_demo_sets
-from .fields import make_fields
+from .fields import make_field_device
 from .td3 import TD3
-from .vec_env import ReplayRing, VecEnv, make_field
+from .vec_env import ReplayRing, VecEnv
 
 
 class VecTrainer:
@@ -31,9 +31,8 @@ class VecTrainer:
         self.n = int(n_envs)
         self.device = torch.device(device)
         self.seed = int(seed)
-        if field is None:
-            speed, angle = make_fields(self.seed)
-            field = make_field(speed, angle, self.device)
+        if field is None:  # set_dynamics on the device (nav_fields_generate)
+            field = make_field_device(self.seed, self.device)
         self.field = field
         epg = int(envs_per_group) if envs_per_group else self.n
         self.env = VecEnv(self.n, field, seed=self.seed, envs_per_group=epg, demo_flag=demos,

@@ -89,3 +89,20 @@ def test_vec_trainer_uses_cem_demo_sets():
         r = tr.env.region[g * 512].cpu().numpy()
         s0 = pts[off[g]]
         assert r[0] - 1e-4 <= s0[0] <= r[1] + 1e-4 and r[2] - 1e-4 <= s0[1] <= r[3] + 1e-4
+
+
+def test_device_demo_sets_equal_host_augmentation():
+    """nav_demo_augment (the demo sets built on the device) equals the numpy restatement
+    demo_set_from (pinned above against the drop-in's process_demonstration draws) bit for bit."""
+    from nav.cem import cem_group_demo_sets
+    from nav.fields import make_fields
+    from nav.vec_env import make_field
+    speed, angle = make_fields(1707366464)
+    field = make_field(speed, angle, DEV)
+    regions, goals = _groups(5, 31)
+    dev_pts, dev_off = cem_group_demo_sets(field, regions, goals, 99, on_device=True)
+    host_pts, host_off = cem_group_demo_sets(field, regions, goals, 99, on_device=False)
+    assert np.array_equal(dev_off, host_off)
+    got = dev_pts.cpu().numpy()
+    assert got.dtype == host_pts.dtype == np.float64
+    assert np.array_equal(got, host_pts)

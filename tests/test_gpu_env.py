@@ -399,3 +399,18 @@ def test_compute_reward_kernel_vs_oracle(nav, orc):
     for i in range(777):
         r, gr = orc.compute_reward(ns[i], goal[i], t["demo_set"], True)
         assert r == o[i] and gr == bool(hit[i].item())
+
+
+def test_device_field_generator_vs_host(nav):
+    """nav_fields_generate (set_dynamics as nav.fields restates it) vs make_fields on the host:
+    the angle table bit for bit, the speed table within 4 ulp (numpy's SIMD float32 exp is not
+    correctly rounded; the device rounds the f64 exp), over several seeds. Parity against the reference itself is unpinned
+    (perlin_noise is absent)."""
+    from nav.fields import make_field_device, make_fields
+    for seed in (1707366464, 0, 12345):
+        speed, angle = make_fields(seed)
+        f = make_field_device(seed, DEV).cpu().numpy()
+        assert np.array_equal(f[..., 1], angle), seed
+        ulp = np.abs(f[..., 0].view(np.int32).astype(np.int64) - speed.view(np.int32))
+        assert ulp.max() <= 4, (seed, ulp.max())
+        assert (ulp == 0).mean() > 0.5
