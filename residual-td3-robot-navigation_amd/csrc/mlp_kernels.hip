@@ -40,6 +40,9 @@ NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const float* __restr
 #pragma unroll
             for (int i = 0; i < 16; ++i) acc[rt][j][i] = 0.f;
     if (!wc.has0) return;  // wave-uniform (scalar) branch
+#ifdef NAV_AB_SKIP_GEMM
+    return;  // timing experiment only: the non-GEMM part of the row kernels
+#endif
     // A wave without a second tile re-reads its first tile's B (same cache lines) so every load
     // is unconditional; its second-tile MFMAs are skipped by a scalar branch.
     const int t1 = wc.has1 ? wc.t1 : wc.t0;

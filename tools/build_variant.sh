@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build an A/B variant of libnavenv.so with extra -D flags on one translation unit (tuning only):
-#   tools/build_variant.sh NAME learner|env|mlp0 "-DFOO=1 ..."
+#   tools/build_variant.sh NAME learner|env|mlp8 "-DFOO=1 ..."  (mlp8: the hidden-256 row kernels)
 # -> abl/libnavenv_NAME.so (load it with NAV_LIB=abl/libnavenv_NAME.so)
 set -eu
 cd "$(dirname "$0")/.."
@@ -17,6 +17,8 @@ case $unit in
            objs=${objs/$B\/learner_kernels.o/abl\/$name.o} ;;
   env) /opt/rocm/bin/hipcc $FL $flags -c $P/csrc/env_kernels.hip -o abl/$name.o
        objs=${objs/$B\/env_kernels.o/abl\/$name.o} ;;
+  mlp8) /opt/rocm/bin/hipcc $FL $flags -DNAV_MLP_PART=8 -c $P/csrc/mlp_kernels.hip -o abl/$name.o
+        objs=${objs/$B\/mlp_nt8.o/abl\/$name.o} ;;
   *) echo "unit?"; exit 2 ;;
 esac
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o abl/libnavenv_$name.so $objs
