@@ -89,3 +89,64 @@ class VecTrainer:
 
     def env_steps(self):
         return self.steps * self.n
+
+    # ---- checkpoint / resume: every piece of state the next step reads
+    ENV_STATE = ("state", "goal", "region", "hist", "meta", "plan_index", "path_length",
+                 "episodes", "noise_scale")
+
+    def state_dict(self):
+        """The trainer's whole state as host tensors and plain values (torch.save-able, loadable
+        with weights_only=True): per-env SoA state, field, demo set, replay ring, learner (nets,
+        Adam moments, counters) and the step counter that keys the exploration noise. A trainer
+        restored from it continues bit for bit as the original would have."""
+        e = self.env
+        return {
+            "meta": {"n_envs": self.n, "seed": self.seed, "envs_per_group": e.envs_per_group,
+                     "hidden": self.td3.actor_network.hidden,
+                     "n_hidden": self.td3.actor_network.n_hidden,
+                     "batch": self.td3.cfg.batch_size, "updates_per_step": self.updates_per_step,
+                     "steps": self.steps},
+            "env": {k: getattr(e, k).detach().cpu() for k in self.ENV_STATE},
+            "field": self.field.detach().cpu(),
+            "demo_xy": None if e.demo_xy is None else e.demo_xy.cpu(),
+            "demo_off": None if e.demo_off is None else e.demo_off.cpu(),
+            "replay": {"rows": self.replay.rows.cpu(), "position": self.replay.position,
+                       "size": self.replay.size},
+            "td3": self.td3.state_dict(),
+        }
+
+    def load_state_dict(self, sd):
+        m = sd["meta"]
+        assert (m["n_envs"], m["envs_per_group"]) == (self.n, self.env.envs_per_group)
+        assert sd["replay"]["rows"].shape == self.replay.rows.shape
+        for k in self.ENV_STATE:
+            getattr(self.env, k).copy_(sd["env"][k].to(self.device))
+        self.field.copy_(sd["field"].to(self.device))
+        if sd["demo_xy"] is not None:
+            self.env.set_demo(sd["demo_xy"], sd["demo_off"])
+        self.replay.rows.copy_(sd["replay"]["rows"].to(self.device))
+        self.replay.position = int(sd["replay"]["position"])
+        self.replay.size = int(sd["replay"]["size"])
+        self.td3.load_state_dict(sd["td3"])
+        self.steps = int(m["steps"])
+        self.updates_per_step = int(m["updates_per_step"])
+
+    @classmethod
+    def from_state_dict(cls, sd, device="cuda", grad_hook=None):
+        """A trainer resumed from state_dict() without re-running the field generator or the CEM
+        (their results are in the checkpoint)."""
+        m = sd["meta"]
+        t = cls(n_envs=m["n_envs"], hidden=m["hidden"], n_hidden=m["n_hidden"],
+                batch=m["batch"], updates_per_step=m["updates_per_step"],
+                replay_capacity=sd["replay"]["rows"].shape[0], seed=m["seed"],
+                envs_per_group=m["envs_per_group"], demos=False, device=device,
+                field=sd["field"].to(device), grad_hook=grad_hook)
+        t.load_state_dict(sd)
+        return t
+
+    def save(self, path):
+        torch.save(self.state_dict(), path)
+
+    @classmethod
+    def load(cls, path, device="cuda", grad_hook=None):
+        return cls.from_state_dict(torch.load(path, weights_only=True), device, grad_hook)
