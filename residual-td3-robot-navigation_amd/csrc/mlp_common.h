@@ -17,7 +17,7 @@ constexpr int kMaxLayers = 9;
 #ifndef NAV_ACTOR_TOP_REGS
 #define NAV_ACTOR_TOP_REGS 1
 #endif
-// workgroups hold RT row tiles of 32 rows (RT = 2 or 4; NAV_MLP_RT)
+// workgroups hold RT row tiles of 32 rows (RT = 2; RT = 1 for small batches, row_tiles_for)
 
 struct MlpDev {
     const float* params;

@@ -274,7 +274,9 @@ NAV_DEV WoCols load_wo(const MlpDev& net) {
 template <int NT, int RT>
 NAV_DEV void out_partials(const MlpDev& net, const f32x16 (&top)[RT][2], const WoCols& wo,
                           float* red) {
-    constexpr int TM = RT * 32, V = RT * 16, KEEP = V / 32;
+    // RT = 1 (V = 16): four halvings leave lanes l32 and l32 ^ 1 with the two 16-lane halves of
+    // row element l32 >> 1; the fifth exchange adds them and the even lane writes
+    constexpr int TM = RT * 32, V = RT * 16, KEEP = V >= 32 ? V / 32 : 1;
     const int lane = threadIdx.x & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
 #pragma unroll
     for (int jo = 0; jo < 2; ++jo) {
@@ -290,6 +292,10 @@ NAV_DEV void out_partials(const MlpDev& net, const f32x16 (&top)[RT][2], const W
 #pragma unroll
         for (int st = 0; st < 5; ++st) {
             const int m = 16 >> st, n = V >> st;  // compile-time after unrolling
+            if (n < 2) {  // RT = 1, last exchange
+                v[0] += __shfl_xor(v[0], m, 64);
+                continue;
+            }
             // bitwise selects: a ?: over the list would be turned into a dynamic array index
             const uint32_t um = (l32 & m) ? 0xffffffffu : 0u;
 #pragma unroll
@@ -300,10 +306,15 @@ NAV_DEV void out_partials(const MlpDev& net, const f32x16 (&top)[RT][2], const W
                 v[k] = keep + __shfl_xor(send, m, 64);
             }
         }
+        if (V >= 32) {
 #pragma unroll
-        for (int k = 0; k < KEEP; ++k) {
-            const int e = l32 * KEEP + k;
-            red[(jo * kWaves + wv) * TM + c_row(e >> 4, e & 15, h)] = v[k];
+            for (int k = 0; k < KEEP; ++k) {
+                const int e = l32 * KEEP + k;
+                red[(jo * kWaves + wv) * TM + c_row(e >> 4, e & 15, h)] = v[k];
+            }
+        } else if ((l32 & 1) == 0) {
+            const int e = l32 >> 1;
+            red[(jo * kWaves + wv) * TM + c_row(0, e, h)] = v[0];
         }
     }
 }
@@ -550,7 +561,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
                               a.eslab[q] ? a.eslab[q] + (int64_t)blockIdx.x * a.ecount : nullptr);
         return;
     }
-    if (OUT_MODE == OUT_TICK) {
+    if constexpr (OUT_MODE == OUT_TICK) {
         // robot.py:556-567 as OUT_ACT, the action parked in LDS (the input rows are done with),
         // then the tick of env row0 + t by thread t < TM: nav_agent_step's device code
         double* act_lds = reinterpret_cast<double*>(xin);  // [TM][2]
@@ -1081,15 +1092,20 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_actor_rows(ActorRowsArgs a) {
 
 
 // ---- launch helpers (template dispatch on NT = hp / 32 and RT = rows / 32) ----
-// Workgroup height: RT = 4 (128 rows, one workgroup per CU) or RT = 2 (64 rows, two per CU so one
-// workgroup's epilogue overlaps the other's MFMA loop). NAV_MLP_RT overrides (tuning only).
-int row_tiles() {
-    static const int rt = [] {
-        const char* e = getenv("NAV_MLP_RT");
-        const int v = e ? atoi(e) : 2;
-        return (v == 4) ? 4 : 2;
+// Workgroup height: RT = 2 (64 rows, two workgroups per CU so one workgroup's epilogue overlaps
+// the other's MFMA loop; RT = 4, 128 rows and one workgroup per CU, measured slower in round 1:
+// profiles/r01c_micro_rt4.json, no longer built).
+// Small batches take RT = 1 (32-row workgroups): at M <= kSmallRows the 64-row grid leaves CUs
+// idle (config 1's 100 rows: 2 workgroups), and a 32-row block halves each wave's MFMA chain per
+// layer, so the latency-bound small-batch learner runs twice the workgroups at half the chain.
+// Not for the fused tick (its demo pass works on whole waves of envs). NAV_MLP_RT1_MAX overrides
+// the threshold (tuning only; 0 disables).
+int row_tiles_for(int64_t M, bool tick) {
+    static const int64_t small = [] {
+        const char* e = getenv("NAV_MLP_RT1_MAX");
+        return e ? (int64_t)atoll(e) : (int64_t)16384;
     }();
-    return rt;
+    return (!tick && M <= small) ? 1 : 2;
 }
 
 // The row kernels (forward, row backward, critic_rows, actor_rows) are instantiated per NT in
@@ -1158,9 +1174,12 @@ int rows_rt(int fam, int in_mode, int out_mode, const void* args, int n_nets, hi
             const FwdArgs& a = *static_cast<const FwdArgs*>(args);
             if (in_mode == IN_BASELINE && out_mode == OUT_ACT)
                 launch_fwd_k<NT, RT, IN_BASELINE, OUT_ACT>(a, n_nets, st);
-            else if (in_mode == IN_BASELINE && out_mode == OUT_TICK)
-                launch_fwd_k<NT, RT, IN_BASELINE, OUT_TICK>(a, n_nets, st);
-            else if (in_mode == IN_F32 && out_mode == OUT_F32)
+            else if (in_mode == IN_BASELINE && out_mode == OUT_TICK) {
+                if constexpr (RT >= 2)
+                    launch_fwd_k<NT, RT, IN_BASELINE, OUT_TICK>(a, n_nets, st);
+                else
+                    return NAV_EINVAL;
+            } else if (in_mode == IN_F32 && out_mode == OUT_F32)
                 launch_fwd_k<NT, RT, IN_F32, OUT_F32>(a, n_nets, st);
             else if (in_mode == IN_F32 && out_mode == OUT_TARGET)
                 launch_fwd_k<NT, RT, IN_F32, OUT_TARGET>(a, n_nets, st);
@@ -1187,7 +1206,7 @@ int rows_rt(int fam, int in_mode, int out_mode, const void* args, int n_nets, hi
 #define NAV_CAT(a, b) NAV_CAT2(a, b)
 int NAV_CAT(nav_mlp_rows_, NAV_MLP_PART)(int fam, int rt, int in_mode, int out_mode,
                                            const void* args, int n_nets, hipStream_t st) {
-    return rt == 4 ? rows_rt<4>(fam, in_mode, out_mode, args, n_nets, st)
+    return rt == 1 ? rows_rt<1>(fam, in_mode, out_mode, args, n_nets, st)
                    : rows_rt<2>(fam, in_mode, out_mode, args, n_nets, st);
 }
 
@@ -1197,8 +1216,8 @@ namespace {
 
 // hp / 32 -> the per-NT object
 int rows_dispatch(int hp, int fam, int in_mode, int out_mode, const void* args, int n_nets,
-                  hipStream_t st) {
-    const int rt = row_tiles();
+                  int64_t M, hipStream_t st) {
+    const int rt = row_tiles_for(M, fam == FAM_FWD && out_mode == OUT_TICK);
     int r;
     switch (hp / 32) {
         case 1: r = nav_mlp_rows_1(fam, rt, in_mode, out_mode, args, n_nets, st); break;
@@ -1218,16 +1237,16 @@ int rows_dispatch(int hp, int fam, int in_mode, int out_mode, const void* args, 
 
 template <int IN_MODE, int OUT_MODE>
 int launch_fwd(const FwdArgs& a, int n_nets, hipStream_t st) {
-    return rows_dispatch(a.net[0].hp, FAM_FWD, IN_MODE, OUT_MODE, &a, n_nets, st);
+    return rows_dispatch(a.net[0].hp, FAM_FWD, IN_MODE, OUT_MODE, &a, n_nets, a.M, st);
 }
 
 int launch_bwd(const BwdArgs& a, int n_nets, hipStream_t st) {
-    return rows_dispatch(a.net[0].hp, FAM_BWD, 0, 0, &a, n_nets, st);
+    return rows_dispatch(a.net[0].hp, FAM_BWD, 0, 0, &a, n_nets, a.M, st);
 }
 
 #define NAV_ROWS_SWITCH(HP, FAM, ARGS, ST)                                                  \
     {                                                                                       \
-        const int r_ = rows_dispatch((HP), (FAM), 0, 0, &(ARGS), 1, (ST));                   \
+        const int r_ = rows_dispatch((HP), (FAM), 0, 0, &(ARGS), 1, (ARGS).B, (ST));        \
         if (r_) return r_;                                                                  \
     }
 
@@ -1364,7 +1383,7 @@ int nav_mlp_forward(const nav_mlp* nets, int32_t n_nets, int64_t M, const float*
 
 int64_t nav_mlp_row_blocks(int64_t M) {
     if (M < 0) return NAV_EINVAL;
-    const int64_t tm = (int64_t)row_tiles() * 32;
+    const int64_t tm = (int64_t)row_tiles_for(M, false) * 32;
     return (M + tm - 1) / tm;
 }
 

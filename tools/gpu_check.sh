@@ -21,7 +21,6 @@ for step in "$@"; do
     bench) run bench 900 python bench.py ;;
     benchq) run bench 600 python bench.py --steps 10 --warmup 3 --cpu-budget 8 ;;
     micro) run micro 600 python tools/microbench.py ;;
-    micro4) NAV_MLP_RT=4 run micro_rt4 600 python tools/microbench.py ;;
     prof) run prof 900 rocprofv3 --kernel-trace --stats -T -f csv -d gpurun_out/prof -o run -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-sweep ;;
     pmc) run pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE -T -f csv -d gpurun_out/pmc_fetch -o run -- python bench.py --steps 4 --warmup 2 --no-cpu-baseline --no-sweep &&
          run pmc_write 900 rocprofv3 --pmc WRITE_SIZE -T -f csv -d gpurun_out/pmc_write -o run -- python bench.py --steps 4 --warmup 2 --no-cpu-baseline --no-sweep &&
