@@ -116,6 +116,23 @@ NAV_DEV size_t mask_idx(int64_t rowtile, int NT_, int t, int lane) {
 
 constexpr int kWaves = kBlock / 64;
 
+// Phase timing probe (variant builds with -DNAV_PHASE_TRACE only; tools/phase_trace.py): s_memtime
+// at numbered marks, per wave of 4 traced workgroups of the row kernels.
+#ifdef NAV_PHASE_TRACE
+__device__ unsigned long long g_phase_trace[4][kBlock / 64][64];
+#define NAV_MARK(k)                                                                            \
+    do {                                                                                       \
+        const int tw_ = blockIdx.x == 0 ? 0 : blockIdx.x == 1 ? 1 : blockIdx.x == 200 ? 2     \
+                      : blockIdx.x == 511 ? 3 : -1;                                            \
+        if (tw_ >= 0 && (threadIdx.x & 63) == 0 && (k) >= 0 && (k) < 64)                        \
+            g_phase_trace[tw_][threadIdx.x >> 6][(k)] = __builtin_readcyclecounter();          \
+    } while (0)
+#else
+#define NAV_MARK(k) \
+    do {            \
+    } while (0)
+#endif
+
 // Mask image row-tile count: independent of the workgroup height, so any RT reads what any RT
 // wrote (row tile = global row / 32; layers strided by ceil(M/128)*4 tiles).
 __host__ __device__ inline int64_t mask_rowtiles(int64_t M) { return ((M + 127) / 128) * 4; }

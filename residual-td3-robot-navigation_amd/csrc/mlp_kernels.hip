@@ -399,8 +399,9 @@ NAV_DEV void loss_epilogue(const MlpDev& net, const f32x16 (&top)[RT][2], float*
 template <int NT, int RT>
 NAV_DEV void fwd_net(const MlpDev& net, float* act, const float* xin, float* red,
                      uint16_t* masks, int64_t n_rt, float* act_save, uint32_t save_mask,
-                     int64_t row0, int64_t M, int64_t rt0, f32x16 (&top)[RT][2]) {
+                     int64_t row0, int64_t M, int64_t rt0, f32x16 (&top)[RT][2], int mk = -64) {
     constexpr int hp = NT * 32, SS = hp + 4;
+    NAV_MARK(mk);
     const int tid = threadIdx.x, lane = tid & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
     const int d_in = net.d_in, nh = net.n_hidden;
     const WaveCols<NT> wc(wv);
@@ -443,7 +444,9 @@ NAV_DEV void fwd_net(const MlpDev& net, float* act, const float* xin, float* red
             }
         }
     }
+    NAV_MARK(mk + 1);
     __syncthreads();
+    NAV_MARK(mk + 2);
     if (act_save && (save_mask & 1u)) copy_rows<NT, RT>(act, SS, act_save, row0, M);
     // one hidden x hidden layer on MFMA: acc = relu(rows . W_L + b_L), C layout
     auto hidden_layer = [&](int L, f32x16 (&acc)[RT][2]) {
@@ -477,6 +480,7 @@ NAV_DEV void fwd_net(const MlpDev& net, float* act, const float* xin, float* red
     if (nh >= 2) {
         const int L = nh - 1;
         hidden_layer(L, top);
+        NAV_MARK(mk + 3);
         if (act_save && ((save_mask >> L) & 1u)) {
             __syncthreads();
             store_layer<NT, RT>(top, act, SS, mask_of(L), rt0);
@@ -500,7 +504,9 @@ NAV_DEV void fwd_net(const MlpDev& net, float* act, const float* xin, float* red
 
     // ---- output layer (N = d_out <= 2) from the registers; a barrier publishes the partials
     out_partials<NT, RT>(net, top, wo, red);
+    NAV_MARK(mk + 4);
     __syncthreads();
+    NAV_MARK(mk + 5);
 }
 
 template <int NT, int RT, int IN_MODE, int OUT_MODE>
@@ -703,8 +709,10 @@ NAV_DEV void mask_and_store(f32x16 (&acc)[RT][2], const uint32_t (&mbits)[RT][2]
 template <int NT, int RT>
 NAV_DEV void bwd_net(const MlpDev& net, float* act, const float* dys, const float* xin,
                      const uint16_t* masks, int64_t n_rt, float* es, const float* h_top,
-                     float* dz, uint32_t save_mask, int64_t row0, int64_t M, int64_t rt0) {
+                     float* dz, uint32_t save_mask, int64_t row0, int64_t M, int64_t rt0,
+                     int mk = -64) {
     constexpr int hp = NT * 32, SS = hp + 4, TM = RT * 32;
+    NAV_MARK(mk);
     const int tid = threadIdx.x, lane = tid & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
     const int d_in = net.d_in, d_out = net.d_out, nh = net.n_hidden;
     const int64_t MH = M * hp;
@@ -772,6 +780,7 @@ NAV_DEV void bwd_net(const MlpDev& net, float* act, const float* dys, const floa
             }
         }
     }
+    NAV_MARK(mk + 1);
     __syncthreads();
     // per layer: bias gradient db_L = column sums of dz_L (and dW0 at L = 0), then the rows
     // themselves only where the weight-gradient kernel cannot recompute them (save_mask)
@@ -783,6 +792,7 @@ NAV_DEV void bwd_net(const MlpDev& net, float* act, const float* dys, const floa
         if ((save_mask >> L) & 1u) copy_rows<NT, RT>(act, SS, dz + (int64_t)L * MH, row0, M);
     };
     finish_layer(nh - 1);
+    NAV_MARK(mk + 2);
 
     // hidden layers, top-down: dz_{L-1} = (dz_L . W_L) * relu'(act_{L-1}), B = packed Wb_L
     for (int L = nh - 1; L >= 1; --L) {
@@ -791,11 +801,14 @@ NAV_DEV void bwd_net(const MlpDev& net, float* act, const float* dys, const floa
         load_mask_bits<NT, RT>(masks + (size_t)(L - 1) * mstride, rt0, mbits);
         gemm_cols<NT, RT>(act, SS,
                           net.packed + (int64_t)(L - 1) * 2 * hp * hp + (int64_t)hp * hp, acc);
+        NAV_MARK(mk + 3);
         __syncthreads();
         mask_and_store<NT, RT>(acc, mbits, act, SS);
         __syncthreads();
+        NAV_MARK(mk + 4);
         finish_layer(L - 1);
     }
+    NAV_MARK(mk + 5);
 
 }
 
@@ -915,6 +928,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
     float* brow = red + red_floats(TM);  // [TM][8] the sampled replay rows
     float* qv = brow + TM * 8;     // [TM] q1'
     float* dys = qv + TM;          // [TM][4] dL/dq rows of the row backward
+    NAV_MARK(0);
     if (tid < TM) {
         const int64_t b = row0 + tid;
         float4 lo = make_float4(0.f, 0.f, 0.f, 0.f), hi = lo;
@@ -929,9 +943,10 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
         *reinterpret_cast<float4*>(xin + tid * 4) = make_float4(hi.y, hi.z, 0.f, 0.f);  // s'
     }
     __syncthreads();
+    NAV_MARK(1);
     // target actor; a' = clamp(pi'(s') + clamp(policy_noise * eps, +-noise_clip), +-max_action)
     f32x16 top[RT][2];
-    fwd_net<NT, RT>(a.actor_t, act, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0, top);
+    fwd_net<NT, RT>(a.actor_t, act, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0, top, 2);
     if (tid < 2 * TM) {
         const int rloc = tid % TM, j = tid / TM;
         const int64_t r = row0 + rloc;
@@ -954,11 +969,14 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
         xin[rloc * 4 + 2 + j] = v;
     }
     __syncthreads();
+    NAV_MARK(8);
     // twin target critics on (s', a'), then y = r + gamma * min(q1', q2') * (1 - done), kept in
     // the row's thread
-    fwd_net<NT, RT>(a.critic_t[0], act, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0, top);
+    fwd_net<NT, RT>(a.critic_t[0], act, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0, top,
+                    9);
     if (tid < TM) qv[tid] = out_y<RT>(a.critic_t[0], red, tid, 0);
-    fwd_net<NT, RT>(a.critic_t[1], act, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0, top);
+    fwd_net<NT, RT>(a.critic_t[1], act, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0, top,
+                    15);
     float yt = 0.f;
     if (tid < TM) {
         const float q2 = out_y<RT>(a.critic_t[1], red, tid, 0);
@@ -967,24 +985,27 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
         *reinterpret_cast<float4*>(xin + tid * 4) = *reinterpret_cast<const float4*>(brow + tid * 8);
     }
     __syncthreads();
+    NAV_MARK(21);
     // online critics on (s, a)
 #pragma unroll 1
     for (int q = 0; q < 2; ++q) {
         fwd_net<NT, RT>(a.critic[q], act, xin, red, a.masks[q], n_rt, a.acts[q], a.save_mask, row0,
-                        B, rt0, top);
+                        B, rt0, top, 22 + 14 * q);
         float* es = a.eslab[q] ? a.eslab[q] + (int64_t)blockIdx.x * a.ecount : nullptr;
         loss_epilogue<NT, RT>(a.critic[q], top, red, row0, B, yt, a.norm, a.dq[q],
                               a.loss_part[q] + blockIdx.x, es);
         __syncthreads();
+        NAV_MARK(28 + 14 * q);
         if (a.row_backward) {
             if (tid < TM)
                 *reinterpret_cast<float4*>(dys + tid * 4) =
                     make_float4(red[kWaves * TM + tid], 0.f, 0.f, 0.f);  // loss_epilogue's dq
             __syncthreads();
             bwd_net<NT, RT>(a.critic[q], act, dys, xin, a.masks[q], n_rt, es, nullptr, a.dz[q],
-                            a.dz_save_mask, row0, B, rt0);
+                            a.dz_save_mask, row0, B, rt0, 29 + 14 * q);
             __syncthreads();  // the next forward's layer 0 overwrites the rows
         }
+        NAV_MARK(35 + 14 * q);
     }
 }
 
@@ -1209,6 +1230,15 @@ int NAV_CAT(nav_mlp_rows_, NAV_MLP_PART)(int fam, int rt, int in_mode, int out_m
     return rt == 1 ? rows_rt<1>(fam, in_mode, out_mode, args, n_nets, st)
                    : rows_rt<2>(fam, in_mode, out_mode, args, n_nets, st);
 }
+
+#if defined(NAV_PHASE_TRACE) && NAV_MLP_PART == 8
+extern "C" int nav_phase_trace_read(unsigned long long* host, int n) {
+    const size_t bytes = sizeof(g_phase_trace);
+    if (!host || (size_t)n * sizeof(unsigned long long) < bytes) return NAV_EINVAL;
+    const hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(g_phase_trace), bytes);
+    return e == hipSuccess ? 0 : -(int)e;
+}
+#endif
 
 #else  // NAV_MLP_PART == 0
 

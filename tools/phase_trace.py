@@ -1,0 +1,70 @@
+"""Phase timing of k_td3_critic_rows at the bench shape (tuning probe, not a test).
+
+Needs a library built with -DNAV_PHASE_TRACE (tools/build_variant.sh trace mlp8 -DNAV_PHASE_TRACE)
+loaded through NAV_LIB. Runs the bench trainer for a few steps, then reads the s_memtime marks of
+4 traced workgroups (blocks 0, 1, 200, 511) x 4 waves and prints each phase's duration in
+cycles of that counter, per wave, plus the per-phase mean over the 16 traced waves.
+
+NAV_LIB=abl/libnavenv_trace.so python tools/phase_trace.py
+"""
+import ctypes as C
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, ".."))
+sys.path.insert(0, os.path.join(HERE, "..", "residual-td3-robot-navigation_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+# mark -> name (k_td3_critic_rows; fwd_net / bwd_net marks are base + 0..5)
+FWD = ["start", "layer0", "barrier", "gemm", "out_partials", "barrier"]
+BWD = ["start", "top_unit", "barrier+edges", "gemm", "mask+store", "edges0"]
+
+
+def mark_names():
+    n = {0: "kernel start", 1: "sample + barrier"}
+    for base, tag in ((2, "actor_t"), (9, "critic_t1"), (15, "critic_t2"), (22, "critic1"),
+                      (36, "critic2")):
+        for i, s in enumerate(FWD):
+            n[base + i] = f"{tag} fwd {s}"
+    n[8] = "target noise + barrier"
+    n[21] = "TD target + barrier"
+    for q in range(2):
+        n[28 + 14 * q] = f"critic{q + 1} loss epilogue"
+        for i, s in enumerate(BWD):
+            n[29 + 14 * q + i] = f"critic{q + 1} bwd {s}"
+        n[35 + 14 * q] = f"critic{q + 1} done"
+    return n
+
+
+def main():
+    from nav._lib import LIB_PATH
+    from nav.trainer import VecTrainer
+    tr = VecTrainer(n_envs=65536, hidden=256, n_hidden=2, batch=32768, updates_per_step=2,
+                    envs_per_group=1024)
+    for _ in range(4):
+        tr.step()
+    torch.cuda.synchronize()
+    raw = C.CDLL(LIB_PATH)
+    buf = (C.c_ulonglong * (4 * 4 * 64))()
+    rc = raw.nav_phase_trace_read(buf, 4 * 4 * 64)
+    assert rc == 0, rc
+    t = np.frombuffer(buf, dtype=np.uint64).reshape(4, 4, 64).astype(np.int64)
+    names = mark_names()
+    marks = sorted(names)
+    out = {"marks": {}, "total": {}}
+    for wg in range(4):
+        for w in range(4):
+            out["total"][f"wg{wg}w{w}"] = int(t[wg, w, marks[-1]] - t[wg, w, 0])
+    for a, b in zip(marks[:-1], marks[1:]):
+        d = t[:, :, b] - t[:, :, a]
+        out["marks"][f"{b:02d} {names[b]}"] = {"mean": float(d.mean()), "min": int(d.min()),
+                                               "max": int(d.max())}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
