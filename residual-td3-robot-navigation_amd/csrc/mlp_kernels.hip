@@ -249,7 +249,41 @@ NAV_DEV void store_mask(const f32x16 (&acc)[RT][2], uint16_t* mask, int64_t rt0)
 // transpose-reduce across the 32 lanes of each lane half (5 xor exchanges that each halve the
 // list a lane carries: 31 exchanges for RT = 2) sums the columns of the wave; the 4 waves'
 // partials meet in LDS (red [d_out][4][TM]) and out_y adds them in wave order. No LDS copy of the
-// top layer, no barrier between the last GEMM and the output layer.
+// top layer, no barrier between the last GEMM and the output layer. The exchanges run in lane-
+// mask order 1, 2, 4, 8, 16, so the big early stages are DPP moves inside a 16-lane row (xor 1 /
+// 2: quad_perm, xor 4: half-row mirror then quad_perm, xor 8: row rotate by 8) and only the last,
+// single-element one crosses rows (ds_bpermute).
+template <int M_>
+NAV_DEV float lane_xor(float v) {
+    const int x = __float_as_int(v);
+    if constexpr (M_ == 1) {
+        return __int_as_float(__builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false));  // [1,0,3,2]
+    } else if constexpr (M_ == 2) {
+        return __int_as_float(__builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, false));  // [2,3,0,1]
+    } else if constexpr (M_ == 4) {
+        const int m7 = __builtin_amdgcn_mov_dpp(x, 0x141, 0xF, 0xF, false);  // l ^ 7
+        return __int_as_float(__builtin_amdgcn_mov_dpp(m7, 0x1B, 0xF, 0xF, false));  // ^ 3
+    } else if constexpr (M_ == 8) {
+        return __int_as_float(__builtin_amdgcn_mov_dpp(x, 0x128, 0xF, 0xF, false));  // ror 8
+    } else {
+        return __shfl_xor(v, M_, 64);
+    }
+}
+
+// one halving stage of the transpose-reduce: lanes with bit M_ set keep the upper half of the
+// list (n entries) and send the lower half to lane ^ M_
+template <int M_, int N_>
+NAV_DEV void halve(float* v, int l32) {
+    const uint32_t um = (l32 & M_) ? 0xffffffffu : 0u;
+    // bitwise selects: a ?: over the list would be turned into a dynamic array index
+#pragma unroll
+    for (int k = 0; k < N_ / 2; ++k) {
+        const uint32_t lo = __float_as_uint(v[k]), hi = __float_as_uint(v[k + N_ / 2]);
+        const float send = __uint_as_float((lo & um) | (hi & ~um));
+        const float keep = __uint_as_float((hi & um) | (lo & ~um));
+        v[k] = keep + lane_xor<M_>(send);
+    }
+}
 // Wo entries of the lane's columns (0 for absent tiles): wo[output][tile]
 struct WoCols {
     float w[2][2];
@@ -274,9 +308,11 @@ NAV_DEV WoCols load_wo(const MlpDev& net) {
 template <int NT, int RT>
 NAV_DEV void out_partials(const MlpDev& net, const f32x16 (&top)[RT][2], const WoCols& wo,
                           float* red) {
-    // RT = 1 (V = 16): four halvings leave lanes l32 and l32 ^ 1 with the two 16-lane halves of
-    // row element l32 >> 1; the fifth exchange adds them and the even lane writes
-    constexpr int TM = RT * 32, V = RT * 16, KEEP = V >= 32 ? V / 32 : 1;
+    // RT = 2 (V = 32): after the 5 halvings lane l32 holds list element bitrev5(l32). RT = 1
+    // (V = 16): four halvings leave lanes l32 and l32 ^ 16 with the two halves of element
+    // bitrev4(l32 & 15); the fifth exchange adds them and the lane with bit 4 clear writes
+    static_assert(RT == 1 || RT == 2, "row tiles per workgroup");
+    constexpr int TM = RT * 32, V = RT * 16;
     const int lane = threadIdx.x & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
 #pragma unroll
     for (int jo = 0; jo < 2; ++jo) {
@@ -289,32 +325,20 @@ NAV_DEV void out_partials(const MlpDev& net, const f32x16 (&top)[RT][2], const W
             for (int i = 0; i < 16; ++i) v[rt * 16 + i] = fmaf(top[rt][1][i], w1, top[rt][0][i] * w0);
         // lane bit b (mask 16 .. 1) picks which half of the list the lane keeps: the survivor k
         // of lane l32 is list element (l32 * KEEP + k)
-#pragma unroll
-        for (int st = 0; st < 5; ++st) {
-            const int m = 16 >> st, n = V >> st;  // compile-time after unrolling
-            if (n < 2) {  // RT = 1, last exchange
-                v[0] += __shfl_xor(v[0], m, 64);
-                continue;
+        halve<1, V>(v, l32);
+        halve<2, V / 2>(v, l32);
+        halve<4, V / 4>(v, l32);
+        halve<8, V / 8>(v, l32);
+        if constexpr (V >= 32) {
+            halve<16, V / 16>(v, l32);
+            const int e = (int)(__builtin_bitreverse32((uint32_t)l32) >> 27);
+            red[(jo * kWaves + wv) * TM + c_row(e >> 4, e & 15, h)] = v[0];
+        } else {
+            v[0] += lane_xor<16>(v[0]);
+            if ((l32 & 16) == 0) {
+                const int e = (int)(__builtin_bitreverse32((uint32_t)l32) >> 28);
+                red[(jo * kWaves + wv) * TM + c_row(0, e, h)] = v[0];
             }
-            // bitwise selects: a ?: over the list would be turned into a dynamic array index
-            const uint32_t um = (l32 & m) ? 0xffffffffu : 0u;
-#pragma unroll
-            for (int k = 0; k < n / 2; ++k) {
-                const uint32_t lo = __float_as_uint(v[k]), hi = __float_as_uint(v[k + n / 2]);
-                const float send = __uint_as_float((lo & um) | (hi & ~um));
-                const float keep = __uint_as_float((hi & um) | (lo & ~um));
-                v[k] = keep + __shfl_xor(send, m, 64);
-            }
-        }
-        if (V >= 32) {
-#pragma unroll
-            for (int k = 0; k < KEEP; ++k) {
-                const int e = l32 * KEEP + k;
-                red[(jo * kWaves + wv) * TM + c_row(e >> 4, e & 15, h)] = v[k];
-            }
-        } else if ((l32 & 1) == 0) {
-            const int e = l32 >> 1;
-            red[(jo * kWaves + wv) * TM + c_row(0, e, h)] = v[0];
         }
     }
 }
@@ -408,37 +432,42 @@ NAV_DEV void fwd_net(const MlpDev& net, float* act, const float* xin, float* red
     (void)tid;
     // the output layer's Wo columns: issued now, in flight under layer 0 and the GEMMs
     const WoCols wo = load_wo<NT>(net);
-    // ---- layer 0 (K = d_in) on the VALU, written in the C layout of the wave's column tiles
+    // ---- layer 0 (K = d_in <= 4) on MFMA, straight into the C layout of the wave's column
+    // tiles: the bias tile by a K = 2 product of (1, 0) x (b, 0) (exactly b), then x[:, 0:2] and
+    // x[:, 2:4] against W0's columns: each element is fma(x3, w3, fma(x2, w2, fma(x1, w1,
+    // fma(x0, w0, b)))) — layer0_unit's chain, bit for bit (absent inputs and weights are 0)
     {
         const float* W0 = net.params + net.w_off[0];
         const float* b0 = net.params + net.b_off[0];
+        const f32x16 zero = {};
+        const float one = h == 0 ? 1.f : 0.f;
+        // A operands: row l32 of each row tile, inputs h and 2 + h
+        float xa[RT], xb[RT];
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+            const float4 xr = *reinterpret_cast<const float4*>(xin + (rt * 32 + l32) * 4);
+            xa[rt] = h ? xr.y : xr.x;
+            xb[rt] = h ? xr.w : xr.z;
+        }
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             if (!(j == 0 ? wc.has0 : wc.has1)) continue;
             const int t = j == 0 ? wc.t0 : wc.t1;
             const int c = t * 32 + l32;
-            float w[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (k < d_in) w[k] = W0[c * d_in + k];
-            const float b = b0[c];
+            const float wa = h < d_in ? W0[c * d_in + h] : 0.f;
+            const float wb = 2 + h < d_in ? W0[c * d_in + 2 + h] : 0.f;
+            const f32x16 bias = mfma(one, h == 0 ? b0[c] : 0.f, zero);
             float* col = act + c + 4 * h * SS;
-            const float* xr = xin + 4 * h * 4;
-#pragma unroll 1
-            for (int rt = 0; rt < RT; ++rt) {
-                uint32_t bits = 0;
-                // all 16 input rows first: the LDS stores below may alias them for the compiler,
-                // which would otherwise wait on every read
-                float4 xs[16];
 #pragma unroll
-                for (int i = 0; i < 16; ++i)
-                    xs[i] = *reinterpret_cast<const float4*>(xr + (rt * 32 + (i & 3) + 8 * (i >> 2)) * 4);
+            for (int rt = 0; rt < RT; ++rt) {
+                f32x16 v = mfma(xa[rt], wa, bias);
+                v = mfma(xb[rt], wb, v);
+                uint32_t bits = 0;
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
-                    const int ro = rt * 32 + (i & 3) + 8 * (i >> 2);
-                    const float v = layer0_unit(xs[i], w[0], w[1], w[2], w[3], b);
-                    col[ro * SS] = v;
-                    bits |= (v > 0.f ? 1u : 0u) << i;
+                    const float r = fmaxf(v[i], 0.f);
+                    col[(rt * 32 + (i & 3) + 8 * (i >> 2)) * SS] = r;
+                    bits |= (r > 0.f ? 1u : 0u) << i;
                 }
                 if (masks) masks[mask_idx(rt0 + rt, NT, t, lane)] = (uint16_t)bits;
             }
@@ -681,6 +710,62 @@ NAV_DEV void load_mask_bits(const uint16_t* mask, int64_t rt0, uint32_t (&bits)[
     }
 }
 
+// Edge partials of one hidden layer's dz from the C-layout registers: db[c] = column sum over the
+// block's rows (each lane sums its 16 * RT rows in (row tile, element) order, then the two lane
+// halves meet: rows +0 / +4), and for layer 0 also dW0[c][k] = sum_rows dz[row][c] x[row][k]
+// (x rows from xin [TM][4], one broadcast read per row shared by both column tiles).
+template <int NT, int RT>
+NAV_DEV void edge_regs(const MlpDev& net, const f32x16 (&z)[RT][2], const float* xin, int L,
+                       float* es) {
+    const int lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
+    const WaveCols<NT> wc(wave_id());
+    const int d_in = net.d_in;
+    float sb[2] = {0.f, 0.f}, sw[2][4] = {};
+    if (L == 0) {
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const float4 x = *reinterpret_cast<const float4*>(xin + c_row(rt, i, h) * 4);
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const float v = z[rt][j][i];
+                    sb[j] += v;
+                    sw[j][0] = fmaf(v, x.x, sw[j][0]);
+                    sw[j][1] = fmaf(v, x.y, sw[j][1]);
+                    sw[j][2] = fmaf(v, x.z, sw[j][2]);
+                    sw[j][3] = fmaf(v, x.w, sw[j][3]);
+                }
+            }
+    } else {
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) sb[j] += z[rt][j][i];
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        sb[j] += __shfl_xor(sb[j], 32, 64);
+        if (L == 0)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) sw[j][k] += __shfl_xor(sw[j][k], 32, 64);
+    }
+    if (h != 0) return;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        if (!(j == 0 ? wc.has0 : wc.has1)) continue;
+        const int c = (j == 0 ? wc.t0 : wc.t1) * 32 + l32;
+        es[e_b(net, L) + c] = sb[j];
+        if (L == 0)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (k < d_in) es[net.w_off[0] + c * d_in + k] = sw[j][k];
+    }
+}
+
+// Masks the layer's dz registers in place (ReLU derivative bits) and stores them to the LDS rows.
 template <int NT, int RT>
 NAV_DEV void mask_and_store(f32x16 (&acc)[RT][2], const uint32_t (&mbits)[RT][2], float* act,
                             int S_) {
@@ -688,16 +773,23 @@ NAV_DEV void mask_and_store(f32x16 (&acc)[RT][2], const uint32_t (&mbits)[RT][2]
     const WaveCols<NT> wc(wv);
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-        if (!(j == 0 ? wc.has0 : wc.has1)) continue;
+        if (!(j == 0 ? wc.has0 : wc.has1)) {
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) acc[rt][j][i] = 0.f;
+            continue;
+        }
         const int t = j == 0 ? wc.t0 : wc.t1;
         float* col = act + t * 32 + l32 + 4 * h * S_;
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) {
             const uint32_t bits = mbits[rt][j];
 #pragma unroll
-            for (int i = 0; i < 16; ++i)
-                col[(rt * 32 + (i & 3) + 8 * (i >> 2)) * S_] =
-                    (bits >> i) & 1u ? acc[rt][j][i] : 0.f;
+            for (int i = 0; i < 16; ++i) {
+                acc[rt][j][i] = (bits >> i) & 1u ? acc[rt][j][i] : 0.f;
+                col[(rt * 32 + (i & 3) + 8 * (i >> 2)) * S_] = acc[rt][j][i];
+            }
         }
     }
 }
@@ -750,44 +842,42 @@ NAV_DEV void bwd_net(const MlpDev& net, float* act, const float* dys, const floa
         }
     }
 
-    // top hidden layer: dz = (dy . Wo) * relu'(.), in the C layout
+    // top hidden layer: dz = (dy . Wo) * relu'(.), in the C layout: one K = 2 MFMA per tile of
+    // dy rows (lane l32 = row, h = output) against Wo's columns, fma(dy1, w1, dy0 w0) — the
+    // chain the weight-gradient kernel recomputes — then the forward's ReLU bits
     {
         const float* Wo = net.params + net.w_off[nh];
         const uint16_t* mk = masks + (size_t)(nh - 1) * mstride;
+        const f32x16 zero = {};
+        float ga[RT];
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+            const float4 g = *reinterpret_cast<const float4*>(dys + (rt * 32 + l32) * 4);
+            ga[rt] = h < d_out ? (h ? g.y : g.x) : 0.f;
+        }
+        uint32_t mb[RT][2];
+        load_mask_bits<NT, RT>(mk, rt0, mb);
+        f32x16 z[RT][2];
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-            if (!(j == 0 ? wc.has0 : wc.has1)) continue;
-            const int t = j == 0 ? wc.t0 : wc.t1;
-            const int c = t * 32 + l32;
-            const float w0 = Wo[c];
-            const float w1 = d_out > 1 ? Wo[hp + c] : 0.f;
-            float* col = act + c + 4 * h * SS;
-            const float* gr = dys + 4 * h * 4;
-#pragma unroll 1
-            for (int rt = 0; rt < RT; ++rt) {
-                const uint32_t bits = mk[mask_idx(rt0 + rt, NT, t, lane)];
-                float4 gs[16];
+            const bool has = j == 0 ? wc.has0 : wc.has1;
+            const int c = (j == 0 ? wc.t0 : has ? wc.t1 : wc.t0) * 32 + l32;
+            const float wb = has && h < d_out ? Wo[h * hp + c] : 0.f;
 #pragma unroll
-                for (int i = 0; i < 16; ++i)
-                    gs[i] = *reinterpret_cast<const float4*>(gr + (rt * 32 + (i & 3) + 8 * (i >> 2)) * 4);
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const int ro = rt * 32 + (i & 3) + 8 * (i >> 2);
-                    const float4 g = gs[i];
-                    const float v = top_unit(g.x, g.y, w0, w1);
-                    col[ro * SS] = (bits >> i) & 1u ? v : 0.f;
-                }
-            }
+            for (int rt = 0; rt < RT; ++rt) z[rt][j] = mfma(ga[rt], wb, zero);
         }
+        mask_and_store<NT, RT>(z, mb, act, SS);
+        if (es && nh > 1) edge_regs<NT, RT>(net, z, xin, nh - 1, es);
     }
     NAV_MARK(mk + 1);
     __syncthreads();
-    // per layer: bias gradient db_L = column sums of dz_L (and dW0 at L = 0), then the rows
-    // themselves only where the weight-gradient kernel cannot recompute them (save_mask)
+    // per layer: the rows themselves only where the weight-gradient kernel cannot recompute them
+    // (save_mask); the edge partials come from the registers (edge_regs), except for a one-layer
+    // network's layer 0 written by the top unit above (LDS column sums)
     auto finish_layer = [&](int L) {
-        if (es) {
+        if (es && nh == 1) {
             edge_col_sums<TM>(act, SS, hp, es + e_b(net, L));
-            if (L == 0) edge_w0<TM>(act, SS, hp, xin, d_in, es + net.w_off[0]);
+            edge_w0<TM>(act, SS, hp, xin, d_in, es + net.w_off[0]);
         }
         if ((save_mask >> L) & 1u) copy_rows<NT, RT>(act, SS, dz + (int64_t)L * MH, row0, M);
     };
@@ -804,6 +894,7 @@ NAV_DEV void bwd_net(const MlpDev& net, float* act, const float* dys, const floa
         NAV_MARK(mk + 3);
         __syncthreads();
         mask_and_store<NT, RT>(acc, mbits, act, SS);
+        if (es) edge_regs<NT, RT>(net, acc, xin, L - 1, es);
         __syncthreads();
         NAV_MARK(mk + 4);
         finish_layer(L - 1);
