@@ -408,11 +408,10 @@ NAV_DEV void loss_epilogue(const MlpDev& net, const f32x16 (&top)[RT][2], float*
     }
     if (!es) return;
     wo_grad_regs<NT, RT>(net, top, dqs, 1, es);
-    if (tid < 4) {  // bo and its 3 padding floats
-        float sum = 0.f;
-        if (tid == 0)
-            for (int rr = 0; rr < TM; ++rr) sum += dqs[rr];
-        es[e_bo(net) + tid] = sum;
+    // bo = sum of dq over the block's rows (all in wave 0: TM <= 64), and its 3 padding floats
+    if (tid < 64) {
+        const float sb = wave_sum(dqv);
+        if (tid < 4) es[e_bo(net) + tid] = tid == 0 ? sb : 0.f;
     }
 }
 
@@ -1020,6 +1019,22 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
     float* qv = brow + TM * 8;     // [TM] q1'
     float* dys = qv + TM;          // [TM][4] dL/dq rows of the row backward
     NAV_MARK(0);
+    // target policy smoothing noise of (row, output) tid % TM, tid / TM: clamp(policy_noise * eps,
+    // +-noise_clip), formed while the sampled rows are in flight
+    float tnz = 0.f;
+    if (tid < 2 * TM && row0 + tid % TM < B) {
+        const int64_t r = row0 + tid % TM;
+        const int j = tid / TM;
+        float e;
+        if (a.eps) {
+            e = a.eps[r * 2 + j];
+        } else {
+            const double2 z = gauss_pair(philox((uint32_t)r, 0u, NAV_TAG_TNOISE, a.noise_ctr,
+                                                a.seed_lo, a.seed_hi));
+            e = (float)(j == 0 ? z.x : z.y);
+        }
+        tnz = fminf(fmaxf(e * a.policy_noise, -a.noise_clip), a.noise_clip);
+    }
     if (tid < TM) {
         const int64_t b = row0 + tid;
         float4 lo = make_float4(0.f, 0.f, 0.f, 0.f), hi = lo;
@@ -1044,17 +1059,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
         float v = 0.f;
         if (r < B) {
             const float y = out_y<RT>(a.actor_t, red, rloc, j);
-            float e;
-            if (a.eps) {
-                e = a.eps[r * 2 + j];
-            } else {
-                const double2 z = gauss_pair(philox((uint32_t)r, 0u, NAV_TAG_TNOISE, a.noise_ctr,
-                                                    a.seed_lo, a.seed_hi));
-                e = (float)(j == 0 ? z.x : z.y);
-            }
-            float nz = e * a.policy_noise;
-            nz = fminf(fmaxf(nz, -a.noise_clip), a.noise_clip);
-            v = y + nz;
+            v = y + tnz;
             v = fminf(fmaxf(v, -a.max_action), a.max_action);
         }
         xin[rloc * 4 + 2 + j] = v;
