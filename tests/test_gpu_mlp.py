@@ -63,6 +63,39 @@ def test_forward_vs_torch(nav, d_in, d_out, hidden, nh, M):
         assert (a[:, hidden:] == 0).all()
 
 
+@pytest.mark.parametrize("d_in,d_out,hidden,nh", [(4, 1, 256, 2), (2, 2, 200, 3), (4, 1, 64, 1)])
+def test_forward_row_block_heights_bitwise(nav, d_in, d_out, hidden, nh):
+    """Batches <= 16 384 rows run 32-row blocks (RT = 1), larger ones 64-row blocks (RT = 2). The
+    forward is the same K-ordered chain and the same output-layer lane tree either way: the first
+    16 384 rows of a 16 421-row forward equal a 16 384-row forward bit for bit (outputs, saved
+    activations and ReLU bits), and both match torch."""
+    from nav.mlp import forward
+    net, layers = make_net(d_in, d_out, hidden, nh, 9)
+    M1, M2 = 16384, 16421
+    x = (torch.randn(M2, d_in) * 20).to(DEV).contiguous()
+    res = []
+    for M in (M1, M2):
+        out = torch.zeros(M, d_out, device=DEV)
+        acts = torch.zeros(nh, M, net.hp, device=DEV)
+        masks = net.mask_buffer(M)
+        forward([net], x[:M].contiguous(), d_in, 0, [out], d_out, 0, M, acts=[acts],
+                masks=[masks])
+        res.append((out, acts, masks))
+    torch.cuda.synchronize()
+    assert torch.equal(res[0][0], res[1][0][:M1])
+    assert torch.equal(res[0][1], res[1][1][:, :M1])
+    ref = torch_mlp(layers, x.cpu())
+    scale = ref.abs().max().item() + 1
+    assert torch.allclose(res[1][0].cpu(), ref, rtol=1e-4, atol=1e-5 * scale)
+    # ReLU bit images: row tile = row / 32 in both; compare every tile of the first 16 384 rows
+    from nav._lib import lib
+    nt = net.hp // 32
+    m1 = res[0][2].view(nh, -1, nt, 64)[:, :M1 // 32]
+    m2 = res[1][2].view(nh, -1, nt, 64)[:, :M1 // 32]
+    assert torch.equal(m1, m2)
+    assert lib().nav_mlp_row_blocks(M1) == M1 // 32 and lib().nav_mlp_row_blocks(M2) == (M2 + 63) // 64
+
+
 def test_twin_forward_and_target_smoothing(nav):
     from nav.mlp import forward
     c1, L1 = make_net(4, 1, 200, 3, 7)
@@ -131,9 +164,26 @@ def _grad_flat_vs_autograd(net, tl, gflat, d_in, d_out, nh):
         assert (gflat[b_off + o:b_off + fo] == 0).all()
 
 
+def relu_bits(masks, nh, hp, hidden, M):
+    """The forward's ReLU bit image ([nh][M / 32 row tiles][hp / 32][64 lanes] u16 words, C
+    layout: bit i of lane (l32, h) = row (i & 3) + 8 (i >> 2) + 4 h of the tile, column l32) as
+    [nh][M][hidden] booleans."""
+    nt = hp // 32
+    w = masks.cpu().to(torch.int32) & 0xFFFF
+    n_rt = w.numel() // (nh * nt * 64)
+    bits = ((w.view(nh, n_rt, nt, 2, 32, 1) >> torch.arange(16)) & 1).bool()
+    r = torch.arange(32)
+    hh, ii = (r >> 2) & 1, (r & 3) + 4 * (r >> 3)  # lane half and element of tile row r
+    b = bits.permute(0, 1, 3, 5, 2, 4)[:, :, hh, ii]  # [nh][n_rt][32 rows][nt][32 cols]
+    return b.reshape(nh, n_rt * 32, nt * 32)[:, :M, :hidden]
+
+
 @pytest.mark.parametrize("d_in,d_out,hidden,nh,M", [(4, 1, 200, 3, 100), (2, 2, 200, 3, 777),
                                                     (4, 1, 256, 2, 5000), (2, 2, 256, 2, 4096),
-                                                    (4, 1, 64, 1, 300), (2, 2, 96, 4, 333)])
+                                                    (4, 1, 64, 1, 300), (2, 2, 96, 4, 333),
+                                                    # 64-row blocks (RT = 2, > 16 384 rows)
+                                                    (4, 1, 256, 2, 16421), (2, 2, 200, 3, 16421),
+                                                    (4, 1, 64, 1, 16421)])
 def test_backward_and_weight_grads_vs_autograd(nav, d_in, d_out, hidden, nh, M):
     """Row backward + per-block edge partials + recomputing hidden weight gradients + reduce
     against torch autograd; every gradient entry must be written (NaN-filled buffers)."""
@@ -169,11 +219,27 @@ def test_backward_and_weight_grads_vs_autograd(nav, d_in, d_out, hidden, nh, M):
     L.nav_mlp_wgrad(descs(net), 1, M, ptr(xd), d_in, 0, parr(acts), parr(dz), parr(dyd), d_out,
                     parr(masks), parr(hs), splits, s)
     L.nav_grad_reduce(C.byref(net.desc()), ptr(hs), splits, ptr(eslab), nblk, ptr(grad), s)
-    # torch autograd reference
+    # torch autograd reference with the kernel's own ReLU decisions: a pre-activation within the
+    # summation-order error bound of 0 (|z| <= K eps32 sum|w h|) may take the other branch in
+    # torch's order and move a whole unit's term (at 16 421 rows one does: tools/dx_diag.py,
+    # profiles/r02ag_dx_diag.log), so the reference multiplies by the forward's bit image, and
+    # the bits must equal torch's (z > 0) everywhere outside that bound
+    bits = relu_bits(masks, nh, net.hp, hidden, M)
+    with torch.no_grad():
+        h = x
+        for L, (W, b) in enumerate(layers[:-1]):
+            z = torch.nn.functional.linear(h, W, b)
+            bound = W.shape[1] * 1.2e-7 * (h.abs() @ W.abs().t() + b.abs())
+            assert torch.equal(bits[L][z.abs() > bound], (z > 0)[z.abs() > bound]), L
+            h = torch.relu(z)
     tl = [(W.clone().requires_grad_(True), b.clone().requires_grad_(True)) for W, b in layers]
     xr = x.clone().requires_grad_(True)
-    y = torch_mlp(tl, xr)
-    (y * dy).sum().backward()
+    h = xr
+    for L, (W, b) in enumerate(tl):
+        h = torch.nn.functional.linear(h, W, b)
+        if L < nh:
+            h = h * bits[L].float()
+    (h * dy).sum().backward()
     assert torch.allclose(dx.cpu(), xr.grad, rtol=1e-3, atol=1e-6 * (xr.grad.abs().max() + 1e-3))
     gflat = grad.cpu()
     assert torch.isfinite(gflat).all()
