@@ -250,6 +250,45 @@ __global__ __launch_bounds__(kDemoBlock) void k_demo_reward(nav_params p, int64_
     if (reward_out) reward_out[e] = r;
 }
 
+// The same for a handful of envs (the N = 1 drop-in's process_transition): one workgroup per env,
+// its threads over the demonstration points (a lane per point instead of a lane per env), the
+// minimum by wave shuffles and LDS — the same f64 minimum over the same set, so the same reward.
+__global__ __launch_bounds__(kDemoBlock) void k_demo_reward_few(nav_params p,
+                                                                const double2* __restrict__ ns,
+                                                                const double* __restrict__ gterm,
+                                                                const uint8_t* __restrict__ flags,
+                                                                const double* __restrict__ demo,
+                                                                const int64_t* __restrict__ off,
+                                                                int64_t m_shared, int32_t epg,
+                                                                float* __restrict__ rows,
+                                                                int64_t cap, int64_t base,
+                                                                double* __restrict__ reward_out) {
+    __shared__ double part[kDemoBlock / 64];
+    const int64_t e = blockIdx.x;
+    const uint8_t f = flags[e];
+    if (!(f & F_DEMO)) return;  // workgroup-uniform
+    const double2 s = ns[e];
+    const int64_t g = off ? e / epg : 0;
+    const int64_t lo = off ? off[g] : 0, hi = off ? off[g + 1] : m_shared;
+    double best = __builtin_inf();
+    for (int64_t j = lo + threadIdx.x; j < hi; j += kDemoBlock)
+        best = fmin(sqd(s.x, s.y, demo[2 * j], demo[2 * j + 1]), best);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) best = fmin(best, __shfl_xor(best, o, 64));
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = best;
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+#pragma unroll
+    for (int k = 1; k < kDemoBlock / 64; ++k) best = fmin(best, part[k]);
+    // robot.py:756-760 then the stuck penalty of robot.py:667-669 (k_demo_reward's order)
+    const double mn = sqrt(best);
+    double r = gterm[e] + p.demo_factor * (-mn);
+    if (f & F_STUCK) r -= p.stuck_penalty;
+    const int64_t slot = (base + e) % cap;
+    rows[slot * NAV_ROW + 4] = (float)r;
+    if (reward_out) reward_out[e] = r;
+}
+
 // Batched open-loop rollouts through Environment.dynamics (the CEM demonstrator's inner loop,
 // environment.py:151-165): lane = path, T sequential steps, state carried in f64; paths [P][T+1][2]
 // f64; reward (nullable) = -||f32(s_T) - goal|| as compute_reward on the float32 planning_paths
@@ -1156,6 +1195,14 @@ int nav_demo_reward(const nav_params* p, int64_t n, const double* next_state,
     if (demo_off && epg <= 0) return NAV_EINVAL;
     if (!demo_off && m > 0 && !demo_xy) return NAV_EINVAL;
     if (n == 0 || (!demo_off && m == 0)) return 0;
+    if (n <= 8) {  // a lane per point (the N = 1 drop-in): 81 us -> a few per call
+        hipLaunchKernelGGL(k_demo_reward_few, dim3((unsigned)n), dim3(kDemoBlock), 0, S(stream),
+                           *p, reinterpret_cast<const double2*>(next_state), goal_term, flags,
+                           demo_xy, demo_off, m, epg > 0 ? epg : 1, replay->rows,
+                           replay->capacity, replay_base % replay->capacity, reward_out);
+        NAV_CHECK_LAUNCH();
+        return 0;
+    }
     hipLaunchKernelGGL(k_demo_reward, dim3((unsigned)((n + kDemoEnvs - 1) / kDemoEnvs)),
                        dim3(kDemoBlock), 0, S(stream), *p, n,
                        reinterpret_cast<const double2*>(next_state), goal_term, flags, demo_xy,

@@ -996,6 +996,7 @@ struct CriticRowsArgs {
     uint32_t save_mask;
     uint16_t* masks[2];
     int row_backward;     // also each online critic's row backward (robot.py:361 .backward())
+    int split_twins;      // grid.y = 2: workgroup y runs online critic y only (small batches)
     float* dz[2];         // [nh][B][hp] dz rows of dz_save_mask layers (row_backward)
     uint32_t dz_save_mask;
 };
@@ -1082,9 +1083,10 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
     }
     __syncthreads();
     NAV_MARK(21);
-    // online critics on (s, a)
+    // online critics on (s, a): both, or (split_twins) the one of this workgroup's grid row
 #pragma unroll 1
     for (int q = 0; q < 2; ++q) {
+        if (a.split_twins && q != (int)blockIdx.y) continue;  // workgroup-uniform
         fwd_net<NT, RT>(a.critic[q], act, xin, red, a.masks[q], n_rt, a.acts[q], a.save_mask, row0,
                         B, rt0, top, 22 + 14 * q);
         float* es = a.eslab[q] ? a.eslab[q] + (int64_t)blockIdx.x * a.ecount : nullptr;
@@ -1270,7 +1272,8 @@ void launch_critic_rows_k(const CriticRowsArgs& a, hipStream_t st) {
     auto k = k_td3_critic_rows<NT, RT>;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
-    hipLaunchKernelGGL(k, dim3((unsigned)((a.B + TM - 1) / TM)), dim3(kBlock), lds, st, a);
+    hipLaunchKernelGGL(k, dim3((unsigned)((a.B + TM - 1) / TM), a.split_twins ? 2u : 1u),
+                       dim3(kBlock), lds, st, a);
 }
 
 template <int NT, int RT>
@@ -1602,6 +1605,14 @@ int nav_td3_critic_rows(const nav_mlp* target_actor, const nav_mlp* target_criti
     }
     a.row_backward = row_backward ? 1 : 0;
     a.dz_save_mask = row_backward ? dz_save_mask : 0u;
+    // Small batches leave most CUs idle and each workgroup's chain of network passes sets the
+    // time: the twin online critics then run in separate workgroups (grid.y = 2), each repeating
+    // the sampling, target actor and twin target critics (identical values) — 5 instead of 7
+    // passes per workgroup. NAV_CRITIC_SPLIT_MAX overrides the batch threshold (tuning only).
+    static const int64_t split_max = getenv("NAV_CRITIC_SPLIT_MAX")
+                                         ? (int64_t)atoll(getenv("NAV_CRITIC_SPLIT_MAX"))
+                                         : (int64_t)2048;
+    a.split_twins = B <= split_max ? 1 : 0;
     a.B = B;
     a.rows = replay->rows;
     a.rsize = size;
