@@ -185,6 +185,8 @@ def tick_forms(tr, reps=50):
 
 
 def cpu_info():
+    """(CPU model, CPUs this process may run on, CPUs the machine has). os.cpu_count() ignores
+    the lease's affinity mask; sched_getaffinity does not."""
     model = None
     try:
         with open("/proc/cpuinfo") as f:
@@ -194,7 +196,7 @@ def cpu_info():
                     break
     except OSError:
         pass
-    return model, os.cpu_count()
+    return model, len(os.sched_getaffinity(0)), os.cpu_count()
 
 
 def cpu_baseline(args, trainer):
@@ -208,19 +210,34 @@ def cpu_baseline(args, trainer):
     pts = trainer.env.demo_xy.cpu().numpy()
     off = trainer.env.demo_off.cpu().numpy() if trainer.env.demo_off is not None else \
         [0, len(pts)]
-    port = CPUPort(n, args.hidden, args.layers, args.batch, args.updates,
-                   args.envs_per_group, args.seed, speed, angle, pts, off)
-    k, dt = time_port(port, args.cpu_budget, 64)
+    model, affinity, machine = cpu_info()
+    # one thread per CPU this process may use, capped by the lease's CPU share (OMP_NUM_THREADS,
+    # 16 per GPU on the box): the OpenMP env tick and torch's intra-op pool both run that many
+    share = int(os.environ.get("OMP_NUM_THREADS", affinity) or affinity)
+    threads = max(1, min(affinity, share))
+    O.lib().orc_set_threads(threads)
+    torch_threads = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        port = CPUPort(n, args.hidden, args.layers, args.batch, args.updates,
+                       args.envs_per_group, args.seed, speed, angle, pts, off)
+        k, dt = time_port(port, args.cpu_budget, 64)
+        omp = O.lib().orc_threads()
+        used = torch.get_num_threads()
+    finally:
+        torch.set_num_threads(torch_threads)
     single = single_env_rates(speed, angle, pts[off[0]:off[1]], 2.0)
-    model, nproc = cpu_info()
-    threads = max(O.lib().orc_threads(), torch.get_num_threads())
     return {"value": k * n / dt, "unit": "env-steps/s", "cores": threads,
             "kind": "port",
             "sample": f"{k} vector steps of the same workload ({n} envs, TD3 {args.updates} "
                       f"epochs x batch {args.batch}, {args.layers}x{args.hidden}) on the oracle "
                       f"CPU port: C OpenMP env tick with the same exact bucketed demo index as the "
                       f"GPU + torch-CPU fp32 TD3, {threads} threads, {dt:.1f} s",
-            "cpu_model": model, "nproc": nproc,
+            "cpu_model": model, "affinity_cpus": affinity, "omp_threads": omp,
+            "torch_threads": used, "cpu_share": share, "machine_cpus": machine,
+            "cores_note": "cores = threads run = min(CPUs in this process's affinity mask, the "
+                          "lease's CPU share OMP_NUM_THREADS); machine_cpus is os.cpu_count(), "
+                          "which ignores the affinity mask",
             "single_env_1core": {k2: round(v, 1) for k2, v in single.items()},
             "single_env_note": "one env, one core, the C restatement looping in one call: "
                                "Environment.step alone / the whole agent tick without the learner"}

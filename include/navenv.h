@@ -253,11 +253,13 @@ int nav_cem_elite(int32_t n_prob, int32_t P, int32_t T, int32_t E, const double*
                   const float* actions, float* mean, float* stdv, int32_t* best, void* stream);
 /* environment.py:59-95 set_dynamics as nav.fields restates it (perlin_noise is absent: the field
  * values are parity unpinned against the reference): unit gradient tables g5 [6][6][2],
- * g10 [11][11][2], g20 [21][21][2] (speed octaves) and ga5 [6][6][2] (angle), f64, from the
- * host's seeded draws; field out [100][100][2] float32 (speed, angle) x-major, the table every
- * dynamics kernel reads. Same f32 values as nav.fields.make_fields (speed within 4 ulp: numpy's f32 exp). */
-int nav_fields_generate(const double* g5, const double* g10, const double* g20,
-                        const double* ga5, float* field, void* stream);
+ * g10 [11][11][2], g20 [21][21][2], f64, from the host's seeded draws. The speed cells mix the
+ * three octaves (environment.py:72-74); the angle cells are the SAME octave-5 noise (:85 is the
+ * function of :62), min-max normalised. field out [100][100][2] float32 (speed, angle) x-major,
+ * the table every dynamics kernel reads. Same f32 values as nav.fields.make_fields (angle bit
+ * for bit, speed within 4 ulp: numpy's f32 exp). */
+int nav_fields_generate(const double* g5, const double* g10, const double* g20, float* field,
+                        void* stream);
 /* Robot.process_demonstration's demonstration set for n_demo demonstrations (robot.py:694-698,
  * 771-824): per demo its T states [T][2] (f32, the CEM output) followed by n_aug augmentations
  * of (T-1)*(steps+1) + 1 states each, f64 out [n_demo][T + n_aug*((T-1)(steps+1)+1)][2];

@@ -593,6 +593,14 @@ int orc_threads(void) {
 #endif
 }
 
+void orc_set_threads(int n) {
+#ifdef _OPENMP
+    if (n > 0) omp_set_num_threads(n);
+#else
+    (void)n;
+#endif
+}
+
 void orc_vec_agent_step_batch(const orc_params_t* p, const float* speed, const float* angle,
                               const double* demo, int64_t m, int64_t n, double* state,
                               const double* goal, const double* region, double* hist,

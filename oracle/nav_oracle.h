@@ -106,6 +106,7 @@ void orc_act_epilogue(const double* s, const double* g, const float* residual, d
 
 /* Whole-batch helpers for the cpu_baseline leg (OpenMP over envs when built with -fopenmp). */
 int  orc_threads(void);
+void orc_set_threads(int n); /* OpenMP team size of the batched tick (cpu_baseline) */
 void orc_vec_agent_step_batch(const orc_params_t* p, const float* speed, const float* angle,
                               const double* demo_xy, int64_t m, int64_t n, double* state,
                               const double* goal, const double* region, double* hist,

@@ -84,6 +84,8 @@ def lib():
                                          _dp, _fp, _dp, _dp]
         L.orc_act_epilogue.argtypes = [_dp, _dp, _fp, C.c_double, _dp, C.c_double, _dp]
         L.orc_threads.restype = C.c_int
+        L.orc_set_threads.restype = None
+        L.orc_set_threads.argtypes = [C.c_int]
         L.orc_vec_agent_step_batch.argtypes = [C.POINTER(Params), _fp, _fp, _dp, C.c_int64,
                                                C.c_int64, _dp, _dp, _dp, _dp, _u32p, _i32p, _i32p,
                                                _i32p, _dp, _dp, _dp, _fp, C.c_int64, C.c_int64,

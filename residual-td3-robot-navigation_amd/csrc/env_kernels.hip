@@ -366,7 +366,7 @@ __global__ __launch_bounds__(kBlock) void k_cem_rollout(const float2* __restrict
 // nav.fields' construction on the device: per cell (i, j) of the x-major 100 x 100 grid the f64
 // gradient noise of octave o at (i/100*o, j/100*o) from the unit gradient table g_o [o+1][o+1][2]
 // (quintic fade, bilinear blend), speed cells = f32((n5 + .5 n10) + .25 n20), angle cells =
-// f32(n5'), each min-max normalised in f32 and the speed stretched by 1/(1 + exp(-10 (x - .5)))
+// f32(n5) (the same octave-5 values), each min-max normalised in f32 and the speed stretched by 1/(1 + exp(-10 (x - .5)))
 // in f32 (the exp rounded from f64) — numpy's operation order, -ffp-contract=off. One 1024-thread workgroup (10 000 cells,
 // block min / max in LDS); field out [100][100][2] (speed, angle) interleaved, the kernels'
 // table layout.
@@ -414,7 +414,6 @@ NAV_DEV void block_minmax(float& mn, float& mx, float* red) {
 __global__ __launch_bounds__(kFieldThreads) void k_fields(const double* __restrict__ g5,
                                                           const double* __restrict__ g10,
                                                           const double* __restrict__ g20,
-                                                          const double* __restrict__ ga,
                                                           float2* __restrict__ field) {
     constexpr int N = NAV_WORLD_CELLS * NAV_WORLD_CELLS;
     __shared__ float sp[N];
@@ -423,9 +422,11 @@ __global__ __launch_bounds__(kFieldThreads) void k_fields(const double* __restri
     float smn = __builtin_inff(), smx = -__builtin_inff(), amn = smn, amx = smx;
     for (int c = threadIdx.x; c < N; c += kFieldThreads) {
         const int i = c / NAV_WORLD_CELLS, j = c % NAV_WORLD_CELLS;
-        const double v = (grad_noise(g5, 5, i, j) + 0.5 * grad_noise(g10, 10, i, j)) +
-                         0.25 * grad_noise(g20, 20, i, j);
-        const float fs = (float)v, fa = (float)grad_noise(ga, 5, i, j);
+        // the angle's noise IS the speed's first term (environment.py:62 and :85: the same
+        // PerlinNoise(octaves=5, seed) function), so one evaluation feeds both tables
+        const double n5 = grad_noise(g5, 5, i, j);
+        const double v = (n5 + 0.5 * grad_noise(g10, 10, i, j)) + 0.25 * grad_noise(g20, 20, i, j);
+        const float fs = (float)v, fa = (float)n5;
         sp[c] = fs;
         an[c] = fa;
         smn = fminf(smn, fs);
@@ -1145,10 +1146,10 @@ int nav_cem_elite(int32_t n_prob, int32_t P, int32_t T, int32_t E, const double*
     return 0;
 }
 
-int nav_fields_generate(const double* g5, const double* g10, const double* g20,
-                        const double* ga5, float* field, void* stream) {
-    if (!g5 || !g10 || !g20 || !ga5 || !field) return NAV_EINVAL;
-    hipLaunchKernelGGL(k_fields, dim3(1), dim3(kFieldThreads), 0, S(stream), g5, g10, g20, ga5,
+int nav_fields_generate(const double* g5, const double* g10, const double* g20, float* field,
+                        void* stream) {
+    if (!g5 || !g10 || !g20 || !field) return NAV_EINVAL;
+    hipLaunchKernelGGL(k_fields, dim3(1), dim3(kFieldThreads), 0, S(stream), g5, g10, g20,
                        reinterpret_cast<float2*>(field));
     NAV_CHECK_LAUNCH();
     return 0;

@@ -1041,9 +1041,11 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
         float4 lo = make_float4(0.f, 0.f, 0.f, 0.f), hi = lo;
         if (b < B) {
             sample_row(a.rows, a.rsize, a.idx, a.seed_lo, a.seed_hi, a.sample_ctr, b, lo, hi);
-            float4* dst = reinterpret_cast<float4*>(a.batch) + 2 * b;
-            dst[0] = lo;
-            dst[1] = hi;
+            if (blockIdx.y == 0) {  // split twins: one writer per batch row
+                float4* dst = reinterpret_cast<float4*>(a.batch) + 2 * b;
+                dst[0] = lo;
+                dst[1] = hi;
+            }
         }
         *reinterpret_cast<float4*>(brow + tid * 8) = lo;
         *reinterpret_cast<float4*>(brow + tid * 8 + 4) = hi;
@@ -1608,10 +1610,10 @@ int nav_td3_critic_rows(const nav_mlp* target_actor, const nav_mlp* target_criti
     // Small batches leave most CUs idle and each workgroup's chain of network passes sets the
     // time: the twin online critics then run in separate workgroups (grid.y = 2), each repeating
     // the sampling, target actor and twin target critics (identical values) — 5 instead of 7
-    // passes per workgroup. NAV_CRITIC_SPLIT_MAX overrides the batch threshold (tuning only).
-    static const int64_t split_max = getenv("NAV_CRITIC_SPLIT_MAX")
-                                         ? (int64_t)atoll(getenv("NAV_CRITIC_SPLIT_MAX"))
-                                         : (int64_t)2048;
+    // passes per workgroup. NAV_CRITIC_SPLIT_MAX overrides the batch threshold, read at every
+    // call (tuning, and the test that runs one batch both ways).
+    const char* split_env = getenv("NAV_CRITIC_SPLIT_MAX");
+    const int64_t split_max = split_env ? (int64_t)atoll(split_env) : (int64_t)2048;
     a.split_twins = B <= split_max ? 1 : 0;
     a.B = B;
     a.rows = replay->rows;

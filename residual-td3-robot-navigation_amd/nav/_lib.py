@@ -84,7 +84,7 @@ SIGNATURES = [
     ("nav_demo_index_scan", C.c_int, [_vp, C.c_int32, _vp, _vp]),
     ("nav_demo_index_fill", C.c_int, [_vp, _vp, C.c_int32, C.c_int64, _vp, _vp, _vp, _vp]),
     ("nav_demo_index_res", C.c_int32, []),
-    ("nav_fields_generate", C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
+    ("nav_fields_generate", C.c_int, [_vp, _vp, _vp, _vp, _vp]),
     ("nav_demo_augment", C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, _vp, _vp, _vp,
                                    _vp]),
     ("nav_demo_index_subplan", C.c_int, [_vp, _vp, C.c_int32, _vp, _vp, _vp, _vp, _vp]),

@@ -19,15 +19,13 @@ def _gradient_table(rng, octaves):
 
 
 def gradient_tables(seed):
-    """(g5, g10, g20, ga5): make_fields' gradient tables, drawn in its order."""
+    """(g5, g10, g20): make_fields' gradient tables, drawn in its order."""
     rng = np.random.default_rng(seed)
-    return tuple(_gradient_table(rng, o) for o in (5, 10, 20, 5))
+    return tuple(_gradient_table(rng, o) for o in (5, 10, 20))
 
 
-def _gradient_noise(rng, octaves, n=100, g=None):
-    """Classic 2-D Perlin gradient noise with `octaves` lattice cells across [0,1)."""
-    if g is None:
-        g = _gradient_table(rng, octaves)
+def _gradient_noise(g, octaves, n=100):
+    """Classic 2-D Perlin gradient noise with `octaves` lattice cells across [0,1), f64."""
     u = np.arange(n) / n * octaves
     x, y = np.meshgrid(u, u, indexing="ij")  # [col][row] like environment.py:69-75
     x0, y0 = np.floor(x).astype(int), np.floor(y).astype(int)
@@ -46,17 +44,26 @@ def _gradient_noise(rng, octaves, n=100, g=None):
     return (n00 * (1 - wx) + n10 * wx) * (1 - wy) + (n01 * (1 - wx) + n11 * wx) * wy
 
 
+def noise_terms(seed):
+    """(noise5, noise10, noise20): the three f64 [100][100] noise functions sampled at
+    (col/100, row/100) — PerlinNoise(octaves=5/10/20, seed) of environment.py:62-64."""
+    return tuple(_gradient_noise(g, o) for g, o in zip(gradient_tables(seed), (5, 10, 20)))
+
+
+def minmax(cells):
+    """environment.py:77-79 / :92-94 on a float32 table (float32 arithmetic, NEP 50)."""
+    mn, mx = np.min(cells), np.max(cells)
+    return (cells - mn) / (mx - mn)
+
+
 def make_fields(seed):
     """(speed, angle) float32 [100][100], x-major, value ranges as set_dynamics produces."""
-    rng = np.random.default_rng(seed)
-    cells = (_gradient_noise(rng, 5) + 0.5 * _gradient_noise(rng, 10)
-             + 0.25 * _gradient_noise(rng, 20)).astype(np.float32)
-    mn, mx = np.min(cells), np.max(cells)
-    norm = (cells - mn) / (mx - mn)
+    n5, n10, n20 = noise_terms(seed)
+    # environment.py:72-75: the cell sum in Python floats, stored float32
+    norm = minmax(((n5 + 0.5 * n10) + 0.25 * n20).astype(np.float32))
     speed = (1 / (1 + np.exp(-10 * (norm - 0.5)))).astype(np.float32)
-    cells = _gradient_noise(rng, 5).astype(np.float32)
-    mn, mx = np.min(cells), np.max(cells)
-    angle = ((cells - mn) / (mx - mn)).astype(np.float32)
+    # environment.py:85-95: the SAME octave-5 function as the speed's first term
+    angle = minmax(n5.astype(np.float32)).astype(np.float32)
     return speed, angle
 
 

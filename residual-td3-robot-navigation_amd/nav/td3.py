@@ -70,9 +70,17 @@ class TD3:
         self.seed = seed
         self.update_counter = 0  # Philox counter for sampling / smoothing noise
         # shared policy (BASELINE config 5): grad_hook(bucket) SUM-all-reduces a flat gradient
-        # bucket in place (nav.dist.GradAllReduce: RCCL over xGMI); Adam divides by grad_div
+        # bucket in place (nav.dist.GradAllReduce: RCCL over xGMI) and Adam divides by the hook's
+        # world_size. The contract is explicit: a hook without world_size is refused, since a
+        # plain SUM callable would silently train on world_size x the mean gradient.
         self.grad_hook = grad_hook
-        self.grad_div = float(getattr(grad_hook, "world_size", 1)) if grad_hook else 1.0
+        self.grad_div = 1.0
+        if grad_hook is not None:
+            ws = getattr(grad_hook, "world_size", None)
+            if not isinstance(ws, int) or ws < 1:
+                raise ValueError("grad_hook must carry an int world_size >= 1: it SUM-all-reduces "
+                                 "the gradient bucket and Adam divides by world_size")
+            self.grad_div = float(ws)
         # train_critic's row backward inside the critic_rows launch (NAV_CRITIC_ROW_BWD=0: its
         # own launch; tuning / A/B only)
         self.row_backward = os.environ.get("NAV_CRITIC_ROW_BWD", "1") != "0"

@@ -50,6 +50,13 @@ def test_environment_dynamics_and_step_api(navmods):
         assert np.max(np.abs(after - d["step"][i])) < 1e-11
 
 
+def ulps_f32(a, b):
+    """|a - b| in float32 ulps (both finite float32 of one sign: positions in the world)."""
+    a = np.asarray(a, np.float32).view(np.int32).astype(np.int64)
+    b = np.asarray(b, np.float32).view(np.int32).astype(np.int64)
+    return np.abs(a - b)
+
+
 def _trace_setup(environment, robot):
     t = golden("trace.npz")
     torch.manual_seed(0)
@@ -68,7 +75,12 @@ def test_demonstration_matches_reference(navmods):
     ds, da = env.get_demonstration()
     assert ds.dtype == np.float32 and ds.shape == (200, 2) and da.shape == (200, 2)
     assert np.array_equal(da, t["demo_actions"][0])
-    assert np.max(np.abs(ds - t["demo_states"][0])) < 1e-4
+    # nav/demos.py's claim, checked: the GPU CEM's dynamics differs from numpy's by < 1e-14
+    # before environment.py:179's float32 cast, which can move a state by at most one float32
+    # ulp (<= 7.6e-6 in [64, 128): inside north_star's 1e-5)
+    ref = t["demo_states"][0].astype(np.float32)
+    assert np.all(ulps_f32(ds, ref) <= 1), int(ulps_f32(ds, ref).max())
+    assert np.max(np.abs(ds.astype(np.float64) - ref)) <= 1e-5
 
 
 def test_robot_replays_reference_trace(navmods):
@@ -116,7 +128,12 @@ def test_robot_replays_reference_trace(navmods):
         assert rb.current_noise_scale == cc[6]
     assert len(rb.demonstration_states) == len(t["demo_set"])
     got = np.asarray([np.asarray(x, np.float64) for x in rb.demonstration_states])
-    assert np.max(np.abs(got - t["demo_set"])) < 1e-4
+    # the originals are the CEM's float32 states (<= 1 ulp, above); an augmented point is a
+    # float32 interpolation of two of them plus float64 noise (robot.py:795-816), so it moves
+    # by at most what one ulp of its endpoints moves the interpolation: north_star's 1e-5
+    err = np.abs(got - t["demo_set"])
+    print(f"demo set: max |diff| {err.max():.3e}, exact {np.mean(err == 0):.4f}")
+    assert err.max() <= 1e-5
     assert len(rb.memory) == len(t["push_r"])
 
 

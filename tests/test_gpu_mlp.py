@@ -552,3 +552,52 @@ def test_fused_row_kernels_match_unfused(nav, hidden, nh, B):
     assert torch.equal(u["es"], v["es"])
     if actor.middle_layers():
         assert torch.equal(u["dz"][1:nh - 1], v["dz"][1:nh - 1])
+
+
+@pytest.mark.parametrize("hidden,nh,B", [(256, 2, 100), (256, 2, 2048), (200, 3, 777)])
+def test_critic_rows_split_twins_bit_identical(nav, hidden, nh, B, monkeypatch):
+    """nav_td3_critic_rows with the twin online critics in separate workgroups (grid.y = 2, the
+    small-batch form) and in one (grid.y = 1) at the same batch: batch rows, dq, loss partials,
+    edge slabs, saved rows, ReLU bits and dz all bit-equal (same per-critic device code and
+    order; the twin workgroups only repeat the target passes, and only y == 0 writes `batch`)."""
+    from nav._lib import NavReplay, descs, lib, parr, ptr, stream_handle
+    L = lib()
+    s = stream_handle()
+    ta, _ = make_net(2, 2, hidden, nh, 161)
+    tc = [make_net(4, 1, hidden, nh, 162 + k)[0] for k in range(2)]
+    cr = [make_net(4, 1, hidden, nh, 164 + k)[0] for k in range(2)]
+    hp = ta.hp
+    cap = 3000
+    g = torch.Generator().manual_seed(19)
+    rows = torch.randn(cap, 8, generator=g) * 10
+    rows[:, 7] = (torch.rand(cap, generator=g) < 0.1).float()
+    rows = rows.to(DEV)
+    rd = NavReplay(rows.data_ptr(), cap)
+    mid = cr[0].middle_layers()
+    nblk = L.nav_mlp_row_blocks(B)
+    f = lambda *sh: torch.full(sh, float("nan"), device=DEV)  # noqa: E731
+    ec = L.nav_mlp_edge_count(4, 1, hp, nh)
+    out = {}
+    for split in (True, False):
+        monkeypatch.setenv("NAV_CRITIC_SPLIT_MAX", str(B if split else 0))
+        o = dict(batch=f(B, 8), dq=[f(B), f(B)], lp=f(2, nblk), es=[f(nblk, ec), f(nblk, ec)],
+                 acts=[f(nh, B, hp), f(nh, B, hp)], dz=[f(nh, B, hp), f(nh, B, hp)],
+                 masks=[cr[0].mask_buffer(B) for _ in range(2)])
+        assert L.nav_td3_critic_rows(
+            C.byref(ta.desc()), descs(*tc), descs(*cr), C.byref(rd), cap, B, None, 1707366464,
+            0, 5, None, 0.2, 0.5, 5.0, 0.99, ptr(o["batch"]), parr(*o["dq"]),
+            parr(o["lp"][0], o["lp"][1]), parr(*o["es"]), parr(*o["acts"]), mid,
+            parr(*o["masks"]), 1, parr(*o["dz"]), mid, s) == 0
+        out[split] = o
+    torch.cuda.synchronize()
+    a, b = out[True], out[False]
+    assert torch.equal(a["batch"], b["batch"])
+    assert torch.equal(a["lp"], b["lp"])
+    for k in range(2):
+        assert torch.equal(a["dq"][k], b["dq"][k]), k
+        assert torch.equal(a["es"][k], b["es"][k]), k
+        assert torch.equal(a["masks"][k], b["masks"][k]), k
+        if mid:
+            sel = [l for l in range(nh) if (mid >> l) & 1]
+            assert torch.equal(a["acts"][k][sel], b["acts"][k][sel]), k
+            assert torch.equal(a["dz"][k][sel], b["dz"][k][sel]), k
