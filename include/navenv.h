@@ -91,9 +91,10 @@ typedef struct nav_replay {
 /* ReLU MLP (robot.py:128-206) in the device layout: one flat fp32 buffer per network,
  * hidden width padded to a multiple of 32 with zeros (exact: relu(0)=0, zero rows/cols add 0):
  *   W0 [hp][d_in], b0 [hp], {Wl [hp][hp], bl [hp]} x (n_hidden-1), Wo [d_out][hp], bo [d_out]
- * plus `packed` = per hidden->hidden layer: Wf [hp/4][hp][4] (Wf[q][n][j] = W[n][4q+j]) then
- * Wb [hp/4][hp][4] (Wb[q][k][j] = W[4q+j][k]); kept current by nav_adam / nav_polyak /
- * nav_mlp_pack. */
+ * plus `packed` = per hidden->hidden layer the split bf16 MFMA B-operand images of the forward
+ * (B[k][n] = W[n][k]) then of the backward (B[k][n] = W[k][n]) product: each W entry as three
+ * bf16 hi + mid + lo == W exactly, laid out [plane 3][hp/16][2][hp][8] (entry (p, k/16, (k/8)&1,
+ * n, k&7)), 1.5 hp^2 floats per image; kept current by nav_adam / nav_polyak / nav_mlp_pack. */
 typedef struct nav_mlp {
     int32_t d_in;       /* 2 actor (robot.py:145), 4 critic (robot.py:185) */
     int32_t d_out;      /* 2 actor, 1 critic */

@@ -574,17 +574,31 @@ struct PackInfo {
 };
 
 NAV_DEV void repack(const PackInfo& pk, int64_t i, float4 v) {
-    // i = flat float index of v.x (multiple of 4)
+    // i = flat float index of v.x (multiple of 4): W[n][k .. k+3] of a hidden x hidden layer ->
+    // the three bf16 planes of the forward image (B[k][n], 4 consecutive j: one 8-B store per
+    // plane) and of the backward image (B[n][k + c], 4 columns)
     for (int L = 1; L < pk.n_hidden; ++L) {
-        const int64_t off = pk.w_off[L], sz = (int64_t)pk.hp * pk.hp;
+        const int hp = pk.hp;
+        const int64_t off = pk.w_off[L], sz = (int64_t)hp * hp;
         if (i >= off && i < off + sz) {
             const int64_t e = i - off;
-            const int n = (int)(e / pk.hp), k = (int)(e % pk.hp);
-            float* Wf = pk.packed + (int64_t)(L - 1) * 2 * sz;
-            float* Wb = Wf + sz;
-            *reinterpret_cast<float4*>(Wf + ((int64_t)(k >> 2) * pk.hp + n) * 4) = v;
-            float* d = Wb + ((int64_t)(n >> 2) * pk.hp + k) * 4 + (n & 3);
-            d[0] = v.x; d[4] = v.y; d[8] = v.z; d[12] = v.w;
+            const int n = (int)(e / hp), k = (int)(e % hp);
+            const int64_t img = split_image_floats(hp);
+            __bf16* Wf = reinterpret_cast<__bf16*>(pk.packed + (int64_t)(L - 1) * 2 * img);
+            __bf16* Wb = reinterpret_cast<__bf16*>(pk.packed + (int64_t)(L - 1) * 2 * img + img);
+            const float x[4] = {v.x, v.y, v.z, v.w};
+            __bf16 sp[3][4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) split1(x[c], sp[0][c], sp[1][c], sp[2][c]);
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+                bf16x4 q4;
+                q4[0] = sp[p][0]; q4[1] = sp[p][1]; q4[2] = sp[p][2]; q4[3] = sp[p][3];
+                *reinterpret_cast<bf16x4*>(Wf + split_entry(hp, p, k, n)) = q4;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) Wb[split_entry(hp, p, n, k + c)] = sp[p][c];
+            }
             return;
         }
     }

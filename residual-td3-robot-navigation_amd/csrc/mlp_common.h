@@ -99,6 +99,65 @@ NAV_DEV f32x16 mfma(float a, float b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
 
+// ---- fp32 GEMMs on the bf16 matrix cores (the hidden x hidden products) ----
+// Every f32 operand x is split EXACTLY into three bf16 x = hi + mid + lo (hi = bf16(x),
+// mid = bf16(x - hi), lo = x - hi - mid, each step round-to-nearest; the remainders are exact in
+// f32 and lo has <= 8 significant bits), and a product sum_k a_k b_k is formed from the six
+// partial products hh + hm + mh + mm + hl + lh on v_mfma_f32_32x32x16_bf16 (f32 accumulate). The
+// three dropped ones (ml, lm, ll) are below 2^-23 |a||b| in total: the GEMM carries f32 accuracy
+// (probe tools/probe/split_gemm_probe.hip: rms error vs fp64 6.5e-7 against 5.8e-7 for the exact
+// f32 MFMA chain) at 16/6 of the f32 MFMA rate (bf16 MFMA is 16x f32 MFMA on gfx950).
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+NAV_DEV f32x16 mfma16(bf16x8 a, bf16x8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+struct Split3 {
+    bf16x8 h, m, l;
+};
+
+NAV_DEV void split1(float x, __bf16& h, __bf16& m, __bf16& l) {
+    h = (__bf16)x;
+    const float r = x - (float)h;
+    m = (__bf16)r;
+    l = (__bf16)(r - (float)m);
+}
+
+// 8 consecutive-k f32 values -> the three bf16 fragments
+NAV_DEV Split3 split8(float4 x0, float4 x1) {
+    const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+    Split3 s;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        __bf16 h, m, l;
+        split1(v[j], h, m, l);
+        s.h[j] = h;
+        s.m[j] = m;
+        s.l[j] = l;
+    }
+    return s;
+}
+
+// acc += a . b over one 16-deep k step, the six partial products smallest first
+NAV_DEV f32x16 mfma_x6(const Split3& a, const bf16x8 (&b)[3], f32x16 c) {
+    c = mfma16(a.m, b[1], c);
+    c = mfma16(a.l, b[0], c);
+    c = mfma16(a.h, b[2], c);
+    c = mfma16(a.m, b[0], c);
+    c = mfma16(a.h, b[1], c);
+    return mfma16(a.h, b[0], c);
+}
+
+// Split B-operand image of one hp x hp matrix B[k][n] (k = the product's K): entry
+// (plane p, k step q = k / 16, lane half h = (k / 8) & 1, column n) holds the 8 bf16 of plane p
+// of B[16q + 8h + j][n], j = 0..7 — one 16-B load per lane per plane and k step, 32 lanes of a
+// half-wave on 512 consecutive bytes. [3][hp/16][2][hp] x 8 bf16 = 1.5 hp^2 floats.
+__host__ __device__ constexpr int64_t split_image_floats(int hp) { return (int64_t)3 * hp * hp / 2; }
+__host__ __device__ inline int64_t split_entry(int hp, int p, int k, int n) {
+    return ((((int64_t)p * (hp / 16) + (k >> 4)) * 2 + ((k >> 3) & 1)) * hp + n) * 8 + (k & 7);
+}
+
 NAV_DEV int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
 
 // Column tiles of a wave: wave w owns 32-column tiles t = w and w + 4 (when < NT) of every

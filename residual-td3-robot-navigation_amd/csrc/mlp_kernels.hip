@@ -12,6 +12,10 @@
 #include "mlp_common.h"
 #include "nav_tick.h"
 
+#ifndef NAV_GEMM_INTERLEAVE
+#define NAV_GEMM_INTERLEAVE 0
+#endif
+
 namespace {
 
 template <int NT>
@@ -21,16 +25,21 @@ struct WaveCols {
     NAV_DEV WaveCols(int wv) : t0(wv), t1(wv + 4), has0(NT >= 4 || wv < NT), has1(NT >= 8 || wv + 4 < NT) {}
 };
 
-// acc[rt][j] = A[128 rows][hp] (LDS, row stride S_) x B[hp][tile t_j], B from a packed image in
-// global memory [hp/4][hp][4] (element (k, n) at ((k>>2)*hp + n)*4 + (k&3)) — L2-resident, read
-// once per workgroup, prefetched two K-steps ahead in registers. No barrier inside the K loop:
-// the LDS rows are read-only during the product. K order inside an 8-deep step is permuted the
-// same way for A and B (lane half h covers k = 8q + 4h + s at MFMA s).
+// acc[rt][j] = A[TM rows][hp] (LDS f32, row stride S_) x B[hp][tile t_j] on the bf16 matrix
+// cores at f32 accuracy (mlp_common.h: three-way exact bf16 split, six partial products). B is the
+// layer's split image (split_entry layout) in global memory — L2-resident, read once per
+// workgroup, each 16-deep k step's three planes loaded one step ahead; A is read from the LDS rows
+// (two 16-B reads per row tile and step) and split in registers one step ahead too, the split
+// of step q+1 interleaved with step q's MFMAs. No barrier inside the k loop: the LDS rows are
+// read-only during the product. Lane (h, l32) holds A[row l32][16q + 8h + j] and
+// B[16q + 8h + j][col l32], j = 0..7 (the 32x32x16 operand maps).
 template <int NT, int RT>
-NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const float* __restrict__ Bp,
+NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const bf16x8* __restrict__ Bs,
                        f32x16 (&acc)[RT][2]) {
     constexpr int hp = NT * 32;
-    constexpr int nq = hp / 8;
+    constexpr int nq = hp / 16;
+    constexpr size_t PL = (size_t)nq * 2 * hp;  // 16-B entries per plane
+    constexpr size_t STEP = 2 * (size_t)hp;     // entries per k step
     const int lane = threadIdx.x & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
     const WaveCols<NT> wc(wv);
 #pragma unroll
@@ -46,44 +55,69 @@ NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const float* __restr
     // A wave without a second tile re-reads its first tile's B (same cache lines) so every load
     // is unconditional; its second-tile MFMAs are skipped by a scalar branch.
     const int t1 = wc.has1 ? wc.t1 : wc.t0;
-    const float4* B0 = reinterpret_cast<const float4*>(Bp) + (size_t)h * hp + wc.t0 * 32 + l32;
-    const float4* B1 = reinterpret_cast<const float4*>(Bp) + (size_t)h * hp + t1 * 32 + l32;
-    constexpr size_t STEP = 2 * (size_t)hp;  // float4 per 8-deep K step
-    constexpr size_t S1 = nq > 1 ? STEP : 0;
-    float4 p0 = B0[0], p1 = B0[S1];
-    float4 r0 = B1[0], r1 = B1[S1];
-    const float* arow = A + l32 * S_ + 4 * h;
-    float4 a[RT], an[RT];
+    const bf16x8* B0 = Bs + (size_t)h * hp + wc.t0 * 32 + l32;
+    const bf16x8* B1 = Bs + (size_t)h * hp + t1 * 32 + l32;
+    bf16x8 b0[3], b1[3];
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt) a[rt] = *reinterpret_cast<const float4*>(arow + rt * 32 * S_);
+    for (int p = 0; p < 3; ++p) {
+        b0[p] = B0[p * PL];
+        b1[p] = B1[p * PL];
+    }
+    const float* arow = A + l32 * S_ + 8 * h;
+    Split3 sa[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+        sa[rt] = split8(*reinterpret_cast<const float4*>(arow + rt * 32 * S_),
+                        *reinterpret_cast<const float4*>(arow + rt * 32 * S_ + 4));
 #pragma unroll
     for (int q = 0; q < nq; ++q) {
-        const float4 c0 = p0, c1 = r0;
-        p0 = p1;
-        r0 = r1;
-        // issue step q+2's B (L2) and step q+1's A (LDS) before step q's MFMAs; the scheduling
-        // fences keep the compiler from sinking the loads next to their uses
-        if (q + 2 < nq) {
-            p1 = B0[(q + 2) * STEP];
-            r1 = B1[(q + 2) * STEP];
+        bf16x8 nb0[3], nb1[3];
+        float4 an[RT][2];
+        if (q + 1 < nq) {
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                nb0[p] = B0[p * PL + (q + 1) * STEP];
+                nb1[p] = B1[p * PL + (q + 1) * STEP];
+            }
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) {
+                an[rt][0] = *reinterpret_cast<const float4*>(arow + rt * 32 * S_ + 16 * (q + 1));
+                an[rt][1] = *reinterpret_cast<const float4*>(arow + rt * 32 * S_ + 16 * (q + 1) + 4);
+            }
+        }
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+            acc[rt][0] = mfma_x6(sa[rt], b0, acc[rt][0]);
+            if (NT >= 8 || wc.has1) acc[rt][1] = mfma_x6(sa[rt], b1, acc[rt][1]);
         }
         if (q + 1 < nq) {
 #pragma unroll
-            for (int rt = 0; rt < RT; ++rt)
-                an[rt] = *reinterpret_cast<const float4*>(arow + rt * 32 * S_ + 8 * (q + 1));
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#define NAV_MF(S, C)                                                                     \
-    _Pragma("unroll") for (int rt = 0; rt < RT; ++rt) {                                 \
-        acc[rt][0] = mfma(a[rt].S, c0.S, acc[rt][0]);                                   \
-        if (NT >= 8 || wc.has1) acc[rt][1] = mfma(a[rt].S, c1.S, acc[rt][1]);           \
-    }
-        NAV_MF(x, 0) NAV_MF(y, 1) NAV_MF(z, 2) NAV_MF(w, 3)
-#undef NAV_MF
-        __builtin_amdgcn_sched_barrier(0);
+            for (int rt = 0; rt < RT; ++rt) sa[rt] = split8(an[rt][0], an[rt][1]);
+#if NAV_GEMM_INTERLEAVE
+            // the split VALU of step q+1 between step q's MFMAs
 #pragma unroll
-        for (int rt = 0; rt < RT; ++rt) a[rt] = an[rt];
+            for (int k = 0; k < 12 * RT; ++k) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+            }
+#endif
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                b0[p] = nb0[p];
+                b1[p] = nb1[p];
+            }
+        }
     }
+}
+
+// the split B images of hidden layer L (1 .. n_hidden-1): forward (B[k][n] = W_L[n][k]) and
+// backward (B[k][n] = W_L[k][n])
+NAV_DEV const bf16x8* img_fwd(const MlpDev& net, int L) {
+    return reinterpret_cast<const bf16x8*>(net.packed + (int64_t)(L - 1) * 2 * split_image_floats(net.hp));
+}
+NAV_DEV const bf16x8* img_bwd(const MlpDev& net, int L) {
+    return reinterpret_cast<const bf16x8*>(net.packed + (int64_t)(L - 1) * 2 * split_image_floats(net.hp) +
+                                           split_image_floats(net.hp));
 }
 
 enum { IN_F32 = 0, IN_BASELINE = 1 };
@@ -482,7 +516,7 @@ NAV_DEV void fwd_net(const MlpDev& net, float* act, const float* xin, float* red
         const float* bL = net.params + net.b_off[L];
         const float bb0 = wc.has0 ? bL[wc.t0 * 32 + l32] : 0.f;
         const float bb1 = wc.has1 ? bL[wc.t1 * 32 + l32] : 0.f;
-        gemm_cols<NT, RT>(act, SS, net.packed + (int64_t)(L - 1) * 2 * hp * hp, acc);
+        gemm_cols<NT, RT>(act, SS, img_fwd(net, L), acc);
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             if (!(j == 0 ? wc.has0 : wc.has1)) continue;
@@ -888,8 +922,7 @@ NAV_DEV void bwd_net(const MlpDev& net, float* act, const float* dys, const floa
         f32x16 acc[RT][2];
         uint32_t mbits[RT][2];
         load_mask_bits<NT, RT>(masks + (size_t)(L - 1) * mstride, rt0, mbits);
-        gemm_cols<NT, RT>(act, SS,
-                          net.packed + (int64_t)(L - 1) * 2 * hp * hp + (int64_t)hp * hp, acc);
+        gemm_cols<NT, RT>(act, SS, img_bwd(net, L), acc);
         NAV_MARK(mk + 3);
         __syncthreads();
         mask_and_store<NT, RT>(acc, mbits, act, SS);
@@ -1395,7 +1428,7 @@ int64_t nav_mlp_param_count(int32_t d_in, int32_t d_out, int32_t hp, int32_t n_h
 
 int64_t nav_mlp_packed_count(int32_t hp, int32_t n_hidden) {
     if (hp < 32 || hp > 256 || (hp & 31) || n_hidden < 1) return NAV_EINVAL;
-    return (int64_t)(n_hidden - 1) * 2 * hp * hp;
+    return (int64_t)(n_hidden - 1) * 2 * split_image_floats(hp);
 }
 
 int nav_mlp_layer_offsets(const nav_mlp* net, int32_t layer, int64_t* w_off, int64_t* b_off) {
