@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define NAV_ABI_VERSION 6
+#define NAV_ABI_VERSION 7
 #define NAV_EINVAL (-100000)
 
 #define NAV_WORLD_CELLS 100 /* field = float32 [100][100][2] (speed, angle), x-major: cell cx*100+cy

@@ -13,7 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # NAV_LIB: load another build of the same ABI instead (A/B timing of kernel variants only)
 LIB_PATH = os.environ.get("NAV_LIB") or os.path.join(HERE, "libnavenv.so")
 NAV_EINVAL = -100000
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 _dp = C.POINTER(C.c_double)
 _vp = C.c_void_p
