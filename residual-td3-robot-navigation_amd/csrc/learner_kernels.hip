@@ -471,38 +471,40 @@ NAV_DEV void wgrad_rows_mfma(const WgradArgs& a, int y, int n0, int k0, int64_t 
         }
     };
     if (r_lo >= r_hi || NAV_WG_EXP == 4) return;  // 4: tuning probe, no row loop
-    // ping-pong operand buffers (a loop-carried copy would cost 64 v_mov per tile, and the VALU
-    // shares the SIMD's issue with the f32 MFMA): tile t uses buffer t & 1 while the operand
-    // MFMAs of tile t + 1 fill the other
-    f32x16 PA[2], QA[2], PB[2], QB[2];
+    // per 32-row tile: the operand MFMAs, their ReLU epilogue, then the tile's two 16-deep k steps
+    // of the bf16 product (the partner wave on the SIMD keeps the matrix pipe busy while this one
+    // waits for its operand MFMAs; double-buffering the operand tiles would not fit the 256
+    // registers of two waves per SIMD next to the split fragments). The raw loads run two tiles
+    // ahead.
     Raw cur = load(r_lo);
-    issue(r_lo, cur, PA, QA);
     Raw nxt = cur;
     if (r_lo + 32 < r_hi) nxt = load(r_lo + 32);
-    finish(cur, PA, QA);
-    auto step = [&](int64_t rt, f32x16 (&P)[2], f32x16 (&Q)[2], f32x16 (&Pn)[2],
-                    f32x16 (&Qn)[2]) {
-        const bool more = rt + 32 < r_hi;
-        // the loads of tile t + 2 are issued first and fenced there, so the wait for tile t + 1's
-        // raw data (loaded a step ago) below leaves them in flight (vmcnt counts in order)
+    for (int64_t rt = r_lo; rt < r_hi; rt += 32) {
         Raw nn = nxt;
         if (rt + 64 < r_hi) nn = load(rt + 64);
-        __builtin_amdgcn_sched_barrier(0);
-        // the next tile's operand MFMAs next: done long before finish() reads them
-        if (more) issue(rt + 32, nxt, Pn, Qn);
+        f32x16 P[2], Q[2];
+        issue(rt, cur, P, Q);
+        finish(cur, P, Q);
+        // registers 8s .. 8s+7 of the C-layout operands are k step s (rows 16s + 8(j>>2) + 4h +
+        // (j&3), the same for P and Q), each split three ways (mlp_common.h) right before its six
+        // partial products
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-            acc[0][0] = mfma(P[0][e], Q[0][e], acc[0][0]);
-            acc[0][1] = mfma(P[0][e], Q[1][e], acc[0][1]);
-            acc[1][0] = mfma(P[1][e], Q[0][e], acc[1][0]);
-            acc[1][1] = mfma(P[1][e], Q[1][e], acc[1][1]);
+        for (int s2 = 0; s2 < 2; ++s2) {
+            Split3 sp[2], sq[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                sp[i] = split8(make_float4(P[i][8 * s2], P[i][8 * s2 + 1], P[i][8 * s2 + 2], P[i][8 * s2 + 3]),
+                               make_float4(P[i][8 * s2 + 4], P[i][8 * s2 + 5], P[i][8 * s2 + 6], P[i][8 * s2 + 7]));
+                sq[i] = split8(make_float4(Q[i][8 * s2], Q[i][8 * s2 + 1], Q[i][8 * s2 + 2], Q[i][8 * s2 + 3]),
+                               make_float4(Q[i][8 * s2 + 4], Q[i][8 * s2 + 5], Q[i][8 * s2 + 6], Q[i][8 * s2 + 7]));
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) acc[i][j] = mfma_x6s(sp[i], sq[j], acc[i][j]);
         }
-        if (more) finish(nxt, Pn, Qn);
+        cur = nxt;
         nxt = nn;
-    };
-    for (int64_t rt = r_lo; rt < r_hi; rt += 64) {
-        step(rt, PA, QA, PB, QB);
-        if (rt + 32 < r_hi) step(rt + 32, PB, QB, PA, QA);
     }
 }
 

@@ -149,6 +149,16 @@ NAV_DEV f32x16 mfma_x6(const Split3& a, const bf16x8 (&b)[3], f32x16 c) {
     return mfma16(a.h, b[0], c);
 }
 
+// the same with both operands split in registers
+NAV_DEV f32x16 mfma_x6s(const Split3& a, const Split3& b, f32x16 c) {
+    c = mfma16(a.m, b.m, c);
+    c = mfma16(a.l, b.h, c);
+    c = mfma16(a.h, b.l, c);
+    c = mfma16(a.m, b.h, c);
+    c = mfma16(a.h, b.m, c);
+    return mfma16(a.h, b.h, c);
+}
+
 // Split B-operand image of one hp x hp matrix B[k][n] (k = the product's K): entry
 // (plane p, k step q = k / 16, lane half h = (k / 8) & 1, column n) holds the 8 bf16 of plane p
 // of B[16q + 8h + j][n], j = 0..7 — one 16-B load per lane per plane and k step, 32 lanes of a
