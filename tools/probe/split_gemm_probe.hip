@@ -85,8 +85,17 @@ __device__ __forceinline__ Split3 split8(float4 x0, float4 x1) {
 __device__ __forceinline__ f32x16 mf16(bf16x8 a, bf16x8 b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
+__device__ __forceinline__ f32x16 mfma_x6b(const Split3& a, const bf16x8 (&b)[3], f32x16 c) {
+    c = mf16(a.m, b[1], c);
+    c = mf16(a.l, b[0], c);
+    c = mf16(a.h, b[2], c);
+    c = mf16(a.m, b[0], c);
+    c = mf16(a.h, b[1], c);
+    return mf16(a.h, b[0], c);
+}
 // B image: [plane 3][q = K/16][h 2][col HP] x 8 bf16 (16 B): lane (h, l32) of tile t reads entry
 // (plane, q, h, t*32 + l32) = B[k = 16q + 8h + j][col], j = 0..7
+template <bool SPLIT = true, bool BLOAD = true>
 __device__ __forceinline__ void gemm_x6(const float* A, const bf16x8* Bs, f32x16 (&acc)[2][2]) {
     constexpr int nq = HP / 16;
     constexpr size_t PL = (size_t)nq * 2 * HP;  // entries per plane
@@ -112,8 +121,8 @@ __device__ __forceinline__ void gemm_x6(const float* A, const bf16x8* Bs, f32x16
     for (int q = 0; q < nq; ++q) {
         if (q + 1 < nq) {
             for (int p = 0; p < 3; ++p) {
-                nb0[p] = B0[p * PL + (q + 1) * STEP];
-                nb1[p] = B1[p * PL + (q + 1) * STEP];
+                nb0[p] = BLOAD ? B0[p * PL + (q + 1) * STEP] : b0[(p + 1) % 3];
+                nb1[p] = BLOAD ? B1[p * PL + (q + 1) * STEP] : b1[(p + 1) % 3];
             }
             for (int rt = 0; rt < 2; ++rt) {
                 an[rt][0] = *reinterpret_cast<const float4*>(arow + rt * 32 * SS + 16 * (q + 1));
@@ -122,7 +131,14 @@ __device__ __forceinline__ void gemm_x6(const float* A, const bf16x8* Bs, f32x16
         }
 #pragma unroll
         for (int rt = 0; rt < 2; ++rt) {
-            const Split3 s = split8(a[rt][0], a[rt][1]);
+            Split3 s;
+            if (SPLIT) {
+                s = split8(a[rt][0], a[rt][1]);
+            } else {
+                s.h = __builtin_bit_cast(bf16x8, a[rt][0]);
+                s.m = __builtin_bit_cast(bf16x8, a[rt][1]);
+                s.l = s.h;
+            }
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
                 const bf16x8* b = j == 0 ? b0 : b1;
@@ -211,6 +227,66 @@ __device__ __forceinline__ void gemm_x6i(const float* A, const bf16x8* Bs, f32x1
                 b1[p] = nb1[p];
             }
             for (int rt = 0; rt < 2; ++rt) s[rt] = sn[rt];
+        }
+    }
+}
+
+// x6 with explicit scheduling: the next step's loads fenced at the top of the step, then the
+// MFMAs of this step interleaved (IL) with the split of the next step, or all MFMAs then the split
+template <bool IL>
+__device__ __forceinline__ void gemm_x6f(const float* A, const bf16x8* Bs, f32x16 (&acc)[2][2]) {
+    constexpr int nq = HP / 16;
+    constexpr size_t PL = (size_t)nq * 2 * HP;
+    const int lane = threadIdx.x & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
+    for (int rt = 0; rt < 2; ++rt)
+        for (int j = 0; j < 2; ++j)
+            for (int i = 0; i < 16; ++i) acc[rt][j][i] = 0.f;
+    const bf16x8* B0 = Bs + (size_t)h * HP + wv * 32 + l32;
+    const bf16x8* B1 = Bs + (size_t)h * HP + (wv + 4) * 32 + l32;
+    constexpr size_t STEP = 2 * (size_t)HP;
+    bf16x8 b0[3], b1[3];
+    for (int p = 0; p < 3; ++p) {
+        b0[p] = B0[p * PL];
+        b1[p] = B1[p * PL];
+    }
+    const float* arow = A + l32 * SS + 8 * h;
+    Split3 s[2];
+    for (int rt = 0; rt < 2; ++rt)
+        s[rt] = split8(*reinterpret_cast<const float4*>(arow + rt * 32 * SS),
+                       *reinterpret_cast<const float4*>(arow + rt * 32 * SS + 4));
+#pragma unroll
+    for (int q = 0; q < nq; ++q) {
+        bf16x8 nb0[3], nb1[3];
+        float4 an[2][2];
+        const int qn = q + 1 < nq ? q + 1 : q;
+        for (int p = 0; p < 3; ++p) {
+            nb0[p] = B0[p * PL + qn * STEP];
+            nb1[p] = B1[p * PL + qn * STEP];
+        }
+        for (int rt = 0; rt < 2; ++rt) {
+            an[rt][0] = *reinterpret_cast<const float4*>(arow + rt * 32 * SS + 16 * qn);
+            an[rt][1] = *reinterpret_cast<const float4*>(arow + rt * 32 * SS + 16 * qn + 4);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[rt][j] = mfma_x6b(s[rt], j == 0 ? b0 : b1, acc[rt][j]);
+        Split3 sn[2];
+        for (int rt = 0; rt < 2; ++rt) sn[rt] = split8(an[rt][0], an[rt][1]);
+        if (IL) {
+#pragma unroll
+            for (int k = 0; k < 22; ++k) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        for (int rt = 0; rt < 2; ++rt) s[rt] = sn[rt];
+        for (int p = 0; p < 3; ++p) {
+            b0[p] = nb0[p];
+            b1[p] = nb1[p];
         }
     }
 }
@@ -336,8 +412,18 @@ __global__ __launch_bounds__(kBlock, 1) void k_probe(const float* rows, const fl
             gemm_f32(act, Bf, acc);
         else if (MODE == 1)
             gemm_x6(act, Bs, acc);
-        else
+        else if (MODE == 2)
             gemm_x6i(act, Bs, acc);
+        else if (MODE == 4)
+            gemm_x6<false, true>(act, Bs, acc);
+        else if (MODE == 5)
+            gemm_x6<true, false>(act, Bs, acc);
+        else if (MODE == 7)
+            gemm_x6f<false>(act, Bs, acc);
+        else if (MODE == 8)
+            gemm_x6f<true>(act, Bs, acc);
+        else
+            gemm_x6<false, false>(act, Bs, acc);
         __syncthreads();
         store_rows(acc, act);
         __syncthreads();
@@ -413,11 +499,11 @@ int main() {
             }
         ref.swap(nxt);
     }
-    for (int mode = 0; mode < 4; ++mode) {
-        auto k = mode == 0 ? k_probe<0> : mode == 1 ? k_probe<1> : k_probe<2>;
+    for (int mode = 0; mode < 9; ++mode) {
+        auto k = mode == 0 ? k_probe<0> : mode == 1 ? k_probe<1> : mode == 2 ? k_probe<2> : mode == 4 ? k_probe<4> : mode == 5 ? k_probe<5> : mode == 6 ? k_probe<6> : mode == 7 ? k_probe<7> : k_probe<8>;
         const size_t lds_pl = (size_t)3 * TM * PS * 2;
         auto launch = [&]() {
-            if (mode < 3)
+            if (mode != 3)
                 hipLaunchKernelGGL(k, dim3(blocks), dim3(kBlock), lds, 0, d_rows, d_Bf, d_Bs, d_out);
             else
                 hipLaunchKernelGGL(k_probe_pl, dim3(blocks), dim3(512), lds_pl, 0, d_rows, d_Bs, d_out);
@@ -450,7 +536,7 @@ int main() {
         }
         printf("{\"mode\": \"%s\", \"us\": %.1f, \"TFs\": %.1f, \"max_abs_err\": %.3e, "
                "\"max_ref\": %.3e, \"rel_rms_err\": %.3e}\n",
-               mode == 0 ? "f32" : mode == 1 ? "bf16x6" : mode == 2 ? "bf16x6_interleaved" : "bf16x6_lds_planes_8w", us, flop / us / 1e6, maxe, maxr, sqrt(sum2 / ref2));
+               mode == 0 ? "f32" : mode == 1 ? "bf16x6" : mode == 2 ? "bf16x6_interleaved" : mode == 3 ? "bf16x6_lds_planes_8w" : mode == 4 ? "x6_nosplit" : mode == 5 ? "x6_noBload" : mode == 6 ? "x6_nosplit_noBload" : mode == 7 ? "x6_fenced" : "x6_fenced_interleaved", us, flop / us / 1e6, maxe, maxr, sqrt(sum2 / ref2));
     }
     return 0;
 }
