@@ -33,9 +33,14 @@ import torch  # noqa: E402
 
 from nav import prof  # noqa: E402
 
+EVENT_SAMPLE = 8             # timed region: event pairs around 1 launch in 8 of the dominant kernel
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP32_MFMA_PEAK_TFS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
 FP64_VALU_PEAK_TFS = 78.6    # MI355X spec FP64 vector
+BF16_MFMA_PEAK_TFS = 2516.6  # MI355X_MICROARCH.md: 1024 FLOP/clk/SIMD x 1024 SIMDs x 2.4 GHz (dense)
+# hidden x hidden GEMM passes per launch of each row kernel (network forwards + row backwards):
+# these run on the bf16 matrix cores as six partial products of the exact 3-way split
+HIDDEN_PASSES = {"critic_rows": 7, "actor_rows": 4, "act": 1, "act_tick": 1}
 # HBM bytes per launch from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this same
 # command (tools/pmc_traffic.py, gfx950 correction applied); bench regions -> kernel names
 PMC_TRAFFIC = os.path.join(HERE, "profiles", "pmc_traffic.json")
@@ -320,7 +325,11 @@ def main():
     dominant = max(breakdown, key=lambda k: breakdown[k]["total_ms"])
 
     # ---- timed region
-    timer = prof.KernelTimer([] if args.no_timed_events else [dominant])
+    # the dominant kernel's launches are bracketed by HIP event pairs on its launch stream, one
+    # launch in EVENT_SAMPLE (each record stalls the stream a few us; bracketing every launch
+    # cost 2.6 % of the step, profiles/r03c_bench.json value vs timed_long)
+    timer = prof.KernelTimer([] if args.no_timed_events else [dominant],
+                             sample_every=EVENT_SAMPLE)
     barrier(ws)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -361,12 +370,24 @@ def main():
         else:
             tf = ach / 1e12
             peak = FP64_VALU_PEAK_TFS if dominant == "demo_reward" else FP32_MFMA_PEAK_TFS
+            hp = (args.hidden + 31) // 32 * 32
+            rows = args.envs if dominant in ("act", "act_tick") else rank_batch
+            hidden = (HIDDEN_PASSES.get(dominant, 0) * (args.layers - 1) * 2.0 * rows * hp * hp)
+            bf16 = 6.0 * hidden / (d["avg_us"] * 1e-6) / 1e12
             roof = {"bound": "valu" if dominant == "demo_reward" else "mfma",
                     "kernel": dominant, "achieved": round(tf, 2), "peak": peak,
+                    "peak_note": "f32 MFMA peak: the path computes in f32 (its hidden x hidden "
+                                 "GEMMs on the bf16 matrix cores as six partial products of an "
+                                 "exact 3-way bf16 split, f32 accuracy); achieved counts f32 FLOPs",
+                    "bf16_pipe": {"hidden_gemm_flop_per_launch": hidden,
+                                  "bf16_flop_per_launch": 6.0 * hidden,
+                                  "achieved_TFs": round(bf16, 1), "peak_TFs": BF16_MFMA_PEAK_TFS,
+                                  "frac": round(bf16 / BF16_MFMA_PEAK_TFS, 4)},
                     "unit": "TFLOP/s", "frac": round(tf / peak, 4), "traffic": traffic,
                     "traffic_source": traffic_src,
                     "flop_per_launch": d["work_per_launch"], "avg_us": round(d["avg_us"], 2),
-                    "launches": d["launches"]}
+                    "launches_timed": d["launches"],
+                    "launches": timer.seen[dominant], "event_sample": EVENT_SAMPLE}
         forms = None if ws > 1 else tick_forms(tr)
         sweep = None if (args.no_sweep or ws > 1) else step_kernel_sweep(
             tr.field, [65536, 1 << 20, 1 << 22, 1 << 24])

@@ -11,4 +11,4 @@ if [ -n "$FIRST" ]; then
   if [ "$rc" -ne 0 ] && [ "$rc" -ne 1 ]; then exit "$rc"; fi
 fi
 exec_steps="$*"
-[ -n "$exec_steps" ] && bash tools/gpu_check.sh $exec_steps
+if [ -n "$exec_steps" ]; then bash tools/gpu_check.sh $exec_steps; fi
