@@ -51,7 +51,8 @@ struct WgradArgs {
 #define NAV_WG_TOTAL 256
 #endif
 #ifndef NAV_WG_EXP
-#define NAV_WG_EXP 0  // tuning probes: 1 = operands without VALU math, 2 = without LDS reads
+#define NAV_WG_EXP 0  // tuning probes: 1 = operands without VALU math, 2 = without LDS reads,
+                      // 4 = no row loop, 5 = no global loads, 6 = no operand split
 #endif
 constexpr int WG_WAVES = NAV_WG_WAVES;
 constexpr int WG_THREADS = WG_WAVES * 64;
@@ -493,6 +494,13 @@ NAV_DEV void wgrad_rows_mfma(const WgradArgs& a, int y, int n0, int k0, int64_t 
             Split3 sp[2], sq[2];
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
+                if (NAV_WG_EXP == 6) {  // tuning probe: operands without the split
+                    sp[i].h = __builtin_bit_cast(bf16x8, make_float4(P[i][8 * s2], P[i][8 * s2 + 1], P[i][8 * s2 + 2], P[i][8 * s2 + 3]));
+                    sp[i].m = sp[i].l = sp[i].h;
+                    sq[i].h = __builtin_bit_cast(bf16x8, make_float4(Q[i][8 * s2], Q[i][8 * s2 + 1], Q[i][8 * s2 + 2], Q[i][8 * s2 + 3]));
+                    sq[i].m = sq[i].l = sq[i].h;
+                    continue;
+                }
                 sp[i] = split8(make_float4(P[i][8 * s2], P[i][8 * s2 + 1], P[i][8 * s2 + 2], P[i][8 * s2 + 3]),
                                make_float4(P[i][8 * s2 + 4], P[i][8 * s2 + 5], P[i][8 * s2 + 6], P[i][8 * s2 + 7]));
                 sq[i] = split8(make_float4(Q[i][8 * s2], Q[i][8 * s2 + 1], Q[i][8 * s2 + 2], Q[i][8 * s2 + 3]),
