@@ -398,6 +398,18 @@ int nav_grad_reduce_adam(const nav_mlp* nets, int32_t n_nets, const float* const
                          float* const* grads, float* const* m, float* const* v, float beta1,
                          float beta2, float eps, const float* step_size, const float* bc2_sqrt,
                          void* stream);
+/* nav_grad_reduce_adam plus the soft updates of robot.py:283-285 in the same launch: each net's
+ * target net_targets[i] <- target*(1-tau) + p_new*tau right after p's Adam step (same thread), and
+ * n_pairs (<= 4) further (target, source) pairs whose sources are final (the critics on a policy
+ * epoch) by extra blocks; bit-identical to nav_grad_reduce_adam followed by nav_polyak_multi. */
+int nav_grad_reduce_adam_polyak(const nav_mlp* nets, int32_t n_nets,
+                                const float* const* hidden_slabs, int32_t splits,
+                                const float* const* edge_slabs, int64_t edge_blocks,
+                                float* const* grads, float* const* m, float* const* v,
+                                float beta1, float beta2, float eps, const float* step_size,
+                                const float* bc2_sqrt, const nav_mlp* net_targets,
+                                const nav_mlp* targets, const nav_mlp* sources, int32_t n_pairs,
+                                float tau, void* stream);
 /* nav_grad_reduce of 1 or 2 same-shape networks in one launch (the twin critics' gradients into
  * one contiguous bucket for the shared-policy all-reduce). */
 int nav_grad_reduce_multi(const nav_mlp* nets, int32_t n_nets, const float* const* hidden_slabs,

@@ -632,6 +632,20 @@ NAV_DEV float adam1(float& p, float g, float& m, float& v, float b1w, float b2, 
 // fixed xor tree adds the lanes). Deterministic: the same order on every run. With ADAM the
 // finished gradient goes straight into torch's Adam update (robot.py:236-239) of the parameter
 // it belongs to and the packed MFMA images are refreshed; up to 2 networks per launch.
+// robot.py:293-310 soft update of up to 4 (target, source) pairs in one launch
+struct PolyPair {
+    float4* t;
+    const float4* s;
+    int64_t n4;
+    PackInfo pk;
+};
+struct PolyArgs {
+    PolyPair q[4];
+    int n;
+    int64_t total4;
+    float omt, tau;
+};
+
 struct RedNet {
     MlpDev net;
     const float4* hs;
@@ -643,6 +657,8 @@ struct RedNet {
     float step_size, bc2s;
     PackInfo pk;
     int nbh, nbe;
+    float4* tgt;   // nullable: this net's target, soft-updated from the new parameters
+    PackInfo tpk;
 };
 
 struct RedArgs {
@@ -650,6 +666,10 @@ struct RedArgs {
     int splits;
     int64_t nblk;
     float b1w, b2, omb2, eps;
+    // the soft updates of the launch (robot.py:283-285): the nets' own targets in red_out, the
+    // extra (target, source) pairs by the blocks past the reduce blocks
+    PolyArgs poly;
+    int red_blocks;
 };
 
 template <bool ADAM>
@@ -665,6 +685,32 @@ NAV_DEV void red_out(const RedArgs& a, const RedNet& rn, int64_t flat4, float4 g
     rn.m[flat4] = mm;
     rn.v[flat4] = vv;
     if (rn.pk.packed) repack(rn.pk, flat4 * 4, pp);
+    if (rn.tgt) {  // robot.py:309 on the parameter just stepped (k_polyak's expression)
+        float4 t = rn.tgt[flat4];
+        t.x = t.x * a.poly.omt + pp.x * a.poly.tau;
+        t.y = t.y * a.poly.omt + pp.y * a.poly.tau;
+        t.z = t.z * a.poly.omt + pp.z * a.poly.tau;
+        t.w = t.w * a.poly.omt + pp.w * a.poly.tau;
+        rn.tgt[flat4] = t;
+        if (rn.tpk.packed) repack(rn.tpk, flat4 * 4, t);
+    }
+}
+
+// soft update of element i of the pairs' concatenation (k_polyak_multi's body)
+NAV_DEV void polyak_elem(const PolyArgs& a, int64_t i) {
+    int64_t j = i;
+    int k = 0;
+    while (k < a.n - 1 && j >= a.q[k].n4) j -= a.q[k++].n4;
+    const PolyPair& q = a.q[k];
+    float4 t = q.t[j];
+    const float4 s = q.s[j];
+    // robot.py:309 target*(1-tau) + source*tau (two products, one sum)
+    t.x = t.x * a.omt + s.x * a.tau;
+    t.y = t.y * a.omt + s.y * a.tau;
+    t.z = t.z * a.omt + s.z * a.tau;
+    t.w = t.w * a.omt + s.w * a.tau;
+    q.t[j] = t;
+    if (q.pk.packed) repack(q.pk, j * 4, t);
 }
 
 template <bool ADAM>
@@ -672,6 +718,12 @@ __global__ __launch_bounds__(kBlock) void k_grad_reduce(RedArgs a) {
     __shared__ float4 part[4][64];
     const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
     int b = blockIdx.x;
+    if (b >= a.red_blocks) {  // the extra soft-update pairs (block-uniform)
+        for (int64_t i = (int64_t)(b - a.red_blocks) * kBlock + threadIdx.x; i < a.poly.total4;
+             i += (int64_t)(gridDim.x - a.red_blocks) * kBlock)
+            polyak_elem(a.poly, i);
+        return;
+    }
     const bool second = b >= a.n[0].nbh + a.n[0].nbe;
     const RedNet& rn = second ? a.n[1] : a.n[0];
     if (second) b -= a.n[0].nbh + a.n[0].nbe;
@@ -700,37 +752,43 @@ __global__ __launch_bounds__(kBlock) void k_grad_reduce(RedArgs a) {
         red_out<ADAM>(a, rn, net.w_off[L] / 4 + i % per, r);
         return;
     }
+    // edge entries: one block = 16 float4 columns x 16 groups of edge blocks; thread (column
+    // t & 15, group t >> 4) sums blocks g, g + 16, g + 32, ... in order (a wave instruction reads
+    // 4 block rows x 256 contiguous bytes), then the 16 group sums meet in group order in LDS
     const int64_t e4 = edge_count(net) / 4;
-    const int64_t o = (int64_t)(b - rn.nbh) * 4 + g;
-    if (o >= e4) return;  // wave-uniform
+    const int ec = threadIdx.x & 15, eg = threadIdx.x >> 4;
+    const int64_t o = (int64_t)(b - rn.nbh) * 16 + ec;
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int64_t k = c; k < a.nblk; k += 64) {
-        const float4 v = rn.es[k * e4 + o];
-        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    if (o < e4) {
+        const float4* col = rn.es + o;
+        int64_t k = eg;
+#pragma unroll 1
+        for (; k + 48 < a.nblk; k += 64) {
+            const float4 v0 = col[k * e4], v1 = col[(k + 16) * e4], v2 = col[(k + 32) * e4],
+                         v3 = col[(k + 48) * e4];
+            s.x += v0.x; s.y += v0.y; s.z += v0.z; s.w += v0.w;
+            s.x += v1.x; s.y += v1.y; s.z += v1.z; s.w += v1.w;
+            s.x += v2.x; s.y += v2.y; s.z += v2.z; s.w += v2.w;
+            s.x += v3.x; s.y += v3.y; s.z += v3.z; s.w += v3.w;
+        }
+        for (; k < a.nblk; k += 16) {
+            const float4 v = col[k * e4];
+            s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+        }
     }
+    float4* gp = &part[0][0];  // [16 groups][16 columns]
+    gp[eg * 16 + ec] = s;
+    __syncthreads();
+    if (eg != 0 || o >= e4) return;
+    float4 r = gp[ec];
 #pragma unroll
-    for (int d = 32; d > 0; d >>= 1) {
-        s.x += __shfl_xor(s.x, d, 64);
-        s.y += __shfl_xor(s.y, d, 64);
-        s.z += __shfl_xor(s.z, d, 64);
-        s.w += __shfl_xor(s.w, d, 64);
+    for (int q = 1; q < 16; ++q) {
+        const float4 v = gp[q * 16 + ec];
+        r.x += v.x; r.y += v.y; r.z += v.z; r.w += v.w;
     }
-    if (c == 0) red_out<ADAM>(a, rn, edge_to_flat(net, 4 * o) / 4, s);
+    red_out<ADAM>(a, rn, edge_to_flat(net, 4 * o) / 4, r);
 }
 
-// robot.py:293-310 soft update of up to 4 (target, source) pairs in one launch
-struct PolyPair {
-    float4* t;
-    const float4* s;
-    int64_t n4;
-    PackInfo pk;
-};
-struct PolyArgs {
-    PolyPair q[4];
-    int n;
-    int64_t total4;
-    float omt, tau;
-};
 
 __global__ __launch_bounds__(kBlock) void k_adam(float4* __restrict__ p,
                                                  const float4* __restrict__ g, float4* m,
@@ -804,21 +862,8 @@ __global__ __launch_bounds__(kBlock) void k_polyak(float4* __restrict__ t,
 
 __global__ __launch_bounds__(kBlock) void k_polyak_multi(PolyArgs a) {
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < a.total4;
-         i += (int64_t)gridDim.x * kBlock) {
-        int64_t j = i;
-        int k = 0;
-        while (k < a.n - 1 && j >= a.q[k].n4) j -= a.q[k++].n4;
-        const PolyPair& q = a.q[k];
-        float4 t = q.t[j];
-        const float4 s = q.s[j];
-        // robot.py:309 target*(1-tau) + source*tau (two products, one sum)
-        t.x = t.x * a.omt + s.x * a.tau;
-        t.y = t.y * a.omt + s.y * a.tau;
-        t.z = t.z * a.omt + s.z * a.tau;
-        t.w = t.w * a.omt + s.w * a.tau;
-        q.t[j] = t;
-        if (q.pk.packed) repack(q.pk, j * 4, t);
-    }
+         i += (int64_t)gridDim.x * kBlock)
+        polyak_elem(a, i);
 }
 
 __global__ __launch_bounds__(kBlock) void k_pack(const float4* __restrict__ p, int64_t n4,
@@ -885,7 +930,7 @@ bool red_net(const nav_mlp* net, const float* hs, int splits, const float* es, f
     rn->es = reinterpret_cast<const float4*>(es);
     rn->grad = reinterpret_cast<float4*>(grad);
     rn->nbh = (int)((hidden_w_count(rn->net) / 4 + 63) / 64);
-    rn->nbe = (int)((edge_count(rn->net) / 4 + 3) / 4);
+    rn->nbe = (int)((edge_count(rn->net) / 4 + 15) / 16);
     return true;
 }
 
@@ -960,8 +1005,9 @@ int nav_grad_reduce(const nav_mlp* net, const float* hidden_slabs, int32_t split
         return NAV_EINVAL;
     a.splits = splits;
     a.nblk = edge_blocks;
-    hipLaunchKernelGGL(k_grad_reduce<false>, dim3((unsigned)(a.n[0].nbh + a.n[0].nbe)),
-                       dim3(kBlock), 0, S(stream), a);
+    a.red_blocks = a.n[0].nbh + a.n[0].nbe;
+    hipLaunchKernelGGL(k_grad_reduce<false>, dim3((unsigned)a.red_blocks), dim3(kBlock), 0,
+                       S(stream), a);
     NAV_CHECK_LAUNCH();
     return 0;
 }
@@ -984,6 +1030,7 @@ int nav_grad_reduce_multi(const nav_mlp* nets, int32_t n_nets, const float* cons
     }
     a.splits = splits;
     a.nblk = edge_blocks;
+    a.red_blocks = blocks;
     hipLaunchKernelGGL(k_grad_reduce<false>, dim3((unsigned)blocks), dim3(kBlock), 0, S(stream),
                        a);
     NAV_CHECK_LAUNCH();
@@ -1023,14 +1070,16 @@ int nav_adam_multi(const nav_mlp* nets, int32_t n_nets, const float* const* grad
     return 0;
 }
 
-int nav_grad_reduce_adam(const nav_mlp* nets, int32_t n_nets, const float* const* hidden_slabs,
-                         int32_t splits, const float* const* edge_slabs, int64_t edge_blocks,
-                         float* const* grads, float* const* m, float* const* v, float beta1,
-                         float beta2, float eps, const float* step_size, const float* bc2_sqrt,
-                         void* stream) {
+static int grad_reduce_adam_impl(const nav_mlp* nets, int32_t n_nets, const float* const* hidden_slabs,
+                          int32_t splits, const float* const* edge_slabs, int64_t edge_blocks,
+                          float* const* grads, float* const* m, float* const* v, float beta1,
+                          float beta2, float eps, const float* step_size, const float* bc2_sqrt,
+                          const nav_mlp* net_targets, const nav_mlp* targets,
+                          const nav_mlp* sources, int32_t n_pairs, float tau, void* stream) {
     RedArgs a{};
     if (!nets || n_nets < 1 || n_nets > 2 || !hidden_slabs || !edge_slabs || edge_blocks < 1 ||
-        splits < 0 || !m || !v || !step_size || !bc2_sqrt)
+        splits < 0 || !m || !v || !step_size || !bc2_sqrt || n_pairs < 0 || n_pairs > 4 ||
+        (n_pairs && (!targets || !sources)))
         return NAV_EINVAL;
     int blocks = 0;
     for (int i = 0; i < n_nets; ++i) {
@@ -1045,8 +1094,33 @@ int nav_grad_reduce_adam(const nav_mlp* nets, int32_t n_nets, const float* const
         rn.step_size = step_size[i];
         rn.bc2s = bc2_sqrt[i];
         rn.pk = pack_info(rn.net, nets[i].packed);
+        if (net_targets) {
+            MlpDev dt;
+            if (!make_dev(&net_targets[i], &dt) || dt.count != rn.net.count ||
+                dt.hp != rn.net.hp || dt.n_hidden != rn.net.n_hidden)
+                return NAV_EINVAL;
+            rn.tgt = reinterpret_cast<float4*>(net_targets[i].params);
+            rn.tpk = pack_info(dt, net_targets[i].packed);
+        }
         blocks += rn.nbh + rn.nbe;
     }
+    for (int i = 0; i < n_pairs; ++i) {
+        MlpDev dt, ds;
+        if (!make_dev(&targets[i], &dt) || !make_dev(&sources[i], &ds) || dt.count != ds.count ||
+            dt.hp != ds.hp || dt.n_hidden != ds.n_hidden)
+            return NAV_EINVAL;
+        a.poly.q[i].t = reinterpret_cast<float4*>(targets[i].params);
+        a.poly.q[i].s = reinterpret_cast<const float4*>(sources[i].params);
+        a.poly.q[i].n4 = dt.count / 4;
+        a.poly.q[i].pk = pack_info(dt, targets[i].packed);
+        a.poly.total4 += a.poly.q[i].n4;
+    }
+    a.poly.n = n_pairs;
+    a.poly.omt = 1.0f - tau;
+    a.poly.tau = tau;
+    a.red_blocks = blocks;
+    if (n_pairs) blocks += (int)((a.poly.total4 + kBlock - 1) / kBlock < 256
+                                     ? (a.poly.total4 + kBlock - 1) / kBlock : 256);
     a.splits = splits;
     a.nblk = edge_blocks;
     a.b1w = 1.0f - beta1;
@@ -1057,6 +1131,30 @@ int nav_grad_reduce_adam(const nav_mlp* nets, int32_t n_nets, const float* const
                        a);
     NAV_CHECK_LAUNCH();
     return 0;
+}
+
+int nav_grad_reduce_adam(const nav_mlp* nets, int32_t n_nets, const float* const* hidden_slabs,
+                         int32_t splits, const float* const* edge_slabs, int64_t edge_blocks,
+                         float* const* grads, float* const* m, float* const* v, float beta1,
+                         float beta2, float eps, const float* step_size, const float* bc2_sqrt,
+                         void* stream) {
+    return grad_reduce_adam_impl(nets, n_nets, hidden_slabs, splits, edge_slabs, edge_blocks,
+                                 grads, m, v, beta1, beta2, eps, step_size, bc2_sqrt, nullptr,
+                                 nullptr, nullptr, 0, 0.f, stream);
+}
+
+int nav_grad_reduce_adam_polyak(const nav_mlp* nets, int32_t n_nets,
+                                const float* const* hidden_slabs, int32_t splits,
+                                const float* const* edge_slabs, int64_t edge_blocks,
+                                float* const* grads, float* const* m, float* const* v,
+                                float beta1, float beta2, float eps, const float* step_size,
+                                const float* bc2_sqrt, const nav_mlp* net_targets,
+                                const nav_mlp* targets, const nav_mlp* sources, int32_t n_pairs,
+                                float tau, void* stream) {
+    if (!net_targets) return NAV_EINVAL;
+    return grad_reduce_adam_impl(nets, n_nets, hidden_slabs, splits, edge_slabs, edge_blocks,
+                                 grads, m, v, beta1, beta2, eps, step_size, bc2_sqrt, net_targets,
+                                 targets, sources, n_pairs, tau, stream);
 }
 
 int nav_polyak_multi(const nav_mlp* targets, const nav_mlp* sources, int32_t n, float tau,

@@ -135,6 +135,10 @@ SIGNATURES = [
     ("nav_grad_reduce_adam", C.c_int, [_P(NavMlp), C.c_int32, _P(_vp), C.c_int32, _P(_vp),
                                        C.c_int64, _P(_vp), _P(_vp), _P(_vp), C.c_float, C.c_float,
                                        C.c_float, _P(C.c_float), _P(C.c_float), _vp]),
+    ("nav_grad_reduce_adam_polyak", C.c_int,
+     [_P(NavMlp), C.c_int32, _P(_vp), C.c_int32, _P(_vp), C.c_int64, _P(_vp), _P(_vp), _P(_vp),
+      C.c_float, C.c_float, C.c_float, _P(C.c_float), _P(C.c_float), _P(NavMlp), _P(NavMlp),
+      _P(NavMlp), C.c_int32, C.c_float, _vp]),
     ("nav_grad_reduce_multi", C.c_int, [_P(NavMlp), C.c_int32, _P(_vp), C.c_int32, _P(_vp),
                                         C.c_int64, _P(_vp), _vp]),
     ("nav_adam_multi", C.c_int, [_P(NavMlp), C.c_int32, _P(_vp), _P(_vp), _P(_vp), C.c_float,

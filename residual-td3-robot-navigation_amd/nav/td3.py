@@ -84,6 +84,9 @@ class TD3:
         # train_critic's row backward inside the critic_rows launch (NAV_CRITIC_ROW_BWD=0: its
         # own launch; tuning / A/B only)
         self.row_backward = os.environ.get("NAV_CRITIC_ROW_BWD", "1") != "0"
+        # a policy epoch's soft updates inside the actor's reduce + Adam launch
+        # (NAV_FUSE_SOFT_UPDATE=0: their own launch; A/B only)
+        self.fuse_soft_update = os.environ.get("NAV_FUSE_SOFT_UPDATE", "1") != "0"
         self._B = 0
         self.actor_losses, self.critic_losses = [], []
 
@@ -147,7 +150,7 @@ class TD3:
                           (4 if adam else 1) * x.count) for x, e in zip(nets, eslabs))
 
     def _grads_and_step(self, nets, opts, M, inp, ld_in, in_col, acts, dz, dy, ld_dy, masks,
-                        eslabs, grads, hslabs, s, stream):
+                        eslabs, grads, hslabs, s, stream, soft_update=False):
         """Weight gradients, then the fixed-order reduce of those and the fwd/bwd edge partials
         fused with each net's Adam step (robot.py:236-239): 2 launches for 1-2 nets. With a
         grad_hook (shared policy) the reduce writes the flat gradient bucket, the hook
@@ -155,13 +158,19 @@ class TD3:
         splits = self._wgrad(nets, M, inp, ld_in, in_col, acts, dz, dy, ld_dy, masks, hslabs, s)
         if self.grad_hook is None:
             coeffs = [o.advance() for o in opts]
-            with prof.region("grad_reduce", self._reduce_bytes(nets, eslabs, splits, True)):
-                lib().nav_grad_reduce_adam(
-                    descs(*nets), len(nets), parr(*hslabs), splits, parr(*eslabs), self.nblk,
+            args = (descs(*nets), len(nets), parr(*hslabs), splits, parr(*eslabs), self.nblk,
                     parr(*grads), parr(*[o.m for o in opts]), parr(*[o.v for o in opts]),
                     opts[0].b1, opts[0].b2, opts[0].eps,
                     (C.c_float * len(nets))(*[c[0] for c in coeffs]),
-                    (C.c_float * len(nets))(*[c[1] for c in coeffs]), s)
+                    (C.c_float * len(nets))(*[c[1] for c in coeffs]))
+            with prof.region("grad_reduce", self._reduce_bytes(nets, eslabs, splits, True)):
+                if soft_update:  # the actor's step and all three soft updates in one launch
+                    lib().nav_grad_reduce_adam_polyak(
+                        *args, descs(self.target_actor),
+                        descs(self.target_critic_network_1, self.target_critic_network_2),
+                        descs(self.critic_network_1, self.critic_network_2), 2, self.cfg.tau, s)
+                else:
+                    lib().nav_grad_reduce_adam(*args, s)
             return
         with prof.region("grad_reduce", self._reduce_bytes(nets, eslabs, splits, False)):
             lib().nav_grad_reduce_multi(descs(*nets), len(nets), parr(*hslabs), splits,
@@ -172,6 +181,8 @@ class TD3:
         with torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext():
             self.grad_hook(bucket)
         self._adam(nets, opts, grads, s, self.grad_div)
+        if soft_update:
+            self.soft_update_all(stream)
 
     def _adam(self, nets, opts, grads, s, grad_div=1.0):
         """One multi-net Adam launch on flat gradients (already reduced) / grad_div."""
@@ -289,12 +300,14 @@ class TD3:
     def _actor_wgrad_args(self):
         return (self.batch2, 8, 0, [self.acts_a], [self.dz_a], [self.da], 2, [self.mask_a])
 
-    def train_actor(self, replay, idx=None, stream=None):
+    def train_actor(self, replay, idx=None, stream=None, soft_update=False):
+        """robot.py:369-398; with soft_update the three soft updates of robot.py:283-285 that
+        follow it on a policy epoch ride in the actor's reduce + Adam launch."""
         s = stream_handle(stream)
         self._actor_rows(replay, idx, s)
         self._grads_and_step([self.actor_network], [self.actor_optimizer], self.cfg.batch_size,
                              *self._actor_wgrad_args(), [self.eslab_a], [self.grad_a],
-                             [self.hslab], s, stream)
+                             [self.hslab], s, stream, soft_update=soft_update)
 
     def actor_gradients(self, replay, idx=None, stream=None):
         """train_actor's gradient phase alone: the actor's flat gradient into `grad_a`."""
@@ -339,10 +352,12 @@ class TD3:
             if track_losses:
                 self.critic_losses.append(sum(self.critic_loss_values()) / 2)
             if epoch % self.cfg.policy_update_delay == 0:
-                self.train_actor(replay, idx=idx_fn() if idx_fn else None, stream=stream)
+                self.train_actor(replay, idx=idx_fn() if idx_fn else None, stream=stream,
+                                 soft_update=self.fuse_soft_update)
                 if track_losses:
                     self.actor_losses.append(self.actor_loss_value())
-                self.soft_update_all(stream)
+                if not self.fuse_soft_update:
+                    self.soft_update_all(stream)
             self.update_counter += 1
 
     def networks(self):

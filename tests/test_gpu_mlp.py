@@ -601,3 +601,46 @@ def test_critic_rows_split_twins_bit_identical(nav, hidden, nh, B, monkeypatch):
             sel = [l for l in range(nh) if (mid >> l) & 1]
             assert torch.equal(a["acts"][k][sel], b["acts"][k][sel]), k
             assert torch.equal(a["dz"][k][sel], b["dz"][k][sel]), k
+
+
+def test_reduce_adam_polyak_fused_bitwise(nav):
+    """nav_grad_reduce_adam_polyak (the actor's reduce + Adam with the three soft updates of
+    robot.py:283-285 in one launch) == nav_grad_reduce_adam then nav_polyak_multi, bit for bit:
+    parameters, moments, targets and every packed image."""
+    from nav._lib import descs, lib, parr, stream_handle
+    L = lib()
+    s = stream_handle()
+    for hidden, nh, d_in, d_out in ((256, 2, 2, 2), (200, 3, 2, 2)):
+        # two identical copies (index 0: unfused, 1: fused) of the actor, its target and the
+        # critics' targets; the critics (sources) are shared
+        a_net = [make_net(d_in, d_out, hidden, nh, 70)[0] for _ in range(2)]
+        atgt = [make_net(d_in, d_out, hidden, nh, 72)[0] for _ in range(2)]
+        crit = [make_net(4, 1, hidden, nh, 74 + k)[0] for k in range(2)]
+        ctgt = [[make_net(4, 1, hidden, nh, 76 + k)[0] for k in range(2)] for _ in range(2)]
+        hp = a_net[0].hp
+        splits, nblk = 4, 37
+        hc = max(4, L.nav_mlp_hidden_count(hp, nh))
+        ec = L.nav_mlp_edge_count(d_in, d_out, hp, nh)
+        hs = torch.randn(splits, hc, device=DEV)
+        es = torch.randn(nblk, ec, device=DEV)
+        m = [torch.randn(a_net[0].count, device=DEV) * 1e-3 for _ in range(2)]
+        v = [torch.rand(a_net[0].count, device=DEV) * 1e-4 for _ in range(2)]
+        m[1].copy_(m[0]); v[1].copy_(v[0])
+        g = [torch.zeros(a_net[0].count, device=DEV) for _ in range(2)]
+        ss, bc = (C.c_float * 1)(1e-3), (C.c_float * 1)(0.5)
+        # unfused: reduce + Adam, then the soft updates of (actor, critic 1, critic 2)
+        L.nav_grad_reduce_adam(descs(a_net[0]), 1, parr(hs), splits, parr(es), nblk, parr(g[0]),
+                               parr(m[0]), parr(v[0]), 0.9, 0.999, 1e-8, ss, bc, s)
+        L.nav_polyak_multi(descs(atgt[0], ctgt[0][0], ctgt[0][1]),
+                           descs(a_net[0], crit[0], crit[1]), 3, 0.001, s)
+        # fused
+        L.nav_grad_reduce_adam_polyak(descs(a_net[1]), 1, parr(hs), splits, parr(es), nblk,
+                                      parr(g[1]), parr(m[1]), parr(v[1]), 0.9, 0.999, 1e-8, ss, bc,
+                                      descs(atgt[1]), descs(ctgt[1][0], ctgt[1][1]),
+                                      descs(crit[0], crit[1]), 2, 0.001, s)
+        torch.cuda.synchronize()
+        assert torch.equal(g[0], g[1]) and torch.equal(m[0], m[1]) and torch.equal(v[0], v[1])
+        assert torch.equal(a_net[0].params, a_net[1].params)
+        assert torch.equal(a_net[0].packed, a_net[1].packed)
+        for x, y in ((atgt[0], atgt[1]), (ctgt[0][0], ctgt[1][0]), (ctgt[0][1], ctgt[1][1])):
+            assert torch.equal(x.params, y.params) and torch.equal(x.packed, y.packed)
