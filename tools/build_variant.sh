@@ -19,6 +19,8 @@ case $unit in
        objs=${objs/$B\/env_kernels.o/abl\/$name.o} ;;
   mlp8) /opt/rocm/bin/hipcc $FL -mllvm -amdgpu-mfma-vgpr-form=1 $flags -DNAV_MLP_PART=8 -c $P/csrc/mlp_kernels.hip -o abl/$name.o
         objs=${objs/$B\/mlp_nt8.o/abl\/$name.o} ;;
+  mlp8agpr) /opt/rocm/bin/hipcc $FL $flags -DNAV_MLP_PART=8 -c $P/csrc/mlp_kernels.hip -o abl/$name.o
+        objs=${objs/$B\/mlp_nt8.o/abl\/$name.o} ;;
   *) echo "unit?"; exit 2 ;;
 esac
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o abl/libnavenv_$name.so $objs

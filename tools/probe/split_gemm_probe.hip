@@ -291,6 +291,87 @@ __device__ __forceinline__ void gemm_x6f(const float* A, const bf16x8* Bs, f32x1
     }
 }
 
+// 128 rows per workgroup (one per CU), each wave 4 row tiles x 2 column tiles: half the B loads
+// per MFMA of the 64-row form, the same A split per MFMA
+constexpr int TM4 = 128;
+__device__ __forceinline__ void gemm_x6_rt4(const float* A, const bf16x8* Bs, f32x16 (&acc)[4][2]) {
+    constexpr int nq = HP / 16;
+    constexpr size_t PL = (size_t)nq * 2 * HP;
+    const int lane = threadIdx.x & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
+    for (int rt = 0; rt < 4; ++rt)
+        for (int j = 0; j < 2; ++j)
+            for (int i = 0; i < 16; ++i) acc[rt][j][i] = 0.f;
+    const bf16x8* B0 = Bs + (size_t)h * HP + wv * 32 + l32;
+    const bf16x8* B1 = Bs + (size_t)h * HP + (wv + 4) * 32 + l32;
+    constexpr size_t STEP = 2 * (size_t)HP;
+    bf16x8 b0[3], b1[3], nb0[3], nb1[3];
+    for (int p = 0; p < 3; ++p) {
+        b0[p] = B0[p * PL];
+        b1[p] = B1[p * PL];
+    }
+    const float* arow = A + l32 * SS + 8 * h;
+    float4 a[4][2], an[4][2];
+    for (int rt = 0; rt < 4; ++rt) {
+        a[rt][0] = *reinterpret_cast<const float4*>(arow + rt * 32 * SS);
+        a[rt][1] = *reinterpret_cast<const float4*>(arow + rt * 32 * SS + 4);
+    }
+#pragma unroll
+    for (int q = 0; q < nq; ++q) {
+        if (q + 1 < nq) {
+            for (int p = 0; p < 3; ++p) {
+                nb0[p] = B0[p * PL + (q + 1) * STEP];
+                nb1[p] = B1[p * PL + (q + 1) * STEP];
+            }
+            for (int rt = 0; rt < 4; ++rt) {
+                an[rt][0] = *reinterpret_cast<const float4*>(arow + rt * 32 * SS + 16 * (q + 1));
+                an[rt][1] = *reinterpret_cast<const float4*>(arow + rt * 32 * SS + 16 * (q + 1) + 4);
+            }
+        }
+#pragma unroll
+        for (int rt = 0; rt < 4; ++rt) {
+            const Split3 sp = split8(a[rt][0], a[rt][1]);
+            acc[rt][0] = mfma_x6b(sp, b0, acc[rt][0]);
+            acc[rt][1] = mfma_x6b(sp, b1, acc[rt][1]);
+        }
+        if (q + 1 < nq) {
+            for (int p = 0; p < 3; ++p) {
+                b0[p] = nb0[p];
+                b1[p] = nb1[p];
+            }
+            for (int rt = 0; rt < 4; ++rt) {
+                a[rt][0] = an[rt][0];
+                a[rt][1] = an[rt][1];
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(256, 1) void k_probe_rt4(const float* rows, const bf16x8* Bs,
+                                                      float* out) {
+    extern __shared__ float act[];
+    const int tid = threadIdx.x;
+    const float* src = rows + (size_t)(blockIdx.x & 3) * TM4 * HP;
+    for (int i = tid; i < TM4 * HP; i += kBlock) act[(i / HP) * SS + i % HP] = src[i];
+    __syncthreads();
+    f32x16 acc[4][2];
+    const int lane = threadIdx.x & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
+    for (int L = 0; L < LAYERS; ++L) {
+        gemm_x6_rt4(act, Bs, acc);
+        __syncthreads();
+        for (int j = 0; j < 2; ++j) {
+            const int t = j == 0 ? wv : wv + 4;
+            float* col = act + t * 32 + l32 + 4 * h * SS;
+            for (int rt = 0; rt < 4; ++rt)
+                for (int i = 0; i < 16; ++i)
+                    col[(rt * 32 + (i & 3) + 8 * (i >> 2)) * SS] = fmaxf(acc[rt][j][i], 0.f);
+        }
+        __syncthreads();
+    }
+    if (blockIdx.x < 4)
+        for (int i = tid; i < TM4 * HP; i += kBlock)
+            out[(size_t)blockIdx.x * TM4 * HP + i] = act[(i / HP) * SS + i % HP];
+}
+
 // A pre-split in LDS: planes [3][TM][HP + 8] bf16, written once per layer; 8 waves, wave w owns
 // column tile w of both row tiles
 constexpr int PS = HP + 8;  // plane row stride (bf16)
@@ -499,17 +580,21 @@ int main() {
             }
         ref.swap(nxt);
     }
-    for (int mode = 0; mode < 9; ++mode) {
+    for (int mode = 0; mode < 10; ++mode) {
         auto k = mode == 0 ? k_probe<0> : mode == 1 ? k_probe<1> : mode == 2 ? k_probe<2> : mode == 4 ? k_probe<4> : mode == 5 ? k_probe<5> : mode == 6 ? k_probe<6> : mode == 7 ? k_probe<7> : k_probe<8>;
+        if (mode == 9) k = k_probe<1>;
         const size_t lds_pl = (size_t)3 * TM * PS * 2;
         auto launch = [&]() {
-            if (mode != 3)
+            if (mode == 9)
+                hipLaunchKernelGGL(k_probe_rt4, dim3(blocks / 2), dim3(kBlock), (size_t)TM4 * SS * 4, 0, d_rows, d_Bs, d_out);
+            else if (mode != 3)
                 hipLaunchKernelGGL(k, dim3(blocks), dim3(kBlock), lds, 0, d_rows, d_Bf, d_Bs, d_out);
             else
                 hipLaunchKernelGGL(k_probe_pl, dim3(blocks), dim3(512), lds_pl, 0, d_rows, d_Bs, d_out);
         };
         hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         hipFuncSetAttribute((const void*)k_probe_pl, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_pl);
+        hipFuncSetAttribute((const void*)k_probe_rt4, hipFuncAttributeMaxDynamicSharedMemorySize, (int)((size_t)TM4 * SS * 4));
         launch();
         hipDeviceSynchronize();
         hipEvent_t e0, e1;
@@ -536,7 +621,7 @@ int main() {
         }
         printf("{\"mode\": \"%s\", \"us\": %.1f, \"TFs\": %.1f, \"max_abs_err\": %.3e, "
                "\"max_ref\": %.3e, \"rel_rms_err\": %.3e}\n",
-               mode == 0 ? "f32" : mode == 1 ? "bf16x6" : mode == 2 ? "bf16x6_interleaved" : mode == 3 ? "bf16x6_lds_planes_8w" : mode == 4 ? "x6_nosplit" : mode == 5 ? "x6_noBload" : mode == 6 ? "x6_nosplit_noBload" : mode == 7 ? "x6_fenced" : "x6_fenced_interleaved", us, flop / us / 1e6, maxe, maxr, sqrt(sum2 / ref2));
+               mode == 0 ? "f32" : mode == 1 ? "bf16x6" : mode == 2 ? "bf16x6_interleaved" : mode == 3 ? "bf16x6_lds_planes_8w" : mode == 4 ? "x6_nosplit" : mode == 5 ? "x6_noBload" : mode == 6 ? "x6_nosplit_noBload" : mode == 7 ? "x6_fenced" : mode == 8 ? "x6_fenced_interleaved" : "x6_rt4_128rows_1wg", us, flop / us / 1e6, maxe, maxr, sqrt(sum2 / ref2));
     }
     return 0;
 }
