@@ -12,9 +12,6 @@
 #include "mlp_common.h"
 #include "nav_tick.h"
 
-#ifndef NAV_GEMM_INTERLEAVE
-#define NAV_GEMM_INTERLEAVE 0
-#endif
 
 namespace {
 
@@ -57,12 +54,18 @@ NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const bf16x8* __rest
     const int t1 = wc.has1 ? wc.t1 : wc.t0;
     const bf16x8* B0 = Bs + (size_t)h * hp + wc.t0 * 32 + l32;
     const bf16x8* B1 = Bs + (size_t)h * hp + t1 * 32 + l32;
-    bf16x8 b0[3], b1[3];
+    // B planes PF steps ahead: one step for 64-row blocks (the register budget of the big row
+    // kernels), two for 32-row blocks, whose step (12 MFMAs per wave) is shorter than an L2 hit
+    constexpr int PF = RT == 1 ? 2 : 1;
+    bf16x8 bq0[PF + 1][3], bq1[PF + 1][3];
 #pragma unroll
-    for (int p = 0; p < 3; ++p) {
-        b0[p] = B0[p * PL];
-        b1[p] = B1[p * PL];
-    }
+    for (int d = 0; d < PF; ++d)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            const int qd = d < nq ? d : nq - 1;
+            bq0[d][p] = B0[p * PL + qd * STEP];
+            bq1[d][p] = B1[p * PL + qd * STEP];
+        }
     const float* arow = A + l32 * S_ + 8 * h;
     Split3 sa[RT];
 #pragma unroll
@@ -71,14 +74,15 @@ NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const bf16x8* __rest
                         *reinterpret_cast<const float4*>(arow + rt * 32 * S_ + 4));
 #pragma unroll
     for (int q = 0; q < nq; ++q) {
-        bf16x8 nb0[3], nb1[3];
         float4 an[RT][2];
-        if (q + 1 < nq) {
+        if (q + PF < nq) {
 #pragma unroll
             for (int p = 0; p < 3; ++p) {
-                nb0[p] = B0[p * PL + (q + 1) * STEP];
-                nb1[p] = B1[p * PL + (q + 1) * STEP];
+                bq0[(q + PF) % (PF + 1)][p] = B0[p * PL + (q + PF) * STEP];
+                bq1[(q + PF) % (PF + 1)][p] = B1[p * PL + (q + PF) * STEP];
             }
+        }
+        if (q + 1 < nq) {
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt) {
                 an[rt][0] = *reinterpret_cast<const float4*>(arow + rt * 32 * S_ + 16 * (q + 1));
@@ -87,25 +91,12 @@ NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const bf16x8* __rest
         }
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) {
-            acc[rt][0] = mfma_x6(sa[rt], b0, acc[rt][0]);
-            if (NT >= 8 || wc.has1) acc[rt][1] = mfma_x6(sa[rt], b1, acc[rt][1]);
+            acc[rt][0] = mfma_x6(sa[rt], bq0[q % (PF + 1)], acc[rt][0]);
+            if (NT >= 8 || wc.has1) acc[rt][1] = mfma_x6(sa[rt], bq1[q % (PF + 1)], acc[rt][1]);
         }
         if (q + 1 < nq) {
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt) sa[rt] = split8(an[rt][0], an[rt][1]);
-#if NAV_GEMM_INTERLEAVE
-            // the split VALU of step q+1 between step q's MFMAs
-#pragma unroll
-            for (int k = 0; k < 12 * RT; ++k) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
-            }
-#endif
-#pragma unroll
-            for (int p = 0; p < 3; ++p) {
-                b0[p] = nb0[p];
-                b1[p] = nb1[p];
-            }
         }
     }
 }
