@@ -115,9 +115,11 @@ class TD3(_GpuTD3):
         ReplayBuffer.sample draws them (robot.py:111), one per train_critic and one per
         train_actor, in epoch order; the smoothing noise from torch.randn(B, 2) per critic epoch.
         Each epoch's draws are taken on the host right before its launches (the same streams, the
-        same order) into pinned slots and copied asynchronously on the launch stream, so the host's
-        sampling of epoch e+1 (numpy's full permutation of the buffer: the larger host cost) runs
-        while the device works on epoch e; no host round trip between epochs."""
+        same order) into pinned host slots that the row kernels read directly (zero-copy: 100
+        indices and 200 noise values per epoch, no copy launch), so the host's sampling of epoch
+        e+1 (numpy's full permutation of the buffer: the larger host cost) runs while the device
+        works on epoch e; no host round trip between epochs. A slot is written once per update;
+        the next update waits for the last launch of this one before reusing them."""
         B, dev = self.batch_size, self.device
         if len(replay_buffer) < B:
             raise TypeError("cannot unpack non-iterable NoneType object")  # robot.py:326
@@ -127,28 +129,24 @@ class TD3(_GpuTD3):
         pin = getattr(self, "_pin", None)
         if pin is None or pin[0].shape != (n_idx, B) or pin[1].shape[0] != self.num_epochs:
             pin = (torch.empty(n_idx, B, dtype=torch.int64).pin_memory(),
-                   torch.empty(self.num_epochs, B, 2).pin_memory(),
-                   torch.empty(n_idx, B, dtype=torch.int64, device=dev),
-                   torch.empty(self.num_epochs, B, 2, device=dev))
+                   torch.empty(self.num_epochs, B, 2).pin_memory())
             self._pin, self._pin_done = pin, None
-        if self._pin_done is not None:  # the previous update's copies have left the slots
+        if self._pin_done is not None:  # the previous update's kernels have read the slots
             self._pin_done.synchronize()
-        h_idx, h_eps, d_idx, d_eps = pin
+        h_idx, h_eps = pin
         cnt = {"i": 0, "e": 0}
 
         def idx_fn():
             k = cnt["i"]
             cnt["i"] += 1
             h_idx[k].numpy()[:] = np.random.choice(L, B, replace=False)
-            d_idx[k].copy_(h_idx[k], non_blocking=True)
-            return d_idx[k]
+            return h_idx[k]
 
         def eps_fn():
             k = cnt["e"]
             cnt["e"] += 1
             h_eps[k].copy_(torch.randn(B, 2))
-            d_eps[k].copy_(h_eps[k], non_blocking=True)
-            return d_eps[k]
+            return h_eps[k]
         super().td3_update(replay_buffer, self.num_epochs, idx_fn=idx_fn, eps_fn=eps_fn)
         self._pin_done = torch.cuda.Event()
         self._pin_done.record()

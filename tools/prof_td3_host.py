@@ -1,19 +1,55 @@
-import cProfile, pstats, sys, os, time
-sys.path.insert(0, "/root/repo"); sys.path.insert(0, "/root/repo/residual-td3-robot-navigation_amd")
-import numpy as np, torch
-from nav import robot
-rb = robot.Robot(np.array([60.0, 40.0]))
-rng = np.random.default_rng(0)
-for s in rng.uniform(0, 100, (400, 2)):
-    rb.memory.push(s, rng.uniform(-5, 5, 2), rng.uniform(-100, 0), s + 1, False)
-for _ in range(3): rb.td3_agent.td3_update(rb.memory)
-torch.cuda.synchronize()
-t0 = time.perf_counter()
-for _ in range(5): rb.td3_agent.td3_update(rb.memory)
-torch.cuda.synchronize()
-print("ms per update", (time.perf_counter() - t0) / 5 * 1e3)
-pr = cProfile.Profile(); pr.enable()
-for _ in range(5): rb.td3_agent.td3_update(rb.memory)
-torch.cuda.synchronize()
-pr.disable()
-pstats.Stats(pr).sort_stats("tottime").print_stats(25)
+"""Host vs device time of the drop-in td3_update (config 1's learner: 100 epochs, batch 100) at a
+given replay size (tuning only). Prints ms per update (wall, synchronised), the host's own time
+to issue one update (no synchronisation inside), and a cProfile of the issuing loop.
+
+python tools/prof_td3_host.py [replay_rows]
+"""
+import cProfile
+import os
+import pstats
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, ".."))
+sys.path.insert(0, os.path.join(HERE, "..", "residual-td3-robot-navigation_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def main():
+    from nav import robot
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 5000
+    rb = robot.Robot(np.array([60.0, 40.0]))
+    rng = np.random.default_rng(0)
+    for s in rng.uniform(0, 100, (n, 2)):
+        rb.memory.push(s, rng.uniform(-5, 5, 2), rng.uniform(-100, 0), s + 1, False)
+    for _ in range(3):
+        rb.td3_agent.td3_update(rb.memory)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(5):
+        rb.td3_agent.td3_update(rb.memory)
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / 5 * 1e3
+    # host issue time: numpy draws only
+    t0 = time.perf_counter()
+    for _ in range(5):
+        for e in range(150):
+            np.random.choice(n, 100, replace=False)
+    draws = (time.perf_counter() - t0) / 5 * 1e3
+    pr = cProfile.Profile()
+    pr.enable()
+    t0 = time.perf_counter()
+    rb.td3_agent.td3_update(rb.memory)
+    host = (time.perf_counter() - t0) * 1e3
+    pr.disable()
+    torch.cuda.synchronize()
+    print(f"replay {n}: ms per update {wall:.2f}; host issue of one update {host:.2f} ms "
+          f"(profiled); numpy choice x150 alone {draws:.2f} ms")
+    pstats.Stats(pr).sort_stats("tottime").print_stats(18)
+
+
+if __name__ == "__main__":
+    main()
