@@ -23,21 +23,25 @@ struct WaveCols {
 };
 
 // acc[rt][j] = A[TM rows][hp] (LDS f32, row stride S_) x B[hp][tile t_j] on the bf16 matrix
-// cores at f32 accuracy (mlp_common.h: three-way exact bf16 split, six partial products). B is the
-// layer's split image (split_entry layout) in global memory — L2-resident, read once per
-// workgroup, each 16-deep k step's three planes loaded one step ahead; A is read from the LDS rows
-// (two 16-B reads per row tile and step) and split in registers one step ahead too, the split
-// of step q+1 interleaved with step q's MFMAs. No barrier inside the k loop: the LDS rows are
-// read-only during the product. Lane (h, l32) holds A[row l32][16q + 8h + j] and
-// B[16q + 8h + j][col l32], j = 0..7 (the 32x32x16 operand maps).
+// cores at f32 accuracy (mlp_common.h: three-way exact bf16 split, six partial products). Per
+// 16-deep k step the workgroup splits the step's TM x 16 A values ONCE, four per thread, into an
+// LDS stage of three bf16 planes (split_stage), and every wave reads its 16-B fragments from there
+// (before: each of the 4 waves split every A value it read — the split was ~15 % of the GEMM;
+// probe r03v: -10 %). Two barriers per step: stage written, stage read. B is the layer's split
+// image (split_entry layout) in global memory, L2-resident, its three planes loaded PF steps
+// ahead. Lane (h, l32) holds A[row l32][16q + 8h + j] and B[16q + 8h + j][col l32], j = 0..7 (the
+// 32x32x16 operand maps). Every wave runs the split and the barriers; waves without a column
+// tile (NT < 4) skip only the MFMAs.
 template <int NT, int RT>
 NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const bf16x8* __restrict__ Bs,
-                       f32x16 (&acc)[RT][2]) {
+                       __bf16* stage, f32x16 (&acc)[RT][2]) {
     constexpr int hp = NT * 32;
     constexpr int nq = hp / 16;
+    constexpr int TM = RT * 32;
     constexpr size_t PL = (size_t)nq * 2 * hp;  // 16-B entries per plane
     constexpr size_t STEP = 2 * (size_t)hp;     // entries per k step
-    const int lane = threadIdx.x & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
+    constexpr int PP = TM * 16;                 // bf16 per stage plane
+    const int tid = threadIdx.x, lane = tid & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
     const WaveCols<NT> wc(wv);
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt)
@@ -45,14 +49,11 @@ NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const bf16x8* __rest
         for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int i = 0; i < 16; ++i) acc[rt][j][i] = 0.f;
-    if (!wc.has0) return;  // wave-uniform (scalar) branch
-#ifdef NAV_AB_SKIP_GEMM
-    return;  // timing experiment only: the non-GEMM part of the row kernels
-#endif
     // A wave without a second tile re-reads its first tile's B (same cache lines) so every load
-    // is unconditional; its second-tile MFMAs are skipped by a scalar branch.
-    const int t1 = wc.has1 ? wc.t1 : wc.t0;
-    const bf16x8* B0 = Bs + (size_t)h * hp + wc.t0 * 32 + l32;
+    // is unconditional; its second-tile MFMAs are skipped by a scalar branch (a wave without any
+    // tile reads tile 0's and issues none).
+    const int t0 = wc.has0 ? wc.t0 : 0, t1 = wc.has1 ? wc.t1 : t0;
+    const bf16x8* B0 = Bs + (size_t)h * hp + t0 * 32 + l32;
     const bf16x8* B1 = Bs + (size_t)h * hp + t1 * 32 + l32;
     // B planes PF steps ahead: one step for 64-row blocks (the register budget of the big row
     // kernels), two for 32-row blocks, whose step (12 MFMAs per wave) is shorter than an L2 hit
@@ -66,15 +67,34 @@ NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const bf16x8* __rest
             bq0[d][p] = B0[p * PL + qd * STEP];
             bq1[d][p] = B1[p * PL + qd * STEP];
         }
-    const float* arow = A + l32 * S_ + 8 * h;
-    Split3 sa[RT];
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt)
-        sa[rt] = split8(*reinterpret_cast<const float4*>(arow + rt * 32 * S_),
-                        *reinterpret_cast<const float4*>(arow + rt * 32 * S_ + 4));
+    // this thread's share of a step: 4 values of row sr at k offset sk; the stage's two 16-B
+    // halves of row r are swapped when (r >> 3) & 1, which makes both the 8-B stores and the
+    // waves' 16-B fragment reads bank-conflict-free (ds_read_b128 lane groups)
+    const bool sp = tid < TM * 4;
+    const int sr = tid >> 2, sk = (tid & 3) * 4;
+    const float* src = A + sr * S_ + sk;
+    __bf16* dst = stage + sr * 16 + ((((sk >> 3) ^ (sr >> 3)) & 1) << 3) + (sk & 7);
+    const __bf16* frag = stage + l32 * 16 + (((h ^ (l32 >> 3)) & 1) << 3);
+    float4 x = sp ? *reinterpret_cast<const float4*>(src) : make_float4(0.f, 0.f, 0.f, 0.f);
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 #pragma unroll
     for (int q = 0; q < nq; ++q) {
-        float4 an[RT][2];
+        if (sp) {
+            const float v[4] = {x.x, x.y, x.z, x.w};
+            bf16x4 ph, pm, pl;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                __bf16 hh, mm, ll;
+                split1(v[j], hh, mm, ll);
+                ph[j] = hh;
+                pm[j] = mm;
+                pl[j] = ll;
+            }
+            *reinterpret_cast<bf16x4*>(dst) = ph;
+            *reinterpret_cast<bf16x4*>(dst + PP) = pm;
+            *reinterpret_cast<bf16x4*>(dst + 2 * PP) = pl;
+            if (q + 1 < nq) x = *reinterpret_cast<const float4*>(src + 16 * (q + 1));
+        }
         if (q + PF < nq) {
 #pragma unroll
             for (int p = 0; p < 3; ++p) {
@@ -82,22 +102,26 @@ NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const bf16x8* __rest
                 bq1[(q + PF) % (PF + 1)][p] = B1[p * PL + (q + PF) * STEP];
             }
         }
-        if (q + 1 < nq) {
-#pragma unroll
-            for (int rt = 0; rt < RT; ++rt) {
-                an[rt][0] = *reinterpret_cast<const float4*>(arow + rt * 32 * S_ + 16 * (q + 1));
-                an[rt][1] = *reinterpret_cast<const float4*>(arow + rt * 32 * S_ + 16 * (q + 1) + 4);
-            }
-        }
+        __syncthreads();  // the step's stage is written
+        Split3 sa[RT];
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) {
-            acc[rt][0] = mfma_x6(sa[rt], bq0[q % (PF + 1)], acc[rt][0]);
-            if (NT >= 8 || wc.has1) acc[rt][1] = mfma_x6(sa[rt], bq1[q % (PF + 1)], acc[rt][1]);
+            const __bf16* f = frag + rt * 32 * 16;
+            sa[rt].h = *reinterpret_cast<const bf16x8*>(f);
+            sa[rt].m = *reinterpret_cast<const bf16x8*>(f + PP);
+            sa[rt].l = *reinterpret_cast<const bf16x8*>(f + 2 * PP);
         }
-        if (q + 1 < nq) {
+        __syncthreads();  // ... and read: the next step may overwrite it
+#ifndef NAV_AB_SKIP_GEMM
+        if (wc.has0) {  // wave-uniform
 #pragma unroll
-            for (int rt = 0; rt < RT; ++rt) sa[rt] = split8(an[rt][0], an[rt][1]);
+            for (int rt = 0; rt < RT; ++rt) {
+                acc[rt][0] = mfma_x6(sa[rt], bq0[q % (PF + 1)], acc[rt][0]);
+                if (NT >= 8 || wc.has1)
+                    acc[rt][1] = mfma_x6(sa[rt], bq1[q % (PF + 1)], acc[rt][1]);
+            }
         }
+#endif
     }
 }
 
@@ -162,10 +186,14 @@ struct FwdArgs {
 // Output-layer partial sums: [d_out <= 2][4 waves][TM rows] (red_floats per block).
 __host__ __device__ constexpr int red_floats(int tm) { return 2 * kWaves * tm; }
 
-// rows [tm][hp+4] + input/dy staging [tm][4] + output-layer partial sums
-inline size_t lds_bytes(int hp, int tm) {
-    return ((size_t)tm * (hp + 4) + tm * 4 + red_floats(tm)) * 4;
+// bytes of gemm_cols' split stage for TM rows: [3 planes][TM][16] bf16
+__host__ __device__ constexpr size_t stage_bytes(int tm) { return (size_t)3 * tm * 16 * 2; }
+
+// rows [tm][hp+4] + input/dy staging [tm][4] + output-layer partial sums, then the split stage
+__host__ __device__ constexpr size_t lds_floats(int hp, int tm) {
+    return (size_t)tm * (hp + 4) + tm * 4 + red_floats(tm);
 }
+inline size_t lds_bytes(int hp, int tm) { return lds_floats(hp, tm) * 4 + stage_bytes(tm); }
 
 
 // Store a layer's C-layout result into the LDS rows (the next layer's A operand) and its ReLU
@@ -445,7 +473,7 @@ NAV_DEV void loss_epilogue(const MlpDev& net, const f32x16 (&top)[RT][2], float*
 // for its global copy — and the output layer's per-wave partials land in `red` (ready for out_y
 // after the trailing barrier).
 template <int NT, int RT>
-NAV_DEV void fwd_net(const MlpDev& net, float* act, const float* xin, float* red,
+NAV_DEV void fwd_net(const MlpDev& net, float* act, __bf16* stage, const float* xin, float* red,
                      uint16_t* masks, int64_t n_rt, float* act_save, uint32_t save_mask,
                      int64_t row0, int64_t M, int64_t rt0, f32x16 (&top)[RT][2], int mk = -64) {
     constexpr int hp = NT * 32, SS = hp + 4;
@@ -507,7 +535,7 @@ NAV_DEV void fwd_net(const MlpDev& net, float* act, const float* xin, float* red
         const float* bL = net.params + net.b_off[L];
         const float bb0 = wc.has0 ? bL[wc.t0 * 32 + l32] : 0.f;
         const float bb1 = wc.has1 ? bL[wc.t1 * 32 + l32] : 0.f;
-        gemm_cols<NT, RT>(act, SS, img_fwd(net, L), acc);
+        gemm_cols<NT, RT>(act, SS, img_fwd(net, L), stage, acc);
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             if (!(j == 0 ? wc.has0 : wc.has1)) continue;
@@ -576,6 +604,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
     const int64_t n_rt = mask_rowtiles(M);
     float* act = smem;
     float* xin = smem + TM * SS;  // [TM][4]
+    __bf16* stage = reinterpret_cast<__bf16*>(smem + lds_floats(hp, TM));
     const int d_in = net.d_in, d_out = net.d_out;
 
     // ---- input rows -> xin
@@ -602,7 +631,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
 
     float* red = xin + TM * 4;  // [2][PARTS][TM]
     f32x16 top[RT][2];
-    fwd_net<NT, RT>(net, act, xin, red, masks, n_rt, act_save, a.save_mask, row0, M, rt0, top);
+    fwd_net<NT, RT>(net, act, stage, xin, red, masks, n_rt, act_save, a.save_mask, row0, M, rt0, top);
     const int rloc = tid % TM;
     const int j = tid / TM;
     const int64_t r = row0 + rloc;
@@ -823,7 +852,7 @@ NAV_DEV void mask_and_store(f32x16 (&acc)[RT][2], const uint32_t (&mbits)[RT][2]
 // partials (every bias, dW0 from the input rows xin [TM][4], and dWo / dbo when h_top [M][hp] is
 // given); dz_L rows to dz for save_mask bits.
 template <int NT, int RT>
-NAV_DEV void bwd_net(const MlpDev& net, float* act, const float* dys, const float* xin,
+NAV_DEV void bwd_net(const MlpDev& net, float* act, __bf16* stage, const float* dys, const float* xin,
                      const uint16_t* masks, int64_t n_rt, float* es, const float* h_top,
                      float* dz, uint32_t save_mask, int64_t row0, int64_t M, int64_t rt0,
                      int mk = -64) {
@@ -913,7 +942,7 @@ NAV_DEV void bwd_net(const MlpDev& net, float* act, const float* dys, const floa
         f32x16 acc[RT][2];
         uint32_t mbits[RT][2];
         load_mask_bits<NT, RT>(masks + (size_t)(L - 1) * mstride, rt0, mbits);
-        gemm_cols<NT, RT>(act, SS, img_bwd(net, L), acc);
+        gemm_cols<NT, RT>(act, SS, img_bwd(net, L), stage, acc);
         NAV_MARK(mk + 3);
         __syncthreads();
         mask_and_store<NT, RT>(acc, mbits, act, SS);
@@ -949,6 +978,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_bwd(BwdArgs a) {
     const int64_t rt0 = (int64_t)blockIdx.x * RT;
     const int64_t n_rt = mask_rowtiles(M);
     float* act = smem;
+    __bf16* stage = reinterpret_cast<__bf16*>(smem + lds_floats(hp, TM));
     float* dys = smem + TM * SS;  // [TM][4] dy rows
     float* xin = dys + TM * 4;    // [TM][4] forward input rows (dW0), inside the red scratch
     const int d_in = net.d_in, d_out = net.d_out;
@@ -968,7 +998,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_bwd(BwdArgs a) {
         *reinterpret_cast<float4*>(xin + tid * 4) = make_float4(xi[0], xi[1], xi[2], xi[3]);
     }
     __syncthreads();
-    bwd_net<NT, RT>(net, act, dys, xin, a.masks[y], n_rt, es, a.h_top[y], a.dz[y], a.save_mask,
+    bwd_net<NT, RT>(net, act, stage, dys, xin, a.masks[y], n_rt, es, a.h_top[y], a.dz[y], a.save_mask,
                     row0, M, rt0);
 
     // dx = dz_0 . W0 : thread = (row, input)
@@ -1043,6 +1073,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
     float* brow = red + red_floats(TM);  // [TM][8] the sampled replay rows
     float* qv = brow + TM * 8;     // [TM] q1'
     float* dys = qv + TM;          // [TM][4] dL/dq rows of the row backward
+    __bf16* stage = reinterpret_cast<__bf16*>(dys + TM * 4);  // gemm_cols' split stage
     NAV_MARK(0);
     // target policy smoothing noise of (row, output) tid % TM, tid / TM: clamp(policy_noise * eps,
     // +-noise_clip), formed while the sampled rows are in flight
@@ -1079,7 +1110,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
     NAV_MARK(1);
     // target actor; a' = clamp(pi'(s') + clamp(policy_noise * eps, +-noise_clip), +-max_action)
     f32x16 top[RT][2];
-    fwd_net<NT, RT>(a.actor_t, act, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0, top, 2);
+    fwd_net<NT, RT>(a.actor_t, act, stage, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0, top, 2);
     if (tid < 2 * TM) {
         const int rloc = tid % TM, j = tid / TM;
         const int64_t r = row0 + rloc;
@@ -1095,10 +1126,10 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
     NAV_MARK(8);
     // twin target critics on (s', a'), then y = r + gamma * min(q1', q2') * (1 - done), kept in
     // the row's thread
-    fwd_net<NT, RT>(a.critic_t[0], act, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0, top,
+    fwd_net<NT, RT>(a.critic_t[0], act, stage, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0, top,
                     9);
     if (tid < TM) qv[tid] = out_y<RT>(a.critic_t[0], red, tid, 0);
-    fwd_net<NT, RT>(a.critic_t[1], act, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0, top,
+    fwd_net<NT, RT>(a.critic_t[1], act, stage, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0, top,
                     15);
     float yt = 0.f;
     if (tid < TM) {
@@ -1113,7 +1144,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
 #pragma unroll 1
     for (int q = 0; q < 2; ++q) {
         if (a.split_twins && q != (int)blockIdx.y) continue;  // workgroup-uniform
-        fwd_net<NT, RT>(a.critic[q], act, xin, red, a.masks[q], n_rt, a.acts[q], a.save_mask, row0,
+        fwd_net<NT, RT>(a.critic[q], act, stage, xin, red, a.masks[q], n_rt, a.acts[q], a.save_mask, row0,
                         B, rt0, top, 22 + 14 * q);
         float* es = a.eslab[q] ? a.eslab[q] + (int64_t)blockIdx.x * a.ecount : nullptr;
         loss_epilogue<NT, RT>(a.critic[q], top, red, row0, B, yt, a.norm, a.dq[q],
@@ -1125,7 +1156,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
                 *reinterpret_cast<float4*>(dys + tid * 4) =
                     make_float4(red[kWaves * TM + tid], 0.f, 0.f, 0.f);  // loss_epilogue's dq
             __syncthreads();
-            bwd_net<NT, RT>(a.critic[q], act, dys, xin, a.masks[q], n_rt, es, nullptr, a.dz[q],
+            bwd_net<NT, RT>(a.critic[q], act, stage, dys, xin, a.masks[q], n_rt, es, nullptr, a.dz[q],
                             a.dz_save_mask, row0, B, rt0, 29 + 14 * q);
             __syncthreads();  // the next forward's layer 0 overwrites the rows
         }
@@ -1170,6 +1201,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_actor_rows(ActorRowsArgs a) {
     float* red = xin + TM * 4;       // [2][PARTS][TM]
     float* dys = red + red_floats(TM);  // [TM][4] critic dy
     float* dys2 = dys + TM * 4;      // [TM][4] actor dy = dL/da
+    __bf16* stage = reinterpret_cast<__bf16*>(dys2 + TM * 4);  // gemm_cols' split stage
     if (tid < TM) {
         const int64_t b = row0 + tid;
         float4 lo = make_float4(0.f, 0.f, 0.f, 0.f), hi = lo;
@@ -1187,10 +1219,10 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_actor_rows(ActorRowsArgs a) {
     // the actor's top hidden layer stays in registers until dL/da is known (its dWo partials)
     f32x16 topa[RT][2];
 #if NAV_ACTOR_TOP_REGS
-    fwd_net<NT, RT>(a.actor, act, xin, red, a.masks_a, n_rt, a.acts, a.save_mask, row0, B, rt0,
+    fwd_net<NT, RT>(a.actor, act, stage, xin, red, a.masks_a, n_rt, a.acts, a.save_mask, row0, B, rt0,
                     topa);
 #else
-    fwd_net<NT, RT>(a.actor, act, xin, red, a.masks_a, n_rt, a.acts,
+    fwd_net<NT, RT>(a.actor, act, stage, xin, red, a.masks_a, n_rt, a.acts,
                     a.save_mask | (1u << (a.actor.n_hidden - 1)), row0, B, rt0, topa);
 #endif
     if (tid < 2 * TM) {
@@ -1199,9 +1231,9 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_actor_rows(ActorRowsArgs a) {
     }
     __syncthreads();
     f32x16 top[RT][2];
-    fwd_net<NT, RT>(a.critic, act, xin, red, a.masks_c, n_rt, nullptr, 0u, row0, B, rt0, top);
+    fwd_net<NT, RT>(a.critic, act, stage, xin, red, a.masks_c, n_rt, nullptr, 0u, row0, B, rt0, top);
     if (tid < TM && a.q && row0 + tid < B) a.q[row0 + tid] = out_y<RT>(a.critic, red, tid, 0);
-    bwd_net<NT, RT>(a.critic, act, dys, xin, a.masks_c, n_rt, nullptr, nullptr, nullptr, 0u, row0,
+    bwd_net<NT, RT>(a.critic, act, stage, dys, xin, a.masks_c, n_rt, nullptr, nullptr, nullptr, 0u, row0,
                     B, rt0);
     if (tid < 2 * TM) {
         const int rloc = tid % TM, j = tid / TM;
@@ -1226,10 +1258,10 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_actor_rows(ActorRowsArgs a) {
             for (int rr = 0; rr < TM; ++rr) sb += dys2[rr * 4 + tid];
         es[e_bo(a.actor) + tid] = sb;
     }
-    bwd_net<NT, RT>(a.actor, act, dys2, xin, a.masks_a, n_rt, es, nullptr, a.dz, a.dz_save_mask,
+    bwd_net<NT, RT>(a.actor, act, stage, dys2, xin, a.masks_a, n_rt, es, nullptr, a.dz, a.dz_save_mask,
                     row0, B, rt0);
 #else
-    bwd_net<NT, RT>(a.actor, act, dys2, xin, a.masks_a, n_rt, es,
+    bwd_net<NT, RT>(a.actor, act, stage, dys2, xin, a.masks_a, n_rt, es,
                     a.acts + (int64_t)(a.actor.n_hidden - 1) * B * hp, a.dz, a.dz_save_mask,
                     row0, B, rt0);
 #endif
@@ -1294,7 +1326,8 @@ template <int NT, int RT>
 void launch_critic_rows_k(const CriticRowsArgs& a, hipStream_t st) {
     constexpr int TM = RT * 32;
     const size_t lds =
-        ((size_t)TM * (NT * 32 + 4) + TM * 4 + red_floats(TM) + TM * 8 + TM + TM * 4) * 4;
+        ((size_t)TM * (NT * 32 + 4) + TM * 4 + red_floats(TM) + TM * 8 + TM + TM * 4) * 4 +
+        stage_bytes(TM);
     auto k = k_td3_critic_rows<NT, RT>;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
@@ -1305,7 +1338,8 @@ void launch_critic_rows_k(const CriticRowsArgs& a, hipStream_t st) {
 template <int NT, int RT>
 void launch_actor_rows_k(const ActorRowsArgs& a, hipStream_t st) {
     constexpr int TM = RT * 32;
-    const size_t lds = ((size_t)TM * (NT * 32 + 4) + TM * 4 + red_floats(TM) + TM * 8) * 4;
+    const size_t lds = ((size_t)TM * (NT * 32 + 4) + TM * 4 + red_floats(TM) + TM * 8) * 4 +
+                       stage_bytes(TM);
     auto k = k_td3_actor_rows<NT, RT>;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);

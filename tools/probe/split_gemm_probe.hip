@@ -372,6 +372,79 @@ __global__ __launch_bounds__(256, 1) void k_probe_rt4(const float* rows, const b
             out[(size_t)blockIdx.x * TM4 * HP + i] = act[(i / HP) * SS + i % HP];
 }
 
+// cooperative split: per k step the workgroup's 256 threads split the step's 64 x 16 A values
+// once (4 per thread) into an LDS stage of three bf16 planes (row stride 24 bf16: conflict-free
+// 16-B reads), then every wave reads its fragments from the stage (2 barriers per step)
+constexpr int STG = 24;
+__device__ __forceinline__ void gemm_x6_coop(const float* A, __bf16* stage, const bf16x8* Bs,
+                                             f32x16 (&acc)[2][2]) {
+    constexpr int nq = HP / 16;
+    constexpr size_t PL = (size_t)nq * 2 * HP;
+    const int tid = threadIdx.x, lane = tid & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
+    for (int rt = 0; rt < 2; ++rt)
+        for (int j = 0; j < 2; ++j)
+            for (int i = 0; i < 16; ++i) acc[rt][j][i] = 0.f;
+    const bf16x8* B0 = Bs + (size_t)h * HP + wv * 32 + l32;
+    const bf16x8* B1 = Bs + (size_t)h * HP + (wv + 4) * 32 + l32;
+    constexpr size_t STEP = 2 * (size_t)HP;
+    bf16x8 b0[3], b1[3], nb0[3], nb1[3];
+    for (int p = 0; p < 3; ++p) {
+        b0[p] = B0[p * PL];
+        b1[p] = B1[p * PL];
+    }
+    const int sr = tid >> 2, sk = (tid & 3) * 4;  // this thread's 4 values of a step
+    const float* src = A + sr * SS + sk;
+    constexpr int PP = TM * STG;  // bf16 per plane
+    float4 x = *reinterpret_cast<const float4*>(src);
+#pragma unroll
+    for (int q = 0; q < nq; ++q) {
+        // split this thread's 4 values of step q into the stage
+        {
+            const float v[4] = {x.x, x.y, x.z, x.w};
+            typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+            bf16x4 ph, pm, pl;
+            for (int j = 0; j < 4; ++j) {
+                const __bf16 hb = (__bf16)v[j];
+                const float r = v[j] - (float)hb;
+                const __bf16 mb = (__bf16)r;
+                ph[j] = hb;
+                pm[j] = mb;
+                pl[j] = (__bf16)(r - (float)mb);
+            }
+            __bf16* d = stage + sr * STG + sk;
+            *reinterpret_cast<bf16x4*>(d) = ph;
+            *reinterpret_cast<bf16x4*>(d + PP) = pm;
+            *reinterpret_cast<bf16x4*>(d + 2 * PP) = pl;
+        }
+        if (q + 1 < nq) {
+            x = *reinterpret_cast<const float4*>(src + 16 * (q + 1));
+            for (int p = 0; p < 3; ++p) {
+                nb0[p] = B0[p * PL + (q + 1) * STEP];
+                nb1[p] = B1[p * PL + (q + 1) * STEP];
+            }
+        }
+        __syncthreads();
+        Split3 sa[2];
+        for (int rt = 0; rt < 2; ++rt) {
+            const __bf16* f = stage + (rt * 32 + l32) * STG + 8 * h;
+            sa[rt].h = *reinterpret_cast<const bf16x8*>(f);
+            sa[rt].m = *reinterpret_cast<const bf16x8*>(f + PP);
+            sa[rt].l = *reinterpret_cast<const bf16x8*>(f + 2 * PP);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) {
+            acc[rt][0] = mfma_x6b(sa[rt], b0, acc[rt][0]);
+            acc[rt][1] = mfma_x6b(sa[rt], b1, acc[rt][1]);
+        }
+        if (q + 1 < nq)
+            for (int p = 0; p < 3; ++p) {
+                b0[p] = nb0[p];
+                b1[p] = nb1[p];
+            }
+    }
+}
+
 // A pre-split in LDS: planes [3][TM][HP + 8] bf16, written once per layer; 8 waves, wave w owns
 // column tile w of both row tiles
 constexpr int PS = HP + 8;  // plane row stride (bf16)
@@ -499,6 +572,8 @@ __global__ __launch_bounds__(kBlock, 1) void k_probe(const float* rows, const fl
             gemm_x6<false, true>(act, Bs, acc);
         else if (MODE == 5)
             gemm_x6<true, false>(act, Bs, acc);
+        else if (MODE == 10)
+            gemm_x6_coop(act, reinterpret_cast<__bf16*>(act + TM * SS), Bs, acc);
         else if (MODE == 7)
             gemm_x6f<false>(act, Bs, acc);
         else if (MODE == 8)
@@ -567,7 +642,7 @@ int main() {
     hipMemcpy(d_rows, rows.data(), rows.size() * 4, hipMemcpyHostToDevice);
     hipMemcpy(d_Bf, Bf.data(), Bf.size() * 4, hipMemcpyHostToDevice);
     hipMemcpy(d_Bs, Bs.data(), Bs.size() * 2, hipMemcpyHostToDevice);
-    const size_t lds = (size_t)TM * SS * 4;
+    const size_t lds = (size_t)TM * SS * 4 + (size_t)3 * TM * STG * 2;
     // fp64 reference of workgroup 0
     std::vector<double> ref(TM * HP), nxt(TM * HP);
     for (int i = 0; i < TM * HP; ++i) ref[i] = rows[i];
@@ -580,9 +655,10 @@ int main() {
             }
         ref.swap(nxt);
     }
-    for (int mode = 0; mode < 10; ++mode) {
+    for (int mode = 0; mode < 11; ++mode) {
         auto k = mode == 0 ? k_probe<0> : mode == 1 ? k_probe<1> : mode == 2 ? k_probe<2> : mode == 4 ? k_probe<4> : mode == 5 ? k_probe<5> : mode == 6 ? k_probe<6> : mode == 7 ? k_probe<7> : k_probe<8>;
         if (mode == 9) k = k_probe<1>;
+        if (mode == 10) k = k_probe<10>;
         const size_t lds_pl = (size_t)3 * TM * PS * 2;
         auto launch = [&]() {
             if (mode == 9)
@@ -621,7 +697,7 @@ int main() {
         }
         printf("{\"mode\": \"%s\", \"us\": %.1f, \"TFs\": %.1f, \"max_abs_err\": %.3e, "
                "\"max_ref\": %.3e, \"rel_rms_err\": %.3e}\n",
-               mode == 0 ? "f32" : mode == 1 ? "bf16x6" : mode == 2 ? "bf16x6_interleaved" : mode == 3 ? "bf16x6_lds_planes_8w" : mode == 4 ? "x6_nosplit" : mode == 5 ? "x6_noBload" : mode == 6 ? "x6_nosplit_noBload" : mode == 7 ? "x6_fenced" : mode == 8 ? "x6_fenced_interleaved" : "x6_rt4_128rows_1wg", us, flop / us / 1e6, maxe, maxr, sqrt(sum2 / ref2));
+               mode == 0 ? "f32" : mode == 1 ? "bf16x6" : mode == 2 ? "bf16x6_interleaved" : mode == 3 ? "bf16x6_lds_planes_8w" : mode == 4 ? "x6_nosplit" : mode == 5 ? "x6_noBload" : mode == 6 ? "x6_nosplit_noBload" : mode == 7 ? "x6_fenced" : mode == 8 ? "x6_fenced_interleaved" : mode == 9 ? "x6_rt4_128rows_1wg" : "x6_coop_split_stage", us, flop / us / 1e6, maxe, maxr, sqrt(sum2 / ref2));
     }
     return 0;
 }
