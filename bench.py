@@ -48,7 +48,8 @@ REGION_KERNEL = {"critic_rows": "k_td3_critic_rows", "actor_rows": "k_td3_actor_
                  "mlp_bwd": "k_mlp_bwd", "mlp_wgrad": "k_wgrad", "act": "k_mlp_fwd",
                  "agent_step": "k_agent_step", "env_step": "k_env_step",
                  "act_tick": "k_mlp_fwd<tick>", "env_step_k": "k_env_step_k",
-                 "grad_reduce": "k_grad_reduce", "demo_reward": "k_demo_reward_idx"}
+                 "grad_reduce": "k_grad_reduce", "demo_reward": "k_demo_reward_idx",
+                 "wgrad_step": "k_wgrad_step"}
 
 
 def pmc_traffic(region):

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define NAV_ABI_VERSION 7
+#define NAV_ABI_VERSION 8
 #define NAV_EINVAL (-100000)
 
 #define NAV_WORLD_CELLS 100 /* field = float32 [100][100][2] (speed, angle), x-major: cell cx*100+cy
@@ -410,6 +410,27 @@ int nav_grad_reduce_adam_polyak(const nav_mlp* nets, int32_t n_nets,
                                 const float* bc2_sqrt, const nav_mlp* net_targets,
                                 const nav_mlp* targets, const nav_mlp* sources, int32_t n_pairs,
                                 float tau, void* stream);
+/* nav_mlp_wgrad + nav_grad_reduce_adam(_polyak) in ONE launch (the product path of
+ * robot.py:236-239, 357-363, 283-285): the weight-gradient tiles, the edge-slab reduce and the Adam
+ * step (and the soft updates) as one grid in which no workgroup waits on another — the last
+ * workgroup to finish a tile (an arrival counter in `tickets`) reduces its split slabs and steps
+ * its hidden weights, the last of all steps the edge parameters (which every tile reads).
+ * Arguments as nav_mlp_wgrad followed by nav_grad_reduce_adam_polyak; grads[i] (required) receive
+ * the reduced gradients. m == NULL: no Adam (the reduce of nav_grad_reduce_multi for the shared
+ * policy's collective; net_targets NULL and n_pairs 0). net_targets NULL / n_pairs 0: no soft
+ * update. tickets: NAV_WGRAD_TICKETS int32, zero before the first launch and left zero by every
+ * launch (one buffer per stream; launches on one stream may share it). Bit-identical to the
+ * unfused launches. */
+#define NAV_WGRAD_TICKETS 256
+int nav_mlp_wgrad_step(const nav_mlp* nets, int32_t n_nets, int64_t M, const float* in,
+                       int32_t ld_in, int32_t in_col, const float* const* acts,
+                       const float* const* dz, const float* const* dy, int32_t ld_dy,
+                       const uint16_t* const* masks, float* const* slabs, int32_t splits,
+                       const float* const* edge_slabs, int64_t edge_blocks, float* const* grads,
+                       float* const* m, float* const* v, float beta1, float beta2, float eps,
+                       const float* step_size, const float* bc2_sqrt, const nav_mlp* net_targets,
+                       const nav_mlp* targets, const nav_mlp* sources, int32_t n_pairs, float tau,
+                       int32_t* tickets, void* stream);
 /* nav_grad_reduce of 1 or 2 same-shape networks in one launch (the twin critics' gradients into
  * one contiguous bucket for the shared-policy all-reduce). */
 int nav_grad_reduce_multi(const nav_mlp* nets, int32_t n_nets, const float* const* hidden_slabs,

@@ -516,20 +516,50 @@ NAV_DEV void wgrad_rows_mfma(const WgradArgs& a, int y, int n0, int k0, int64_t 
     }
 }
 
-// grid: nets x tile jobs x splits workgroups of 8 waves. Block order is XCD-grouped (blocks b and
-// b + 8 share an XCD's L2): the tile jobs of one (net, split) — which read the same rows — are
-// consecutive in the virtual order v and land on one XCD.
-__global__ __launch_bounds__(WG_THREADS) void k_wgrad(WgradArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int total = gridDim.x;
-    const int b = blockIdx.x;
+// One workgroup's tile job: network y, hidden layer L, output tile (n0.., k0..), row split.
+// Workgroups b of a grid of `total`: nets x tile jobs x splits. Block order is XCD-grouped
+// (blocks b and b + 8 share an XCD's L2): the tile jobs of one (net, split) — which read the same
+// rows — are consecutive in the virtual order v and land on one XCD.
+struct TileJob {
+    int y, job, split, L, n0, k0;
+};
+NAV_DEV TileJob wgrad_job(const WgradArgs& a, int b, int total) {
     const int v = (total % 8 == 0) ? (b % 8) * (total / 8) + b / 8 : b;
-    const int grp = v / a.n_hid, job = v % a.n_hid;
-    const int y = grp / a.splits, split = grp % a.splits;
+    const int grp = v / a.n_hid, TT = a.TT;
+    TileJob t;
+    t.job = v % a.n_hid;
+    t.y = grp / a.splits;
+    t.split = grp % a.splits;
+    t.L = t.job / (TT * TT) + 1;
+    t.n0 = ((t.job % (TT * TT)) / TT) * WG_TILE;
+    t.k0 = (t.job % TT) * WG_TILE;
+    return t;
+}
+
+// device-scope (coherent across the XCDs' L2s) 32-bit store / load: what the fused step's
+// workgroups hand each other goes through these, so no L2 writeback or invalidate is needed
+NAV_DEV void st_dev(float* p, float v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+NAV_DEV float ld_dev(const float* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+NAV_DEV void st_dev4(float4* p, float4 v) {
+    float* q = reinterpret_cast<float*>(p);
+    st_dev(q, v.x); st_dev(q + 1, v.y); st_dev(q + 2, v.z); st_dev(q + 3, v.w);
+}
+NAV_DEV float4 ld_dev4(const float4* p) {
+    const float* q = reinterpret_cast<const float*>(p);
+    return make_float4(ld_dev(q), ld_dev(q + 1), ld_dev(q + 2), ld_dev(q + 3));
+}
+
+// The tile job's partial over its split's rows, written as one slab tile (8 waves' partials
+// summed in wave order); DEV: with device-scope stores (the fused step's tile tail reads them)
+template <bool DEV>
+NAV_DEV void wgrad_tile(const WgradArgs& a, const TileJob& t, float* smem) {
+    const int y = t.y, split = t.split, L = t.L, n0 = t.n0, k0 = t.k0;
     const MlpDev& net = a.net[y];
-    const int hp = net.hp, nh = net.n_hidden, TT = a.TT;
-    const int L = job / (TT * TT) + 1;
-    const int n0 = ((job % (TT * TT)) / TT) * WG_TILE, k0 = (job % TT) * WG_TILE;
+    const int hp = net.hp, nh = net.n_hidden;
     const int wv = wave_id(), lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
     const int64_t M = a.M;
     const int64_t s_lo = (int64_t)split * a.per_split < M ? (int64_t)split * a.per_split : M;
@@ -572,8 +602,17 @@ __global__ __launch_bounds__(WG_THREADS) void k_wgrad(WgradArgs a) {
         float s = red[idx];
 #pragma unroll
         for (int w = 1; w < WG_WAVES; ++w) s += red[w * WG_TILE * WG_TILE + idx];
-        if (n0 + m < hp && k0 + c < hp) o[(int64_t)(n0 + m) * hp + k0 + c] = s;
+        if (n0 + m < hp && k0 + c < hp) {
+            if (DEV) st_dev(o + (int64_t)(n0 + m) * hp + k0 + c, s);
+            else o[(int64_t)(n0 + m) * hp + k0 + c] = s;
+        }
     }
+}
+
+// grid: nets x tile jobs x splits workgroups of 8 waves
+__global__ __launch_bounds__(WG_THREADS) void k_wgrad(WgradArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    wgrad_tile<false>(a, wgrad_job(a, blockIdx.x, gridDim.x), smem);
 }
 
 // ---------------- optimizer / target update, refreshing the packed images ----------------
@@ -672,10 +711,9 @@ struct RedArgs {
     int red_blocks;
 };
 
-template <bool ADAM>
-NAV_DEV void red_out(const RedArgs& a, const RedNet& rn, int64_t flat4, float4 g) {
-    if (rn.grad) rn.grad[flat4] = g;
-    if (!ADAM) return;
+// Adam on the float4 of parameters at flat4 with its finished gradient g, the packed images and
+// the net's own target (when soft-updated in the launch)
+NAV_DEV void adam_out(const RedArgs& a, const RedNet& rn, int64_t flat4, float4 g) {
     float4 pp = rn.p[flat4], mm = rn.m[flat4], vv = rn.v[flat4];
     adam1(pp.x, g.x, mm.x, vv.x, a.b1w, a.b2, a.omb2, a.eps, rn.step_size, rn.bc2s);
     adam1(pp.y, g.y, mm.y, vv.y, a.b1w, a.b2, a.omb2, a.eps, rn.step_size, rn.bc2s);
@@ -694,6 +732,12 @@ NAV_DEV void red_out(const RedArgs& a, const RedNet& rn, int64_t flat4, float4 g
         rn.tgt[flat4] = t;
         if (rn.tpk.packed) repack(rn.tpk, flat4 * 4, t);
     }
+}
+
+template <bool ADAM>
+NAV_DEV void red_out(const RedArgs& a, const RedNet& rn, int64_t flat4, float4 g) {
+    if (rn.grad) rn.grad[flat4] = g;
+    if (ADAM) adam_out(a, rn, flat4, g);
 }
 
 // soft update of element i of the pairs' concatenation (k_polyak_multi's body)
@@ -760,16 +804,19 @@ __global__ __launch_bounds__(kBlock) void k_grad_reduce(RedArgs a) {
     const int64_t o = (int64_t)(b - rn.nbh) * 16 + ec;
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
     if (o < e4) {
+        // 16 loads in flight per trip: a thread's 32 blocks (the bench's 512 / 16 groups) in two
+        // memory round trips instead of eight (the launch's critical path)
         const float4* col = rn.es + o;
         int64_t k = eg;
 #pragma unroll 1
-        for (; k + 48 < a.nblk; k += 64) {
-            const float4 v0 = col[k * e4], v1 = col[(k + 16) * e4], v2 = col[(k + 32) * e4],
-                         v3 = col[(k + 48) * e4];
-            s.x += v0.x; s.y += v0.y; s.z += v0.z; s.w += v0.w;
-            s.x += v1.x; s.y += v1.y; s.z += v1.z; s.w += v1.w;
-            s.x += v2.x; s.y += v2.y; s.z += v2.z; s.w += v2.w;
-            s.x += v3.x; s.y += v3.y; s.z += v3.z; s.w += v3.w;
+        for (; k + 240 < a.nblk; k += 256) {
+            float4 v[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) v[u] = col[(k + 16 * u) * e4];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w;
+            }
         }
         for (; k < a.nblk; k += 16) {
             const float4 v = col[k * e4];
@@ -787,6 +834,163 @@ __global__ __launch_bounds__(kBlock) void k_grad_reduce(RedArgs a) {
         r.x += v.x; r.y += v.y; r.z += v.z; r.w += v.w;
     }
     red_out<ADAM>(a, rn, edge_to_flat(net, 4 * o) / 4, r);
+}
+
+// ---------------- weight gradients + reduce + Adam in one launch ----------------
+// k_wgrad, k_grad_reduce's two parts and (optionally) the soft updates as one grid of 8-wave
+// workgroups, with no workgroup ever waiting on another (arrival counters, no spinning):
+//  - edge workgroups [0, E): two 256-thread halves, each one k_grad_reduce edge block (same
+//    columns, same order), writing the finished edge gradient to grads;
+//  - tile workgroups [E, E + W): k_wgrad's tile jobs. After its slab tile a workgroup takes a
+//    ticket on its tile; the one that arrives last (splits - 1 before it) sums the tile's split
+//    slabs in k_grad_reduce's order and applies Adam (+ the net's own target soft update) to the
+//    tile's hidden weights;
+//  - soft-update workgroups [E + W, E + W + P): the extra (target, source) pairs (grid stride).
+// The edge parameters (W0, the biases, Wo) are read by every tile workgroup (h_0 and dz of the
+// top layer are recomputed from them), so their Adam step waits for the last arrival of ALL edge
+// and tile workgroups (a second ticket): that workgroup reads the edge gradients back and steps
+// them. Tickets reset themselves (the last arrival zeroes its counter). The slabs and edge
+// gradients cross XCDs (each with its own L2): they are stored and read back with device-scope
+// accesses, and a workgroup's stores complete before its ticket (take_ticket).
+// Everything is bit-identical to nav_mlp_wgrad + nav_grad_reduce(_adam)(_polyak).
+struct WgradStepArgs {
+    WgradArgs w;
+    RedArgs r;
+    int* tickets;     // [n_nets * n_hid] tile arrivals, then [1] all arrivals
+    int edge_wgs, tile_wgs, poly_wgs;
+    int edge_virt;    // k_grad_reduce edge blocks over all nets (two per edge workgroup)
+    int n_nets;
+};
+
+// Arrival on a counter: every wave waits until its device-scope stores have completed, then one
+// device-scope atomic; the returned count goes to every thread through LDS. (A C++ device-scope
+// fence here would write back and invalidate the XCD's whole L2 per wave, thrashing the
+// workgroups still in their row loops: +100 us per launch, profiles/r03y.)
+NAV_DEV int take_ticket(int* counter, int* slot) {
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (threadIdx.x == 0)
+        *slot = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int t = *slot;
+    __syncthreads();  // the slot may be reused by the next ticket
+    return t;
+}
+
+template <bool ADAM>
+__global__ __launch_bounds__(WG_THREADS) void k_wgrad_step(WgradStepArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    __shared__ int s_ticket;
+    const RedArgs& ra = a.r;
+    int b = blockIdx.x;
+    int* all_ctr = a.tickets + a.n_nets * a.w.n_hid;
+    const int participants = a.edge_wgs + a.tile_wgs;
+    // the last of all edge and tile workgroups: Adam on every edge parameter
+    auto edge_adam = [&]() {
+        for (int q = 0; q < 2; ++q) {
+            const RedNet& rn = ra.n[q];
+            if (rn.nbe == 0) continue;
+            const int64_t e4 = edge_count(rn.net) / 4;
+            for (int64_t o = threadIdx.x; o < e4; o += WG_THREADS) {
+                const int64_t f4 = edge_to_flat(rn.net, 4 * o) / 4;
+                adam_out(ra, rn, f4, ld_dev4(rn.grad + f4));
+            }
+        }
+        if (threadIdx.x == 0) __hip_atomic_store(all_ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    if (b < a.edge_wgs) {
+        // k_grad_reduce's edge block 2b + half over 256 threads
+        const int half = threadIdx.x >> 8, t = threadIdx.x & 255;
+        int ve = 2 * b + half;
+        const bool valid = ve < a.edge_virt;
+        const bool second = ve >= ra.n[0].nbe;
+        const RedNet& rn = second ? ra.n[1] : ra.n[0];
+        if (second) ve -= ra.n[0].nbe;
+        const int64_t e4 = valid ? edge_count(rn.net) / 4 : 0;
+        const int ec = t & 15, eg = t >> 4;
+        const int64_t o = (int64_t)ve * 16 + ec;
+        float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (o < e4) {
+            // k_grad_reduce's order, 16 loads in flight per trip (the few edge workgroups hold
+            // CUs that tile workgroups wait for: their time is latency, not bandwidth)
+            const float4* col = rn.es + o;
+            int64_t k = eg;
+#pragma unroll 1
+            for (; k + 240 < ra.nblk; k += 256) {
+                float4 v[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) v[u] = col[(k + 16 * u) * e4];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) {
+                    s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w;
+                }
+            }
+            for (; k < ra.nblk; k += 16) {
+                const float4 v = col[k * e4];
+                s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+            }
+        }
+        float4* gp = reinterpret_cast<float4*>(smem) + half * 256;  // [16 groups][16 columns]
+        gp[eg * 16 + ec] = s;
+        __syncthreads();
+        if (eg == 0 && o < e4) {
+            float4 r = gp[ec];
+#pragma unroll
+            for (int q = 1; q < 16; ++q) {
+                const float4 v = gp[q * 16 + ec];
+                r.x += v.x; r.y += v.y; r.z += v.z; r.w += v.w;
+            }
+            st_dev4(rn.grad + edge_to_flat(rn.net, 4 * o) / 4, r);
+        }
+        if (ADAM && take_ticket(all_ctr, &s_ticket) == participants - 1) edge_adam();
+        return;
+    }
+    b -= a.edge_wgs;
+    if (b >= a.tile_wgs) {  // the extra soft-update pairs
+        b -= a.tile_wgs;
+        for (int64_t i = (int64_t)b * WG_THREADS + threadIdx.x; i < ra.poly.total4;
+             i += (int64_t)a.poly_wgs * WG_THREADS)
+            polyak_elem(ra.poly, i);
+        return;
+    }
+    const TileJob t = wgrad_job(a.w, b, a.tile_wgs);
+    wgrad_tile<true>(a.w, t, smem);
+    const int tile = t.y * a.w.n_hid + t.job;
+    const bool last = take_ticket(a.tickets + tile, &s_ticket) == a.w.splits - 1;
+    // this workgroup's reads of the edge parameters are done: count it for their Adam step
+    const bool all_last = ADAM && take_ticket(all_ctr, &s_ticket) == participants - 1;
+    if (last) {
+        const RedNet& rn = ra.n[t.y];
+        const MlpDev& net = rn.net;
+        const int hp = net.hp;
+        const int64_t hw4 = hidden_w_count(net) / 4, per = (int64_t)hp * hp / 4;
+        for (int idx = threadIdx.x; idx < WG_TILE * WG_TILE / 4; idx += WG_THREADS) {
+            const int m = idx / (WG_TILE / 4), c = 4 * (idx % (WG_TILE / 4));
+            if (t.n0 + m >= hp || t.k0 + c >= hp) continue;
+            const int64_t i = ((int64_t)(t.L - 1) * hp * hp + (int64_t)(t.n0 + m) * hp + t.k0 + c) / 4;
+            // k_grad_reduce's order: group g = split % 4 summed in split order, then the groups
+            const float4* col = rn.hs + i;
+            float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0, s2 = s0, s3 = s0;
+            auto add = [](float4& d, const float4 v) { d.x += v.x; d.y += v.y; d.z += v.z; d.w += v.w; };
+            int k = 0;
+            for (; k + 3 < a.w.splits; k += 4) {
+                add(s0, ld_dev4(col + (int64_t)k * hw4));
+                add(s1, ld_dev4(col + (int64_t)(k + 1) * hw4));
+                add(s2, ld_dev4(col + (int64_t)(k + 2) * hw4));
+                add(s3, ld_dev4(col + (int64_t)(k + 3) * hw4));
+            }
+            if (k < a.w.splits) add(s0, ld_dev4(col + (int64_t)k * hw4));
+            if (k + 1 < a.w.splits) add(s1, ld_dev4(col + (int64_t)(k + 1) * hw4));
+            if (k + 2 < a.w.splits) add(s2, ld_dev4(col + (int64_t)(k + 2) * hw4));
+            float4 r = s0;
+            add(r, s1);
+            add(r, s2);
+            add(r, s3);
+            red_out<ADAM>(ra, rn, net.w_off[t.L] / 4 + i % per, r);
+        }
+        if (threadIdx.x == 0) __hip_atomic_store(a.tickets + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (all_last) edge_adam();
 }
 
 
@@ -953,12 +1157,11 @@ int32_t nav_mlp_wgrad_splits(int32_t n_nets, int32_t hidden_pad, int32_t n_hidde
     return (int32_t)(s < 1 ? 1 : s);
 }
 
-int nav_mlp_wgrad(const nav_mlp* nets, int32_t n_nets, int64_t M, const float* in,
-                  int32_t ld_in, int32_t in_col, const float* const* acts,
-                  const float* const* dz, const float* const* dy, int32_t ld_dy,
-                  const uint16_t* const* masks, float* const* slabs, int32_t splits,
-                  void* stream) {
-    WgradArgs a{};
+static int wgrad_args(const nav_mlp* nets, int32_t n_nets, int64_t M, const float* in,
+                      int32_t ld_in, int32_t in_col, const float* const* acts,
+                      const float* const* dz, const float* const* dy, int32_t ld_dy,
+                      const uint16_t* const* masks, float* const* slabs, int32_t splits,
+                      WgradArgs& a) {
     if (!nets || n_nets < 1 || n_nets > 2 || M < 1 || splits < 1 || !in || !dy || ld_dy < 0 ||
         !masks || !slabs)
         return NAV_EINVAL;
@@ -975,7 +1178,6 @@ int nav_mlp_wgrad(const nav_mlp* nets, int32_t n_nets, int64_t M, const float* i
         a.slabs[i] = slabs[i];
     }
     if (in_col < 0 || in_col + a.net[0].d_in > ld_in) return NAV_EINVAL;
-    if (a.net[0].n_hidden < 2) return 0;
     a.M = M;
     a.in = in;
     a.ld_in = ld_in;
@@ -987,8 +1189,21 @@ int nav_mlp_wgrad(const nav_mlp* nets, int32_t n_nets, int64_t M, const float* i
     // 64-row aligned splits and per-wave ranges: a chunk's mask row tiles start on a tile boundary
     a.per_split = ((M + splits - 1) / splits + WG_CHUNK - 1) / WG_CHUNK * WG_CHUNK;
     a.per_wave = ((a.per_split + WG_WAVES - 1) / WG_WAVES + WG_CHUNK - 1) / WG_CHUNK * WG_CHUNK;
+    if ((int64_t)n_nets * a.n_hid * splits > ((int64_t)1 << 30)) return NAV_EINVAL;
+    return 0;
+}
+
+int nav_mlp_wgrad(const nav_mlp* nets, int32_t n_nets, int64_t M, const float* in,
+                  int32_t ld_in, int32_t in_col, const float* const* acts,
+                  const float* const* dz, const float* const* dy, int32_t ld_dy,
+                  const uint16_t* const* masks, float* const* slabs, int32_t splits,
+                  void* stream) {
+    WgradArgs a{};
+    const int rc = wgrad_args(nets, n_nets, M, in, ld_in, in_col, acts, dz, dy, ld_dy, masks,
+                              slabs, splits, a);
+    if (rc) return rc;
+    if (a.net[0].n_hidden < 2) return 0;
     const int64_t blocks = (int64_t)n_nets * a.n_hid * splits;
-    if (blocks > ((int64_t)1 << 30)) return NAV_EINVAL;
     const size_t lds = wgrad_lds_bytes();
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wgrad),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -1070,30 +1285,36 @@ int nav_adam_multi(const nav_mlp* nets, int32_t n_nets, const float* const* grad
     return 0;
 }
 
-static int grad_reduce_adam_impl(const nav_mlp* nets, int32_t n_nets, const float* const* hidden_slabs,
-                          int32_t splits, const float* const* edge_slabs, int64_t edge_blocks,
-                          float* const* grads, float* const* m, float* const* v, float beta1,
-                          float beta2, float eps, const float* step_size, const float* bc2_sqrt,
-                          const nav_mlp* net_targets, const nav_mlp* targets,
-                          const nav_mlp* sources, int32_t n_pairs, float tau, void* stream) {
-    RedArgs a{};
+// RedArgs of the reduce (+ Adam when m is non-NULL, + the soft updates): *blocks = the reduce
+// blocks of k_grad_reduce (a.red_blocks) plus its soft-update blocks
+static int red_args(const nav_mlp* nets, int32_t n_nets, const float* const* hidden_slabs,
+                    int32_t splits, const float* const* edge_slabs, int64_t edge_blocks,
+                    float* const* grads, float* const* m, float* const* v, float beta1,
+                    float beta2, float eps, const float* step_size, const float* bc2_sqrt,
+                    const nav_mlp* net_targets, const nav_mlp* targets, const nav_mlp* sources,
+                    int32_t n_pairs, float tau, RedArgs& a, int* blocks_out) {
+    const bool adam = m != nullptr;
     if (!nets || n_nets < 1 || n_nets > 2 || !hidden_slabs || !edge_slabs || edge_blocks < 1 ||
-        splits < 0 || !m || !v || !step_size || !bc2_sqrt || n_pairs < 0 || n_pairs > 4 ||
-        (n_pairs && (!targets || !sources)))
+        splits < 0 || (adam && (!v || !step_size || !bc2_sqrt)) || n_pairs < 0 || n_pairs > 4 ||
+        (n_pairs && (!targets || !sources)) || (!adam && (n_pairs || net_targets || !grads)))
         return NAV_EINVAL;
     int blocks = 0;
     for (int i = 0; i < n_nets; ++i) {
         RedNet& rn = a.n[i];
-        if (!edge_slabs[i] || !m[i] || !v[i] ||
+        if (!edge_slabs[i] || (adam && (!m[i] || !v[i])) || (!adam && !grads[i]) ||
             !red_net(&nets[i], hidden_slabs[i], splits, edge_slabs[i], grads ? grads[i] : nullptr,
                      &rn))
             return NAV_EINVAL;
-        rn.p = reinterpret_cast<float4*>(nets[i].params);
-        rn.m = reinterpret_cast<float4*>(m[i]);
-        rn.v = reinterpret_cast<float4*>(v[i]);
-        rn.step_size = step_size[i];
-        rn.bc2s = bc2_sqrt[i];
-        rn.pk = pack_info(rn.net, nets[i].packed);
+        if (rn.net.hp != a.n[0].net.hp || rn.net.n_hidden != a.n[0].net.n_hidden)
+            return NAV_EINVAL;
+        if (adam) {
+            rn.p = reinterpret_cast<float4*>(nets[i].params);
+            rn.m = reinterpret_cast<float4*>(m[i]);
+            rn.v = reinterpret_cast<float4*>(v[i]);
+            rn.step_size = step_size[i];
+            rn.bc2s = bc2_sqrt[i];
+            rn.pk = pack_info(rn.net, nets[i].packed);
+        }
         if (net_targets) {
             MlpDev dt;
             if (!make_dev(&net_targets[i], &dt) || dt.count != rn.net.count ||
@@ -1127,8 +1348,71 @@ static int grad_reduce_adam_impl(const nav_mlp* nets, int32_t n_nets, const floa
     a.b2 = beta2;
     a.omb2 = 1.0f - beta2;
     a.eps = eps;
+    *blocks_out = blocks;
+    return 0;
+}
+
+static int grad_reduce_adam_impl(const nav_mlp* nets, int32_t n_nets, const float* const* hidden_slabs,
+                          int32_t splits, const float* const* edge_slabs, int64_t edge_blocks,
+                          float* const* grads, float* const* m, float* const* v, float beta1,
+                          float beta2, float eps, const float* step_size, const float* bc2_sqrt,
+                          const nav_mlp* net_targets, const nav_mlp* targets,
+                          const nav_mlp* sources, int32_t n_pairs, float tau, void* stream) {
+    RedArgs a{};
+    int blocks = 0;
+    if (!m) return NAV_EINVAL;
+    const int rc = red_args(nets, n_nets, hidden_slabs, splits, edge_slabs, edge_blocks, grads, m,
+                            v, beta1, beta2, eps, step_size, bc2_sqrt, net_targets, targets,
+                            sources, n_pairs, tau, a, &blocks);
+    if (rc) return rc;
     hipLaunchKernelGGL(k_grad_reduce<true>, dim3((unsigned)blocks), dim3(kBlock), 0, S(stream),
                        a);
+    NAV_CHECK_LAUNCH();
+    return 0;
+}
+
+int nav_mlp_wgrad_step(const nav_mlp* nets, int32_t n_nets, int64_t M, const float* in,
+                       int32_t ld_in, int32_t in_col, const float* const* acts,
+                       const float* const* dz, const float* const* dy, int32_t ld_dy,
+                       const uint16_t* const* masks, float* const* slabs, int32_t splits,
+                       const float* const* edge_slabs, int64_t edge_blocks, float* const* grads,
+                       float* const* m, float* const* v, float beta1, float beta2, float eps,
+                       const float* step_size, const float* bc2_sqrt, const nav_mlp* net_targets,
+                       const nav_mlp* targets, const nav_mlp* sources, int32_t n_pairs, float tau,
+                       int32_t* tickets, void* stream) {
+    WgradStepArgs a{};
+    int rblocks = 0;
+    if (!tickets || !grads) return NAV_EINVAL;
+    int rc = wgrad_args(nets, n_nets, M, in, ld_in, in_col, acts, dz, dy, ld_dy, masks, slabs,
+                        splits, a.w);
+    if (rc) return rc;
+    rc = red_args(nets, n_nets, reinterpret_cast<const float* const*>(slabs), splits, edge_slabs,
+                  edge_blocks, grads, m, v, beta1, beta2, eps, step_size, bc2_sqrt, net_targets,
+                  targets, sources, n_pairs, tau, a.r, &rblocks);
+    if (rc) return rc;
+    if (n_nets * a.w.n_hid + 1 > NAV_WGRAD_TICKETS) return NAV_EINVAL;
+    a.tickets = tickets;
+    a.n_nets = n_nets;
+    a.tile_wgs = n_nets * a.w.n_hid * splits;
+    a.edge_virt = 0;
+    for (int i = 0; i < n_nets; ++i) a.edge_virt += a.r.n[i].nbe;
+    a.edge_wgs = (a.edge_virt + 1) / 2;
+    a.poly_wgs = n_pairs ? (int)((a.r.poly.total4 + WG_THREADS - 1) / WG_THREADS < 64
+                                     ? (a.r.poly.total4 + WG_THREADS - 1) / WG_THREADS : 64)
+                         : 0;
+    const int64_t blocks = (int64_t)a.edge_wgs + a.tile_wgs + a.poly_wgs;
+    const size_t lds = wgrad_lds_bytes();
+    if (m) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wgrad_step<true>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL(k_wgrad_step<true>, dim3((unsigned)blocks), dim3(WG_THREADS), lds,
+                           S(stream), a);
+    } else {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wgrad_step<false>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL(k_wgrad_step<false>, dim3((unsigned)blocks), dim3(WG_THREADS), lds,
+                           S(stream), a);
+    }
     NAV_CHECK_LAUNCH();
     return 0;
 }

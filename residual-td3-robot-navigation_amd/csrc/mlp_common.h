@@ -185,6 +185,9 @@ NAV_DEV size_t mask_idx(int64_t rowtile, int NT_, int t, int lane) {
 
 constexpr int kWaves = kBlock / 64;
 
+#ifndef NAV_PHASE_FENCE
+#define NAV_PHASE_FENCE 1
+#endif
 // Phase timing probe (variant builds with -DNAV_PHASE_TRACE only; tools/phase_trace.py): s_memtime
 // at numbered marks, per wave of 4 traced workgroups of the row kernels.
 #ifdef NAV_PHASE_TRACE
@@ -196,6 +199,12 @@ __device__ unsigned long long g_phase_trace[4][kBlock / 64][64];
         if (tw_ >= 0 && (threadIdx.x & 63) == 0 && (k) >= 0 && (k) < 64)                        \
             g_phase_trace[tw_][threadIdx.x >> 6][(k)] = __builtin_readcyclecounter();          \
     } while (0)
+#elif NAV_PHASE_FENCE
+// The phase marks are scheduling fences: the scheduler may not move code across a phase boundary
+// (layer 0, the GEMM, the output layer, the epilogues). Without them it spreads one phase's
+// loads and VALU into the next phase's MFMA loop, and the 256-VGPR actor program runs 30 %
+// slower (profiles/r03zc: actor_rows 137 vs 101 us, the whole step 0.698 vs 0.668 ms).
+#define NAV_MARK(k) __builtin_amdgcn_sched_barrier(0)
 #else
 #define NAV_MARK(k) \
     do {            \

@@ -15,6 +15,10 @@
 
 namespace {
 
+#ifndef NAV_GEMM_SCHED
+#define NAV_GEMM_SCHED 0  // interleave hints in gemm_cols (A/B)
+#endif
+
 template <int NT>
 struct WaveCols {
     int t0, t1;
@@ -53,8 +57,14 @@ NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const bf16x8* __rest
     // is unconditional; its second-tile MFMAs are skipped by a scalar branch (a wave without any
     // tile reads tile 0's and issues none).
     const int t0 = wc.has0 ? wc.t0 : 0, t1 = wc.has1 ? wc.t1 : t0;
-    const bf16x8* B0 = Bs + (size_t)h * hp + t0 * 32 + l32;
-    const bf16x8* B1 = Bs + (size_t)h * hp + t1 * 32 + l32;
+    // B entries as the uniform image base + a 32-bit per-lane byte offset (SGPR base + VGPR
+    // offset addressing: one 32-bit add per load instead of a 64-bit address pair)
+    const char* Bb = reinterpret_cast<const char*>(Bs);
+    const uint32_t o0 = (uint32_t)(h * hp + t0 * 32 + l32) * 16u;
+    const uint32_t o1 = (uint32_t)(h * hp + t1 * 32 + l32) * 16u;
+    auto ldB = [&](uint32_t o, int p, int q) {
+        return *reinterpret_cast<const bf16x8*>(Bb + (o + (uint32_t)((p * PL + q * STEP) * 16)));
+    };
     // B planes PF steps ahead: one step for 64-row blocks (the register budget of the big row
     // kernels), two for 32-row blocks, whose step (12 MFMAs per wave) is shorter than an L2 hit
     constexpr int PF = RT == 1 ? 2 : 1;
@@ -64,21 +74,22 @@ NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const bf16x8* __rest
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
             const int qd = d < nq ? d : nq - 1;
-            bq0[d][p] = B0[p * PL + qd * STEP];
-            bq1[d][p] = B1[p * PL + qd * STEP];
+            bq0[d][p] = ldB(o0, p, qd);
+            bq1[d][p] = ldB(o1, p, qd);
         }
     // this thread's share of a step: 4 values of row sr at k offset sk; the stage's two 16-B
     // halves of row r are swapped when (r >> 3) & 1, which makes both the 8-B stores and the
-    // waves' 16-B fragment reads bank-conflict-free (ds_read_b128 lane groups)
-    const bool sp = tid < TM * 4;
+    // waves' 16-B fragment reads bank-conflict-free (ds_read_b128 lane groups). With 64 rows
+    // every thread has a share (no branch: the split sits in the MFMAs' basic block)
+    const bool sp = TM * 4 >= kBlock || tid < TM * 4;
     const int sr = tid >> 2, sk = (tid & 3) * 4;
     const float* src = A + sr * S_ + sk;
     __bf16* dst = stage + sr * 16 + ((((sk >> 3) ^ (sr >> 3)) & 1) << 3) + (sk & 7);
     const __bf16* frag = stage + l32 * 16 + (((h ^ (l32 >> 3)) & 1) << 3);
     float4 x = sp ? *reinterpret_cast<const float4*>(src) : make_float4(0.f, 0.f, 0.f, 0.f);
     typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-#pragma unroll
-    for (int q = 0; q < nq; ++q) {
+    // split of step q's share (x) into the stage, the next x from the LDS rows, B planes ahead
+    auto produce = [&](int q) {
         if (sp) {
             const float v[4] = {x.x, x.y, x.z, x.w};
             bf16x4 ph, pm, pl;
@@ -95,15 +106,21 @@ NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const bf16x8* __rest
             *reinterpret_cast<bf16x4*>(dst + 2 * PP) = pl;
             if (q + 1 < nq) x = *reinterpret_cast<const float4*>(src + 16 * (q + 1));
         }
-        if (q + PF < nq) {
+        // production of step q runs during step q - 1's MFMAs: the B planes loaded here are
+        // step q - 1 + PF's (steps 0 .. PF - 1 come from the prologue)
+        const int qb = q - 1 + PF;
+        if (q >= 1 && qb < nq) {
 #pragma unroll
             for (int p = 0; p < 3; ++p) {
-                bq0[(q + PF) % (PF + 1)][p] = B0[p * PL + (q + PF) * STEP];
-                bq1[(q + PF) % (PF + 1)][p] = B1[p * PL + (q + PF) * STEP];
+                bq0[qb % (PF + 1)][p] = ldB(o0, p, qb);
+                bq1[qb % (PF + 1)][p] = ldB(o1, p, qb);
             }
         }
-        __syncthreads();  // the step's stage is written
-        Split3 sa[RT];
+    };
+    Split3 sa[RT];
+    // two barriers per step: the stage is written, then read (the next step may overwrite it)
+    auto consume = [&]() {
+        __syncthreads();
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) {
             const __bf16* f = frag + rt * 32 * 16;
@@ -111,17 +128,41 @@ NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const bf16x8* __rest
             sa[rt].m = *reinterpret_cast<const bf16x8*>(f + PP);
             sa[rt].l = *reinterpret_cast<const bf16x8*>(f + 2 * PP);
         }
-        __syncthreads();  // ... and read: the next step may overwrite it
+        __syncthreads();
+    };
+    produce(0);
+    consume();
+#pragma unroll
+    for (int q = 0; q < nq; ++q) {
+        // step q + 1's production comes first in program order, so the scheduler can place it
+        // between step q's MFMAs (its stage stores follow step q's second barrier)
+        if (q + 1 < nq) produce(q + 1);
+        Split3 cur[RT];
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) cur[rt] = sa[rt];
 #ifndef NAV_AB_SKIP_GEMM
         if (wc.has0) {  // wave-uniform
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt) {
-                acc[rt][0] = mfma_x6(sa[rt], bq0[q % (PF + 1)], acc[rt][0]);
+                acc[rt][0] = mfma_x6(cur[rt], bq0[q % (PF + 1)], acc[rt][0]);
                 if (NT >= 8 || wc.has1)
-                    acc[rt][1] = mfma_x6(sa[rt], bq1[q % (PF + 1)], acc[rt][1]);
+                    acc[rt][1] = mfma_x6(cur[rt], bq1[q % (PF + 1)], acc[rt][1]);
             }
         }
 #endif
+#if NAV_GEMM_SCHED
+        // interleave: 1 MFMA, then 2 of the production's VALU / LDS / VMEM instructions
+        if constexpr (NT >= 8 && RT == 2) {
+            if (q + 1 < nq) {
+#pragma unroll
+                for (int g = 0; g < 24; ++g) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002 | 0x020 | 0x100 | 0x200, 2, 0);
+                }
+            }
+        }
+#endif
+        if (q + 1 < nq) consume();
     }
 }
 
@@ -468,6 +509,31 @@ NAV_DEV void loss_epilogue(const MlpDev& net, const f32x16 (&top)[RT][2], float*
     }
 }
 
+// Layer 0's per-lane constants (W0 columns h and 2 + h, the bias) of the wave's column tiles:
+// loaded one network pass ahead by the fused row programs, so their latency hides under the
+// previous pass instead of opening this pass's layer 0
+struct L0Pre {
+    float wa[2], wb[2], bias[2];
+};
+template <int NT>
+NAV_DEV L0Pre load_l0(const MlpDev& net) {
+    const int lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
+    const WaveCols<NT> wc(wave_id());
+    const float* W0 = net.params + net.w_off[0];
+    const float* b0 = net.params + net.b_off[0];
+    const int d_in = net.d_in;
+    L0Pre p;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const bool has = j == 0 ? wc.has0 : wc.has1;
+        const int c = (j == 0 ? wc.t0 : wc.t1) * 32 + l32;
+        p.wa[j] = has && h < d_in ? W0[c * d_in + h] : 0.f;
+        p.wb[j] = has && 2 + h < d_in ? W0[c * d_in + 2 + h] : 0.f;
+        p.bias[j] = has && h == 0 ? b0[c] : 0.f;
+    }
+    return p;
+}
+
 // One network's forward over the block's TM rows (input rows xin [TM][4] in LDS). The top hidden
 // layer stays in registers (`top`, C layout) — its LDS rows are written only when save_mask asks
 // for its global copy — and the output layer's per-wave partials land in `red` (ready for out_y
@@ -475,22 +541,24 @@ NAV_DEV void loss_epilogue(const MlpDev& net, const f32x16 (&top)[RT][2], float*
 template <int NT, int RT>
 NAV_DEV void fwd_net(const MlpDev& net, float* act, __bf16* stage, const float* xin, float* red,
                      uint16_t* masks, int64_t n_rt, float* act_save, uint32_t save_mask,
-                     int64_t row0, int64_t M, int64_t rt0, f32x16 (&top)[RT][2], int mk = -64) {
+                     int64_t row0, int64_t M, int64_t rt0, f32x16 (&top)[RT][2], int mk = -64,
+                     const L0Pre* pre = nullptr, uint32_t* top_bits = nullptr,
+                     WoCols* wo_out = nullptr) {
     constexpr int hp = NT * 32, SS = hp + 4;
     NAV_MARK(mk);
     const int tid = threadIdx.x, lane = tid & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
-    const int d_in = net.d_in, nh = net.n_hidden;
+    const int nh = net.n_hidden;
     const WaveCols<NT> wc(wv);
     (void)tid;
     // the output layer's Wo columns: issued now, in flight under layer 0 and the GEMMs
     const WoCols wo = load_wo<NT>(net);
+    if (wo_out) *wo_out = wo;
     // ---- layer 0 (K = d_in <= 4) on MFMA, straight into the C layout of the wave's column
     // tiles: the bias tile by a K = 2 product of (1, 0) x (b, 0) (exactly b), then x[:, 0:2] and
     // x[:, 2:4] against W0's columns: each element is fma(x3, w3, fma(x2, w2, fma(x1, w1,
     // fma(x0, w0, b)))) — layer0_unit's chain, bit for bit (absent inputs and weights are 0)
     {
-        const float* W0 = net.params + net.w_off[0];
-        const float* b0 = net.params + net.b_off[0];
+        const L0Pre l0 = pre ? *pre : load_l0<NT>(net);
         const f32x16 zero = {};
         const float one = h == 0 ? 1.f : 0.f;
         // A operands: row l32 of each row tile, inputs h and 2 + h
@@ -506,9 +574,8 @@ NAV_DEV void fwd_net(const MlpDev& net, float* act, __bf16* stage, const float* 
             if (!(j == 0 ? wc.has0 : wc.has1)) continue;
             const int t = j == 0 ? wc.t0 : wc.t1;
             const int c = t * 32 + l32;
-            const float wa = h < d_in ? W0[c * d_in + h] : 0.f;
-            const float wb = 2 + h < d_in ? W0[c * d_in + 2 + h] : 0.f;
-            const f32x16 bias = mfma(one, h == 0 ? b0[c] : 0.f, zero);
+            const float wa = l0.wa[j], wb = l0.wb[j];
+            const f32x16 bias = mfma(one, l0.bias[j], zero);
             float* col = act + c + 4 * h * SS;
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt) {
@@ -569,6 +636,17 @@ NAV_DEV void fwd_net(const MlpDev& net, float* act, __bf16* stage, const float* 
             copy_rows<NT, RT>(act, SS, act_save + (int64_t)L * M * hp, row0, M);
         } else if (masks) {
             store_mask<NT, RT>(top, mask_of(L), rt0);
+        }
+        if (top_bits) {  // the top layer's ReLU bits stay in registers for the row backward
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    uint32_t bits = 0;
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) bits |= (top[rt][j][i] > 0.f ? 1u : 0u) << i;
+                    top_bits[rt * 2 + j] = (j == 0 ? wc.has0 : wc.has1) ? bits : 0u;
+                }
         }
     } else {
         // the top layer is layer 0: its C-layout registers from the LDS rows just written
@@ -855,7 +933,8 @@ template <int NT, int RT>
 NAV_DEV void bwd_net(const MlpDev& net, float* act, __bf16* stage, const float* dys, const float* xin,
                      const uint16_t* masks, int64_t n_rt, float* es, const float* h_top,
                      float* dz, uint32_t save_mask, int64_t row0, int64_t M, int64_t rt0,
-                     int mk = -64) {
+                     int mk = -64, const uint32_t* top_bits = nullptr,
+                     const WoCols* wo_in = nullptr) {
     constexpr int hp = NT * 32, SS = hp + 4, TM = RT * 32;
     NAV_MARK(mk);
     const int tid = threadIdx.x, lane = tid & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
@@ -909,13 +988,22 @@ NAV_DEV void bwd_net(const MlpDev& net, float* act, __bf16* stage, const float* 
             ga[rt] = h < d_out ? (h ? g.y : g.x) : 0.f;
         }
         uint32_t mb[RT][2];
-        load_mask_bits<NT, RT>(mk, rt0, mb);
+        if (top_bits) {  // the forward's bits of this top layer, still in registers
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) mb[rt][j] = top_bits[rt * 2 + j];
+        } else {
+            load_mask_bits<NT, RT>(mk, rt0, mb);
+        }
         f32x16 z[RT][2];
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const bool has = j == 0 ? wc.has0 : wc.has1;
             const int c = (j == 0 ? wc.t0 : has ? wc.t1 : wc.t0) * 32 + l32;
-            const float wb = has && h < d_out ? Wo[h * hp + c] : 0.f;
+            // the forward's Wo registers: wo.w[output][tile] holds Wo[output][c] (0 when absent)
+            const float wb = wo_in ? (h ? wo_in->w[1][j] : wo_in->w[0][j])
+                                   : has && h < d_out ? Wo[h * hp + c] : 0.f;
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt) z[rt][j] = mfma(ga[rt], wb, zero);
         }
@@ -1075,6 +1163,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
     float* dys = qv + TM;          // [TM][4] dL/dq rows of the row backward
     __bf16* stage = reinterpret_cast<__bf16*>(dys + TM * 4);  // gemm_cols' split stage
     NAV_MARK(0);
+    const L0Pre l0_at = load_l0<NT>(a.actor_t);  // in flight under the sampling
     // target policy smoothing noise of (row, output) tid % TM, tid / TM: clamp(policy_noise * eps,
     // +-noise_clip), formed while the sampled rows are in flight
     float tnz = 0.f;
@@ -1108,9 +1197,12 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
     }
     __syncthreads();
     NAV_MARK(1);
-    // target actor; a' = clamp(pi'(s') + clamp(policy_noise * eps, +-noise_clip), +-max_action)
+    // target actor; a' = clamp(pi'(s') + clamp(policy_noise * eps, +-noise_clip), +-max_action).
+    // Each pass's layer-0 constants are loaded one pass ahead (L0Pre).
     f32x16 top[RT][2];
-    fwd_net<NT, RT>(a.actor_t, act, stage, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0, top, 2);
+    const L0Pre l0_ct1 = load_l0<NT>(a.critic_t[0]);
+    fwd_net<NT, RT>(a.actor_t, act, stage, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0, top, 2,
+                    &l0_at);
     if (tid < 2 * TM) {
         const int rloc = tid % TM, j = tid / TM;
         const int64_t r = row0 + rloc;
@@ -1126,11 +1218,14 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
     NAV_MARK(8);
     // twin target critics on (s', a'), then y = r + gamma * min(q1', q2') * (1 - done), kept in
     // the row's thread
+    const L0Pre l0_ct2 = load_l0<NT>(a.critic_t[1]);
     fwd_net<NT, RT>(a.critic_t[0], act, stage, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0, top,
-                    9);
+                    9, &l0_ct1);
     if (tid < TM) qv[tid] = out_y<RT>(a.critic_t[0], red, tid, 0);
+    const int q0 = a.split_twins ? (int)blockIdx.y : 0;  // the first online critic of the block
+    L0Pre l0_on = load_l0<NT>(a.critic[q0]);
     fwd_net<NT, RT>(a.critic_t[1], act, stage, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0, top,
-                    15);
+                    15, &l0_ct2);
     float yt = 0.f;
     if (tid < TM) {
         const float q2 = out_y<RT>(a.critic_t[1], red, tid, 0);
@@ -1144,8 +1239,11 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
 #pragma unroll 1
     for (int q = 0; q < 2; ++q) {
         if (a.split_twins && q != (int)blockIdx.y) continue;  // workgroup-uniform
+        uint32_t top_bits[RT * 2];
+        WoCols wo;
         fwd_net<NT, RT>(a.critic[q], act, stage, xin, red, a.masks[q], n_rt, a.acts[q], a.save_mask, row0,
-                        B, rt0, top, 22 + 14 * q);
+                        B, rt0, top, 22 + 14 * q, &l0_on, top_bits, &wo);
+        if (q == 0 && !a.split_twins) l0_on = load_l0<NT>(a.critic[1]);
         float* es = a.eslab[q] ? a.eslab[q] + (int64_t)blockIdx.x * a.ecount : nullptr;
         loss_epilogue<NT, RT>(a.critic[q], top, red, row0, B, yt, a.norm, a.dq[q],
                               a.loss_part[q] + blockIdx.x, es);
@@ -1157,7 +1255,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
                     make_float4(red[kWaves * TM + tid], 0.f, 0.f, 0.f);  // loss_epilogue's dq
             __syncthreads();
             bwd_net<NT, RT>(a.critic[q], act, stage, dys, xin, a.masks[q], n_rt, es, nullptr, a.dz[q],
-                            a.dz_save_mask, row0, B, rt0, 29 + 14 * q);
+                            a.dz_save_mask, row0, B, rt0, 29 + 14 * q, top_bits, &wo);
             __syncthreads();  // the next forward's layer 0 overwrites the rows
         }
         NAV_MARK(35 + 14 * q);

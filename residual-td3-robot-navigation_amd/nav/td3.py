@@ -87,6 +87,11 @@ class TD3:
         # a policy epoch's soft updates inside the actor's reduce + Adam launch
         # (NAV_FUSE_SOFT_UPDATE=0: their own launch; A/B only)
         self.fuse_soft_update = os.environ.get("NAV_FUSE_SOFT_UPDATE", "1") != "0"
+        # weight gradients, reduce and Adam (+ the soft updates) in one launch
+        # (nav_mlp_wgrad_step; NAV_FUSE_WGRAD_STEP=0: nav_mlp_wgrad + the reduce launch, A/B only)
+        self.fuse_wgrad_step = os.environ.get("NAV_FUSE_WGRAD_STEP", "0") == "1"
+        # the step's arrival counters (zero, and left zero by every launch)
+        self.tickets = torch.zeros(256, dtype=torch.int32, device=self.device)
         self._B = 0
         self.actor_losses, self.critic_losses = [], []
 
@@ -151,10 +156,54 @@ class TD3:
 
     def _grads_and_step(self, nets, opts, M, inp, ld_in, in_col, acts, dz, dy, ld_dy, masks,
                         eslabs, grads, hslabs, s, stream, soft_update=False):
-        """Weight gradients, then the fixed-order reduce of those and the fwd/bwd edge partials
-        fused with each net's Adam step (robot.py:236-239): 2 launches for 1-2 nets. With a
-        grad_hook (shared policy) the reduce writes the flat gradient bucket, the hook
-        all-reduces it, and one multi-net Adam launch applies bucket / world_size."""
+        """Weight gradients, the fixed-order reduce of those and the fwd/bwd edge partials, and
+        each net's Adam step (robot.py:236-239) of 1-2 nets: one launch (nav_mlp_wgrad_step).
+        With a grad_hook (shared policy) the launch writes the flat gradient bucket without
+        Adam, the hook all-reduces it, and one multi-net Adam launch applies bucket /
+        world_size."""
+        if not self.fuse_wgrad_step:
+            return self._grads_and_step_unfused(nets, opts, M, inp, ld_in, in_col, acts, dz, dy,
+                                                ld_dy, masks, eslabs, grads, hslabs, s, stream,
+                                                soft_update)
+        net = nets[0]
+        splits = self.splits_a if net is self.actor_network else self.splits_c
+        n = len(nets)
+        wg = (descs(*nets), n, M, ptr(inp), ld_in, in_col, parr(*acts), parr(*dz), parr(*dy),
+              ld_dy, parr(*masks), parr(*hslabs), splits, parr(*eslabs), self.nblk, parr(*grads))
+        work = n * prof.mlp_wgrad_flops(net.hidden, net.n_hidden, M)
+        if self.grad_hook is None:
+            coeffs = [o.advance() for o in opts]
+            adam = (parr(*[o.m for o in opts]), parr(*[o.v for o in opts]), opts[0].b1,
+                    opts[0].b2, opts[0].eps, (C.c_float * n)(*[c[0] for c in coeffs]),
+                    (C.c_float * n)(*[c[1] for c in coeffs]))
+            if soft_update:  # the actor's step and all three soft updates in the same launch
+                tail = (descs(self.target_actor),
+                        descs(self.target_critic_network_1, self.target_critic_network_2),
+                        descs(self.critic_network_1, self.critic_network_2), 2, self.cfg.tau)
+            else:
+                tail = (None, None, None, 0, 0.0)
+            with prof.region("wgrad_step", work):
+                lib().nav_mlp_wgrad_step(*wg, *adam, *tail, ptr(self.tickets), s)
+            return
+        with prof.region("wgrad_step", work):
+            lib().nav_mlp_wgrad_step(*wg, None, None, 0.9, 0.999, 1e-8, None, None, None, None,
+                                     None, 0, 0.0, ptr(self.tickets), s)
+        self._hook_and_adam(nets, opts, grads, s, stream, soft_update)
+
+    def _hook_and_adam(self, nets, opts, grads, s, stream, soft_update):
+        bucket = self.grad_c if len(nets) == 2 else grads[0]
+        # the collective runs on torch's current stream: make it the launch stream, so it
+        # starts after the reduce and Adam starts after it
+        with torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext():
+            self.grad_hook(bucket)
+        self._adam(nets, opts, grads, s, self.grad_div)
+        if soft_update:
+            self.soft_update_all(stream)
+
+    def _grads_and_step_unfused(self, nets, opts, M, inp, ld_in, in_col, acts, dz, dy, ld_dy,
+                                masks, eslabs, grads, hslabs, s, stream, soft_update=False):
+        """The same as two launches: nav_mlp_wgrad, then the reduce fused with Adam (or the
+        reduce alone before the hook)."""
         splits = self._wgrad(nets, M, inp, ld_in, in_col, acts, dz, dy, ld_dy, masks, hslabs, s)
         if self.grad_hook is None:
             coeffs = [o.advance() for o in opts]
@@ -175,14 +224,7 @@ class TD3:
         with prof.region("grad_reduce", self._reduce_bytes(nets, eslabs, splits, False)):
             lib().nav_grad_reduce_multi(descs(*nets), len(nets), parr(*hslabs), splits,
                                         parr(*eslabs), self.nblk, parr(*grads), s)
-        bucket = self.grad_c if len(nets) == 2 else grads[0]
-        # the collective runs on torch's current stream: make it the launch stream, so it
-        # starts after the reduce and Adam starts after it
-        with torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext():
-            self.grad_hook(bucket)
-        self._adam(nets, opts, grads, s, self.grad_div)
-        if soft_update:
-            self.soft_update_all(stream)
+        self._hook_and_adam(nets, opts, grads, s, stream, soft_update)
 
     def _adam(self, nets, opts, grads, s, grad_div=1.0):
         """One multi-net Adam launch on flat gradients (already reduced) / grad_div."""

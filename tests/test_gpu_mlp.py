@@ -644,3 +644,99 @@ def test_reduce_adam_polyak_fused_bitwise(nav):
         assert torch.equal(a_net[0].packed, a_net[1].packed)
         for x, y in ((atgt[0], atgt[1]), (ctgt[0][0], ctgt[1][0]), (ctgt[0][1], ctgt[1][1])):
             assert torch.equal(x.params, y.params) and torch.equal(x.packed, y.packed)
+
+
+@pytest.mark.parametrize("hidden,nh,d_in,d_out,B,n_nets,pairs", [
+    (256, 2, 4, 1, 4096, 2, 0),    # the twin critics' epoch (bench shape, smaller batch)
+    (256, 2, 2, 2, 4096, 1, 2),    # the actor's policy epoch with the three soft updates
+    (200, 3, 4, 1, 777, 2, 0),     # saved middle layers, partial 64 x 64 tiles
+    (64, 1, 2, 2, 300, 1, 2),      # no hidden x hidden layer: edge workgroups only
+    (256, 2, 4, 1, 100, 2, 0)])    # config 1's batch: one split per tile
+def test_wgrad_step_fused_bitwise(nav, hidden, nh, d_in, d_out, B, n_nets, pairs):
+    """nav_mlp_wgrad_step (weight gradients + reduce + Adam (+ soft updates) in one launch, the
+    arrival-counter tail) == nav_mlp_wgrad then nav_grad_reduce_adam(_polyak), bit for bit:
+    gradients, parameters, moments, packed images, targets; twice in a row (the tickets reset
+    themselves); and with m = NULL == nav_grad_reduce_multi (the shared-policy bucket)."""
+    from nav._lib import descs, lib, parr, ptr, stream_handle
+    from nav.mlp import forward
+    L = lib()
+    s = stream_handle()
+    # two identical copies of everything the step writes: [0] unfused, [1] fused
+    nets = [[make_net(d_in, d_out, hidden, nh, 90 + k)[0] for k in range(n_nets)] for _ in range(2)]
+    tg_own = [[make_net(d_in, d_out, hidden, nh, 93 + k)[0] for k in range(n_nets)]
+              for _ in range(2)] if pairs else [None, None]
+    crit = [make_net(4, 1, hidden, nh, 95 + k)[0] for k in range(pairs)]
+    ctgt = [[make_net(4, 1, hidden, nh, 97 + k)[0] for k in range(pairs)] for _ in range(2)]
+    hp = nets[0][0].hp
+    g = torch.Generator().manual_seed(B + nh)
+    x = (torch.randn(B, d_in, generator=g) * 10).to(DEV)
+    dys = [(torch.randn(B, d_out, generator=g) / B).to(DEV) for _ in range(n_nets)]
+    nblk = L.nav_mlp_row_blocks(B)
+    ec = L.nav_mlp_edge_count(d_in, d_out, hp, nh)
+    mid = nets[0][0].middle_layers()
+    acts = [torch.zeros(nh, B, hp, device=DEV) for _ in range(n_nets)]
+    dz = [torch.zeros(nh, B, hp, device=DEV) for _ in range(n_nets)]
+    masks = [nets[0][0].mask_buffer(B) for _ in range(n_nets)]
+    es = [torch.zeros(nblk, ec, device=DEV) for _ in range(n_nets)]
+    for k in range(n_nets):
+        out = torch.zeros(B, d_out, device=DEV)
+        forward([nets[0][k]], x, d_in, 0, [out], d_out, 0, B, acts=[acts[k]],
+                save_mask=mid | nets[0][k].top_layer(), masks=[masks[k]])
+        L.nav_mlp_backward(descs(nets[0][k]), 1, B, parr(dys[k]), d_out, parr(masks[k]), ptr(x),
+                           d_in, 0, parr(acts[k][nh - 1]), parr(dz[k]), mid, None, parr(es[k]), s)
+    hc = max(4, L.nav_mlp_hidden_count(hp, nh))
+    cnt = nets[0][0].count
+    m = [[torch.randn(cnt, device=DEV) * 1e-3 for _ in range(n_nets)]]
+    v = [[torch.rand(cnt, device=DEV) * 1e-4 for _ in range(n_nets)]]
+    m.append([t.clone() for t in m[0]])
+    v.append([t.clone() for t in v[0]])
+    tickets = torch.zeros(256, dtype=torch.int32, device=DEV)
+    for splits in (L.nav_mlp_wgrad_splits(n_nets, hp, nh, B), 3):
+        for rep in range(2):
+            ss = (C.c_float * n_nets)(*[1e-3 * (rep + 1)] * n_nets)
+            bc = (C.c_float * n_nets)(*[0.5 / (rep + 1)] * n_nets)
+            grads = [[torch.full((cnt,), float("nan"), device=DEV) for _ in range(n_nets)]
+                     for _ in range(2)]
+            hs = [[torch.full((splits, hc), float("nan"), device=DEV) for _ in range(n_nets)]
+                  for _ in range(2)]
+            wg_args = lambda c: (descs(*nets[c]), n_nets, B, ptr(x), d_in, 0, parr(*acts),  # noqa: E731
+                                 parr(*dz), parr(*dys), d_out, parr(*masks), parr(*hs[c]), splits)
+            red = lambda c: (parr(*es), nblk, parr(*grads[c]), parr(*m[c]), parr(*v[c]), 0.9,  # noqa: E731
+                             0.999, 1e-8, ss, bc)
+            L.nav_mlp_wgrad(*wg_args(0), s)
+            if pairs:
+                L.nav_grad_reduce_adam_polyak(descs(*nets[0]), n_nets, parr(*hs[0]), splits,
+                                              *red(0), descs(*tg_own[0]), descs(*ctgt[0]),
+                                              descs(*crit), pairs, 0.001, s)
+                L.nav_mlp_wgrad_step(*wg_args(1), *red(1), descs(*tg_own[1]), descs(*ctgt[1]),
+                                     descs(*crit), pairs, 0.001, ptr(tickets), s)
+            else:
+                L.nav_grad_reduce_adam(descs(*nets[0]), n_nets, parr(*hs[0]), splits, *red(0), s)
+                L.nav_mlp_wgrad_step(*wg_args(1), *red(1), None, None, None, 0, 0.0,
+                                     ptr(tickets), s)
+            torch.cuda.synchronize()
+            for k in range(n_nets):
+                assert torch.equal(grads[0][k], grads[1][k]), (splits, rep, k)
+                assert torch.equal(nets[0][k].params, nets[1][k].params), (splits, rep, k)
+                assert torch.equal(nets[0][k].packed, nets[1][k].packed), (splits, rep, k)
+                assert torch.equal(m[0][k], m[1][k]) and torch.equal(v[0][k], v[1][k])
+                if pairs:
+                    assert torch.equal(tg_own[0][k].params, tg_own[1][k].params)
+                    assert torch.equal(tg_own[0][k].packed, tg_own[1][k].packed)
+            for k in range(pairs):
+                assert torch.equal(ctgt[0][k].params, ctgt[1][k].params)
+                assert torch.equal(ctgt[0][k].packed, ctgt[1][k].packed)
+            assert int(tickets.abs().sum().item()) == 0
+        # reduce only (m = NULL): the shared-policy bucket
+        gb = [[torch.full((cnt,), float("nan"), device=DEV) for _ in range(n_nets)]
+              for _ in range(2)]
+        L.nav_mlp_wgrad(*wg_args(0), s)
+        L.nav_grad_reduce_multi(descs(*nets[0]), n_nets, parr(*hs[0]), splits, parr(*es), nblk,
+                                parr(*gb[0]), s)
+        L.nav_mlp_wgrad_step(*wg_args(1), parr(*es), nblk, parr(*gb[1]), None, None, 0.9, 0.999,
+                             1e-8, None, None, None, None, None, 0, 0.0, ptr(tickets), s)
+        torch.cuda.synchronize()
+        for k in range(n_nets):
+            assert torch.isfinite(gb[1][k]).all()
+            assert torch.equal(gb[0][k], gb[1][k]), (splits, k)
+        assert int(tickets.abs().sum().item()) == 0
