@@ -634,19 +634,24 @@ NAV_DEV void fwd_net(const MlpDev& net, float* act, __bf16* stage, const float* 
             store_layer<NT, RT>(top, act, SS, mask_of(L), rt0);
             __syncthreads();
             copy_rows<NT, RT>(act, SS, act_save + (int64_t)L * M * hp, row0, M);
-        } else if (masks) {
+        } else if (masks && !top_bits) {
             store_mask<NT, RT>(top, mask_of(L), rt0);
         }
         if (top_bits) {  // the top layer's ReLU bits stay in registers for the row backward
+            uint16_t* mk = masks && !(act_save && ((save_mask >> L) & 1u)) ? mask_of(L) : nullptr;
 #pragma unroll
-            for (int rt = 0; rt < RT; ++rt)
+            for (int j = 0; j < 2; ++j) {
+                const bool has = j == 0 ? wc.has0 : wc.has1;
 #pragma unroll
-                for (int j = 0; j < 2; ++j) {
+                for (int rt = 0; rt < RT; ++rt) {
                     uint32_t bits = 0;
 #pragma unroll
                     for (int i = 0; i < 16; ++i) bits |= (top[rt][j][i] > 0.f ? 1u : 0u) << i;
-                    top_bits[rt * 2 + j] = (j == 0 ? wc.has0 : wc.has1) ? bits : 0u;
+                    top_bits[rt * 2 + j] = has ? bits : 0u;
+                    if (mk && has)
+                        mk[mask_idx(rt0 + rt, NT, j == 0 ? wc.t0 : wc.t1, lane)] = (uint16_t)bits;
                 }
+            }
         }
     } else {
         // the top layer is layer 0: its C-layout registers from the LDS rows just written
@@ -853,21 +858,29 @@ NAV_DEV void edge_regs(const MlpDev& net, const f32x16 (&z)[RT][2], const float*
     const int d_in = net.d_in;
     float sb[2] = {0.f, 0.f}, sw[2][4] = {};
     if (L == 0) {
+        // dW0's four input columns as two packed pairs (v_pk_fma_f32: the same fused op per
+        // element as fmaf, two elements per instruction)
+        typedef float f32x2 __attribute__((ext_vector_type(2)));
+        f32x2 w01[2] = {{0.f, 0.f}, {0.f, 0.f}}, w23[2] = {{0.f, 0.f}, {0.f, 0.f}};
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 const float4 x = *reinterpret_cast<const float4*>(xin + c_row(rt, i, h) * 4);
+                const f32x2 x01 = {x.x, x.y}, x23 = {x.z, x.w};
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
                     const float v = z[rt][j][i];
+                    const f32x2 vv = {v, v};
                     sb[j] += v;
-                    sw[j][0] = fmaf(v, x.x, sw[j][0]);
-                    sw[j][1] = fmaf(v, x.y, sw[j][1]);
-                    sw[j][2] = fmaf(v, x.z, sw[j][2]);
-                    sw[j][3] = fmaf(v, x.w, sw[j][3]);
+                    w01[j] = __builtin_elementwise_fma(vv, x01, w01[j]);
+                    w23[j] = __builtin_elementwise_fma(vv, x23, w23[j]);
                 }
             }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            sw[j][0] = w01[j].x; sw[j][1] = w01[j].y; sw[j][2] = w23[j].x; sw[j][3] = w23[j].y;
+        }
     } else {
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt)

@@ -93,6 +93,8 @@ class TD3:
         # the step's arrival counters (zero, and left zero by every launch)
         self.tickets = torch.zeros(256, dtype=torch.int32, device=self.device)
         self._B = 0
+        self._st = None  # the per-epoch launches' constant ctypes arguments (_static)
+        self._rd = (None, None)
         self.actor_losses, self.critic_losses = [], []
 
     # ---- workspace, sized per batch
@@ -136,6 +138,7 @@ class TD3:
         self.grad_c = f(2 * cc)
         self.grad_c1, self.grad_c2 = self.grad_c[:cc], self.grad_c[cc:]
         self._B = B
+        self._st = None
 
     def _wgrad(self, nets, M, inp, ld_in, in_col, acts, dz, dy, ld_dy, masks, hslabs, s):
         """Hidden x hidden weight gradients of 1-2 same-shape nets: one MFMA launch writing
@@ -248,6 +251,97 @@ class TD3:
                                    ld_in, in_col, parr(*(h_top or nil)), parr(*(dz or nil)),
                                    save_mask, parr(*(dx or nil)), parr(*(eslab or nil)), s)
 
+    # ---- the per-epoch launches with their constant arguments built once (the small-batch
+    # learner of config 1 is bound by the host's issue of ~450 launches per td3_update)
+    def _fast(self):
+        return (prof._active is None and self.grad_hook is None and self.row_backward and
+                not self.fuse_wgrad_step)
+
+    def _static(self):
+        st = self._st
+        if st is not None:
+            return st
+        c = self.cfg
+        B = c.batch_size
+        c1, c2, a = self.critic_network_1, self.critic_network_2, self.actor_network
+        ta, ca = self.target_actor.desc(), a.desc()
+        c1d = c1.desc()
+        mid, mida = c1.middle_layers(), a.middle_layers()
+        oc, oa = (self.critic_optimizer_1, self.critic_optimizer_2), self.actor_optimizer
+        seed = (self.seed & 0xFFFFFFFF, (self.seed >> 32) & 0xFFFFFFFF)
+        st = {
+            "keep": (ta, ca, c1d),
+            "seed": seed,
+            "cr_head": (C.byref(ta), descs(self.target_critic_network_1,
+                                           self.target_critic_network_2), descs(c1, c2)),
+            "cr_tail": (c.policy_noise, c.noise_clip, c.max_action, c.gamma, ptr(self.batch),
+                        parr(self.dq1, self.dq2), parr(self.loss_part[0], self.loss_part[1]),
+                        parr(self.eslab1, self.eslab2), parr(self.acts1, self.acts2), mid,
+                        parr(self.mask1, self.mask2), 1, parr(self.dz1, self.dz2), mid),
+            "ar_head": (C.byref(ca), C.byref(c1d)),
+            "ar_tail": (ptr(self.batch2), ptr(self.q1), ptr(self.da), ptr(self.acts_a), mida,
+                        ptr(self.dz_a), mida, ptr(self.mask_a), ptr(self.mask1),
+                        ptr(self.eslab_a)),
+        }
+        wc = self._critic_wgrad_args()
+        st["wg_c"] = (descs(c1, c2), 2, B, ptr(wc[0]), wc[1], wc[2], parr(*wc[3]), parr(*wc[4]),
+                      parr(*wc[5]), wc[6], parr(*wc[7]), parr(self.hslab, self.hslab2),
+                      self.splits_c)
+        wa = self._actor_wgrad_args()
+        st["wg_a"] = (descs(a), 1, B, ptr(wa[0]), wa[1], wa[2], parr(*wa[3]), parr(*wa[4]),
+                      parr(*wa[5]), wa[6], parr(*wa[7]), parr(self.hslab), self.splits_a)
+        st["red_c"] = (descs(c1, c2), 2, parr(self.hslab, self.hslab2), self.splits_c,
+                       parr(self.eslab1, self.eslab2), self.nblk, parr(self.grad_c1, self.grad_c2),
+                       parr(*[o.m for o in oc]), parr(*[o.v for o in oc]), oc[0].b1, oc[0].b2,
+                       oc[0].eps)
+        st["red_a"] = (descs(a), 1, parr(self.hslab), self.splits_a, parr(self.eslab_a),
+                       self.nblk, parr(self.grad_a), parr(oa.m), parr(oa.v), oa.b1, oa.b2, oa.eps)
+        st["poly"] = (descs(self.target_actor),
+                      descs(self.target_critic_network_1, self.target_critic_network_2),
+                      descs(c1, c2), 2, c.tau)
+        st["wgrad"] = c1.n_hidden > 1
+        self._st = st
+        return st
+
+    def _replay_ref(self, replay):
+        if self._rd[0] is not replay:
+            d = replay.desc()
+            self._rd = (replay, (d, C.byref(d)))
+        return self._rd[1][1]
+
+    def _critic_epoch_fast(self, replay, idx, eps, s):
+        c = self.cfg
+        B = c.batch_size
+        self._workspace(B)
+        st, L = self._static(), lib()
+        L.nav_td3_critic_rows(*st["cr_head"], self._replay_ref(replay), len(replay), B,
+                              None if idx is None else C.c_void_p(idx.data_ptr()), *st["seed"],
+                              self.update_counter,
+                              None if eps is None else C.c_void_p(eps.data_ptr()), *st["cr_tail"],
+                              s)
+        if st["wgrad"]:
+            L.nav_mlp_wgrad(*st["wg_c"], s)
+        o1, o2 = self.critic_optimizer_1.advance(), self.critic_optimizer_2.advance()
+        L.nav_grad_reduce_adam(*st["red_c"], (C.c_float * 2)(o1[0], o2[0]),
+                               (C.c_float * 2)(o1[1], o2[1]), s)
+
+    def _actor_epoch_fast(self, replay, idx, s, soft_update):
+        c = self.cfg
+        B = c.batch_size
+        self._workspace(B)
+        st, L = self._static(), lib()
+        L.nav_td3_actor_rows(*st["ar_head"], self._replay_ref(replay), len(replay), B,
+                             None if idx is None else C.c_void_p(idx.data_ptr()), *st["seed"],
+                             self.update_counter, *st["ar_tail"], s)
+        if st["wgrad"]:
+            L.nav_mlp_wgrad(*st["wg_a"], s)
+        o = self.actor_optimizer.advance()
+        ss, bc = (C.c_float * 1)(o[0]), (C.c_float * 1)(o[1])
+        if soft_update:
+            L.nav_grad_reduce_adam_polyak(*st["red_a"], ss, bc, *st["poly"], s)
+        else:
+            L.nav_grad_reduce_adam(*st["red_a"], ss, bc, s)
+
     # robot.py:312-366
     def _critic_rows(self, replay, idx, eps, s):
         c = self.cfg
@@ -284,6 +378,8 @@ class TD3:
 
     def train_critic(self, replay, idx=None, eps=None, stream=None):
         s = stream_handle(stream)
+        if self._fast():
+            return self._critic_epoch_fast(replay, idx, eps, s)
         self._critic_rows(replay, idx, eps, s)
         c1, c2 = self.critic_network_1, self.critic_network_2
         B = self.cfg.batch_size
@@ -346,6 +442,8 @@ class TD3:
         """robot.py:369-398; with soft_update the three soft updates of robot.py:283-285 that
         follow it on a policy epoch ride in the actor's reduce + Adam launch."""
         s = stream_handle(stream)
+        if self._fast():
+            return self._actor_epoch_fast(replay, idx, s, soft_update)
         self._actor_rows(replay, idx, s)
         self._grads_and_step([self.actor_network], [self.actor_optimizer], self.cfg.batch_size,
                              *self._actor_wgrad_args(), [self.eslab_a], [self.grad_a],

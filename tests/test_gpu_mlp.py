@@ -740,3 +740,26 @@ def test_wgrad_step_fused_bitwise(nav, hidden, nh, d_in, d_out, B, n_nets, pairs
             assert torch.isfinite(gb[1][k]).all()
             assert torch.equal(gb[0][k], gb[1][k]), (splits, k)
         assert int(tickets.abs().sum().item()) == 0
+
+
+@pytest.mark.parametrize("hidden,nh", [(256, 2), (200, 3), (96, 4), (64, 1)])
+@pytest.mark.parametrize("M", [1, 1000, 20000])
+def test_acting_forward_residual_bitwise(nav, hidden, nh, M):
+    """nav_act's residual (the acting forward, robot.py:556, 598-624: input rows f32(state - goal)
+    formed in the kernel, no masks) equals nav_mlp_forward's on the same f32 rows, bit for bit."""
+    from nav._lib import lib, params_struct, ptr
+    from nav.mlp import forward
+    net, _ = make_net(2, 2, hidden, nh, 123)
+    g = torch.Generator().manual_seed(M + nh)
+    st = (torch.rand(M, 2, generator=g, dtype=torch.float64) * 100).to(DEV)
+    gl = (torch.rand(M, 2, generator=g, dtype=torch.float64) * 100).to(DEV)
+    act = torch.zeros(M, 2, dtype=torch.float64, device=DEV)
+    res = torch.full((M, 2), float("nan"), device=DEV)
+    p = params_struct()
+    lib().nav_act(C.byref(p), C.byref(net.desc()), M, ptr(st), ptr(gl), None, None, 0, 1, ptr(act),
+                  ptr(res), None)
+    x = (st - gl).float().contiguous()
+    out = torch.full((M, 2), float("nan"), device=DEV)
+    forward([net], x, 2, 0, [out], 2, 0, M)
+    torch.cuda.synchronize()
+    assert torch.equal(res, out)
