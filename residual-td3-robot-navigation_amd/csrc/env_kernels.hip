@@ -603,119 +603,200 @@ NAV_DEV double block_min(double v, double* red) {
     return v;
 }
 
-// grid = (cells, groups): bound U^2 and candidate count of one cell of one group
+// grid = (cells / kPlanCells, groups): bound U^2 and candidate count of kPlanCells consecutive
+// cells (one x column, consecutive y) of one group. Each point is loaded once per block and
+// tested against all of the block's cells (the per-cell form re-read the group's points from L2
+// for every cell: 232 GB of L2 reads at the bench's 64 x 10 000 cells, 9.4 ms); min and count are
+// order-independent, so the result is the per-cell form's exactly.
+constexpr int kPlanCells = 10;
+static_assert(kCells % kPlanCells == 0 && NAV_WORLD_CELLS % kPlanCells == 0, "plan strips");
 __global__ __launch_bounds__(kBlock) void k_demo_index_plan(const double2* __restrict__ demo,
                                                             const int64_t* __restrict__ off,
                                                             int64_t m_shared,
                                                             double* __restrict__ bound,
                                                             int32_t* __restrict__ count) {
     __shared__ double red[kBlock / 64];
-    __shared__ int cnt[kBlock / 64];
-    const int cell = blockIdx.x, g = blockIdx.y;
+    __shared__ int cnt[kPlanCells][kBlock / 64];
+    const int cell0 = blockIdx.x * kPlanCells, g = blockIdx.y;
     const int64_t lo = off ? off[g] : 0, hi = off ? off[g + 1] : m_shared;
-    const double lx = (double)(cell / NAV_WORLD_CELLS), ly = (double)(cell % NAV_WORLD_CELLS);
-    double u = __builtin_inf();
+    const double lx = (double)(cell0 / NAV_WORLD_CELLS), ly0 = (double)(cell0 % NAV_WORLD_CELLS);
+    double u[kPlanCells];
+#pragma unroll
+    for (int c = 0; c < kPlanCells; ++c) u[c] = __builtin_inf();
     for (int64_t j = lo + threadIdx.x; j < hi; j += kBlock) {
         const double2 q = demo[j];
-        u = fmin(u, cell_maxd2(q.x, q.y, lx, ly));
+#pragma unroll
+        for (int c = 0; c < kPlanCells; ++c) u[c] = fmin(u[c], cell_maxd2(q.x, q.y, lx, ly0 + c));
     }
-    u = block_min(u, red);
-    const double lim = u * (1.0 + 1e-12) + 1e-12;
-    int c = 0;
+    double lim[kPlanCells];
+#pragma unroll
+    for (int c = 0; c < kPlanCells; ++c) {
+        const double uc = block_min(u[c], red);
+        lim[c] = uc * (1.0 + 1e-12) + 1e-12;
+    }
+    int n[kPlanCells] = {};
     for (int64_t j = lo + threadIdx.x; j < hi; j += kBlock) {
         const double2 q = demo[j];
-        c += cell_mind2(q.x, q.y, lx, ly) <= lim ? 1 : 0;
+#pragma unroll
+        for (int c = 0; c < kPlanCells; ++c) n[c] += cell_mind2(q.x, q.y, lx, ly0 + c) <= lim[c] ? 1 : 0;
     }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-    if ((threadIdx.x & 63) == 0) cnt[threadIdx.x >> 6] = c;
+    for (int c = 0; c < kPlanCells; ++c) {
+        int v = n[c];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        if ((threadIdx.x & 63) == 0) cnt[c][threadIdx.x >> 6] = v;
+    }
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (threadIdx.x < kPlanCells) {
+        const int c = threadIdx.x;
         int t = 0;
-        for (int w = 0; w < kBlock / 64; ++w) t += cnt[w];
-        const int64_t k = (int64_t)g * kCells + cell;
-        bound[k] = lim;
+        for (int w = 0; w < kBlock / 64; ++w) t += cnt[c][w];
+        const int64_t k = (int64_t)g * kCells + cell0 + c;
+        bound[k] = lim[c];
         count[k] = t;
     }
 }
 
-// exclusive scan of counts [n] into start [n + 1] (set-up time only): one 1024-thread workgroup
-// walks the array in coalesced tiles of 4096 (4 per thread), a wave scan + wave-total scan per
-// tile, carrying the running total (n = 10.24 M index cells at the bench config: ~2 500 tiles).
+// exclusive scan of counts [n] into start [n + 1] (set-up time only; n = 10.24 M index cells at
+// the bench config) in three launches over tiles of 4096 counts (4 per thread of a 1024-thread
+// workgroup), using `start` itself as the scratch of the tile totals: (1) every tile's total into
+// start[last index of the tile]; (2) one workgroup scans the ~2 500 totals into each tile's
+// exclusive offset at start[first index of the tile] and writes start[n]; (3) every tile scans its
+// counts from its offset (the tile's own scratch entries are overwritten last). Before: one
+// workgroup walked every tile in turn (3.3 ms per scan, profiles/r03zk_kernel_stats.csv).
 constexpr int kScanThreads = 1024;
-__global__ __launch_bounds__(kScanThreads) void k_scan_counts(const int32_t* __restrict__ count,
-                                                              int64_t n,
-                                                              int64_t* __restrict__ start) {
+constexpr int64_t kScanTile = 4 * kScanThreads;
+
+// inclusive scan of v across the workgroup (kScanThreads), wave scans + the wave totals in LDS
+NAV_DEV int64_t block_incl_scan(int64_t v, int64_t* wtot) {
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int64_t up = __shfl_up(v, o, 64);
+        if (lane >= o) v += up;
+    }
+    if (lane == 63) wtot[wv] = v;
+    __syncthreads();
+    int64_t before = 0;
+    for (int w = 0; w < wv; ++w) before += wtot[w];
+    __syncthreads();  // wtot may be reused by the next call
+    return before + v;
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_scan_tile_sums(const int32_t* __restrict__ count,
+                                                                 int64_t n,
+                                                                 int64_t* __restrict__ start) {
+    __shared__ int64_t wtot[kScanThreads / 64];
+    const int64_t t0 = (int64_t)blockIdx.x * kScanTile, i0 = t0 + 4 * (int64_t)threadIdx.x;
+    int64_t mine = 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) mine += i0 + u < n ? count[i0 + u] : 0;
+    const int64_t incl = block_incl_scan(mine, wtot);
+    if (threadIdx.x == kScanThreads - 1) {
+        const int64_t last = t0 + kScanTile < n ? t0 + kScanTile - 1 : n - 1;
+        start[last] = incl;  // the tile's total
+    }
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_scan_tile_offsets(int64_t n,
+                                                                    int64_t* __restrict__ start) {
     __shared__ int64_t wtot[kScanThreads / 64];
     __shared__ int64_t carry_s;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int64_t tiles = (n + kScanTile - 1) / kScanTile;
     int64_t carry = 0;
-    for (int64_t t0 = 0; t0 < n; t0 += 4 * kScanThreads) {
-        const int64_t i0 = t0 + 4 * (int64_t)tid;
-        int64_t c[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) c[u] = i0 + u < n ? count[i0 + u] : 0;
-        const int64_t mine = c[0] + c[1] + c[2] + c[3];
-        int64_t v = mine;  // inclusive scan within the wave
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int64_t up = __shfl_up(v, o, 64);
-            if (lane >= o) v += up;
-        }
-        if (lane == 63) wtot[wv] = v;
-        __syncthreads();
-        int64_t before = carry;
-        for (int w = 0; w < wv; ++w) before += wtot[w];
-        int64_t run = before + v - mine;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            if (i0 + u < n) start[i0 + u] = run;
-            run += c[u];
-        }
-        if (tid == kScanThreads - 1) carry_s = run;
+    for (int64_t b0 = 0; b0 < tiles; b0 += kScanThreads) {
+        const int64_t b = b0 + threadIdx.x;
+        const int64_t last = b < tiles ? (b * kScanTile + kScanTile < n ? b * kScanTile + kScanTile - 1
+                                                                       : n - 1)
+                                       : 0;
+        const int64_t tot = b < tiles ? start[last] : 0;
+        const int64_t incl = block_incl_scan(tot, wtot);
+        if (b < tiles) start[b * kScanTile] = carry + incl - tot;  // the tile's offset
+        if (threadIdx.x == kScanThreads - 1) carry_s = carry + incl;
         __syncthreads();
         carry = carry_s;
         __syncthreads();
     }
-    if (tid == 0) start[n] = carry;
+    if (threadIdx.x == 0) start[n] = carry;
 }
 
-// grid = (cells, groups): write the cell's candidate indices (group-relative, ascending)
+__global__ __launch_bounds__(kScanThreads) void k_scan_apply(const int32_t* __restrict__ count,
+                                                             int64_t n,
+                                                             int64_t* __restrict__ start) {
+    __shared__ int64_t wtot[kScanThreads / 64];
+    __shared__ int64_t base_s;
+    const int64_t t0 = (int64_t)blockIdx.x * kScanTile, i0 = t0 + 4 * (int64_t)threadIdx.x;
+    if (threadIdx.x == 0) base_s = start[t0];
+    int64_t c[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) c[u] = i0 + u < n ? count[i0 + u] : 0;
+    const int64_t mine = c[0] + c[1] + c[2] + c[3];
+    const int64_t incl = block_incl_scan(mine, wtot);  // synchronises: base_s is read
+    int64_t run = base_s + incl - mine;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        if (i0 + u < n) start[i0 + u] = run;
+        run += c[u];
+    }
+}
+
+inline void scan_counts(const int32_t* count, int64_t n, int64_t* start, hipStream_t st) {
+    const unsigned tiles = (unsigned)((n + kScanTile - 1) / kScanTile);
+    if (n == 0) {
+        hipLaunchKernelGGL(k_scan_tile_offsets, dim3(1), dim3(kScanThreads), 0, st, n, start);
+        return;
+    }
+    hipLaunchKernelGGL(k_scan_tile_sums, dim3(tiles), dim3(kScanThreads), 0, st, count, n, start);
+    hipLaunchKernelGGL(k_scan_tile_offsets, dim3(1), dim3(kScanThreads), 0, st, n, start);
+    hipLaunchKernelGGL(k_scan_apply, dim3(tiles), dim3(kScanThreads), 0, st, count, n, start);
+}
+
+// grid = (cells / kPlanCells, groups): write the candidate indices (group-relative, ascending) of
+// the plan's strip of cells, each point loaded once for all of the strip's cells
 __global__ __launch_bounds__(kBlock) void k_demo_index_fill(const double2* __restrict__ demo,
                                                             const int64_t* __restrict__ off,
                                                             int64_t m_shared,
                                                             const double* __restrict__ bound,
                                                             const int64_t* __restrict__ start,
                                                             int32_t* __restrict__ cand) {
-    __shared__ int wcnt[kBlock / 64];
-    __shared__ int64_t base;
-    const int cell = blockIdx.x, g = blockIdx.y;
+    __shared__ int wcnt[kPlanCells][kBlock / 64];
+    __shared__ int64_t base[kPlanCells];
+    const int cell0 = blockIdx.x * kPlanCells, g = blockIdx.y;
     const int64_t lo = off ? off[g] : 0, hi = off ? off[g + 1] : m_shared;
-    const double lx = (double)(cell / NAV_WORLD_CELLS), ly = (double)(cell % NAV_WORLD_CELLS);
-    const int64_t k = (int64_t)g * kCells + cell;
-    const double lim = bound[k];
+    const double lx = (double)(cell0 / NAV_WORLD_CELLS), ly0 = (double)(cell0 % NAV_WORLD_CELLS);
+    const int64_t k0 = (int64_t)g * kCells + cell0;
+    double lim[kPlanCells];
+#pragma unroll
+    for (int c = 0; c < kPlanCells; ++c) lim[c] = bound[k0 + c];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    if (threadIdx.x == 0) base = start[k];
+    if (threadIdx.x < kPlanCells) base[threadIdx.x] = start[k0 + threadIdx.x];
     __syncthreads();
     for (int64_t j0 = lo; j0 < hi; j0 += kBlock) {
         const int64_t j = j0 + threadIdx.x;
-        bool take = false;
-        if (j < hi) {
-            const double2 q = demo[j];
-            take = cell_mind2(q.x, q.y, lx, ly) <= lim;
+        double2 q = make_double2(0.0, 0.0);
+        if (j < hi) q = demo[j];
+        unsigned long long bal[kPlanCells];
+#pragma unroll
+        for (int c = 0; c < kPlanCells; ++c) {
+            const bool take = j < hi && cell_mind2(q.x, q.y, lx, ly0 + c) <= lim[c];
+            bal[c] = __ballot(take);
+            if (lane == 0) wcnt[c][wv] = __popcll(bal[c]);
         }
-        const unsigned long long bal = __ballot(take);
-        const int before = __popcll(bal & ((1ull << lane) - 1ull));
-        if (lane == 0) wcnt[wv] = __popcll(bal);
         __syncthreads();
-        int wbase = 0, tot = 0;
-        for (int w = 0; w < kBlock / 64; ++w) {
-            if (w < wv) wbase += wcnt[w];
-            tot += wcnt[w];
+#pragma unroll
+        for (int c = 0; c < kPlanCells; ++c) {
+            if (!((bal[c] >> lane) & 1ull)) continue;
+            int wbase = 0;
+            for (int w = 0; w < wv; ++w) wbase += wcnt[c][w];
+            cand[base[c] + wbase + __popcll(bal[c] & ((1ull << lane) - 1ull))] = (int32_t)(j - lo);
         }
-        if (take) cand[base + wbase + before] = (int32_t)(j - lo);
         __syncthreads();
-        if (threadIdx.x == 0) base += tot;
+        if (threadIdx.x < kPlanCells) {
+            int tot = 0;
+            for (int w = 0; w < kBlock / 64; ++w) tot += wcnt[threadIdx.x][w];
+            base[threadIdx.x] += tot;
+        }
         __syncthreads();
     }
 }
@@ -1230,7 +1311,8 @@ int nav_demo_index_plan(const double* demo_xy, const int64_t* demo_off, int32_t 
     if (!demo_xy || n_groups < 1 || (!demo_off && (n_groups != 1 || m < 1)) || !cell_bound ||
         !cell_count)
         return NAV_EINVAL;
-    hipLaunchKernelGGL(k_demo_index_plan, dim3(kCells, n_groups), dim3(kBlock), 0, S(stream),
+    hipLaunchKernelGGL(k_demo_index_plan, dim3(kCells / kPlanCells, n_groups), dim3(kBlock), 0,
+                       S(stream),
                        reinterpret_cast<const double2*>(demo_xy), demo_off, m, cell_bound,
                        cell_count);
     NAV_CHECK_LAUNCH();
@@ -1240,8 +1322,7 @@ int nav_demo_index_plan(const double* demo_xy, const int64_t* demo_off, int32_t 
 int nav_demo_index_scan(const int32_t* cell_count, int32_t n_groups, int64_t* cell_start,
                         void* stream) {
     if (!cell_count || !cell_start || n_groups < 1) return NAV_EINVAL;
-    hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(kScanThreads), 0, S(stream), cell_count,
-                       (int64_t)n_groups * kCells, cell_start);
+    scan_counts(cell_count, (int64_t)n_groups * kCells, cell_start, S(stream));
     NAV_CHECK_LAUNCH();
     return 0;
 }
@@ -1252,7 +1333,8 @@ int nav_demo_index_fill(const double* demo_xy, const int64_t* demo_off, int32_t 
     if (!demo_xy || n_groups < 1 || (!demo_off && n_groups != 1) || !cell_bound ||
         !cell_start || !cand)
         return NAV_EINVAL;
-    hipLaunchKernelGGL(k_demo_index_fill, dim3(kCells, n_groups), dim3(kBlock), 0, S(stream),
+    hipLaunchKernelGGL(k_demo_index_fill, dim3(kCells / kPlanCells, n_groups), dim3(kBlock), 0,
+                       S(stream),
                        reinterpret_cast<const double2*>(demo_xy), demo_off, m, cell_bound,
                        cell_start, cand);
     NAV_CHECK_LAUNCH();
@@ -1277,8 +1359,7 @@ int nav_demo_index_subplan(const double* demo_xy, const int64_t* demo_off, int32
 int nav_demo_index_subscan(const int32_t* sub_count, int32_t n_groups, int64_t* sub_start,
                            void* stream) {
     if (!sub_count || !sub_start || n_groups < 1) return NAV_EINVAL;
-    hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(kScanThreads), 0, S(stream), sub_count,
-                       (int64_t)n_groups * kIdxCells, sub_start);
+    scan_counts(sub_count, (int64_t)n_groups * kIdxCells, sub_start, S(stream));
     NAV_CHECK_LAUNCH();
     return 0;
 }

@@ -414,3 +414,26 @@ def test_device_field_generator_vs_host(nav):
         ulp = np.abs(f[..., 0].view(np.int32).astype(np.int64) - speed.view(np.int32))
         assert ulp.max() <= 4, (seed, ulp.max())
         assert (ulp == 0).mean() > 0.5
+
+
+@pytest.mark.parametrize("groups", [1, 7, 64])
+def test_demo_index_scans_vs_cumsum(nav, groups):
+    """nav_demo_index_scan / _subscan (the multi-workgroup exclusive scans of the demo index
+    build: tile totals, their scan, the tiles from their offsets) equal numpy's exclusive cumsum
+    with the total in the last entry, on ragged sizes (10 000 and 160 000 cells per group are not
+    multiples of the 4 096-count tile)."""
+    from nav._lib import lib, ptr
+    L = lib()
+    res = L.nav_demo_index_res()
+    for n_per, fn in ((10000, L.nav_demo_index_scan), (10000 * res * res, L.nav_demo_index_subscan)):
+        n = groups * n_per
+        g = np.random.default_rng(n)
+        cnt = g.integers(0, 60, n).astype(np.int32)
+        cnt[g.integers(0, n, max(1, n // 50))] = 0
+        c = torch.tensor(cnt, device="cuda")
+        start = torch.full((n + 1,), -7, dtype=torch.int64, device="cuda")
+        fn(ptr(c), groups, ptr(start), None)
+        torch.cuda.synchronize()
+        ref = np.zeros(n + 1, dtype=np.int64)
+        ref[1:] = np.cumsum(cnt, dtype=np.int64)
+        assert np.array_equal(start.cpu().numpy(), ref), (groups, n_per)
