@@ -1176,6 +1176,12 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
     float* dys = qv + TM;          // [TM][4] dL/dq rows of the row backward
     __bf16* stage = reinterpret_cast<__bf16*>(dys + TM * 4);  // gemm_cols' split stage
     NAV_MARK(0);
+#ifdef NAV_STAGGER_SEL
+    // A/B probe: half of the workgroups start ~NAV_STAGGER_N x 8 k cycles late (desynchronising
+    // the two workgroups of a CU, so one's epilogues overlap the other's GEMMs)
+    if (NAV_STAGGER_SEL((int)blockIdx.x))
+        for (int i = 0; i < NAV_STAGGER_N; ++i) __builtin_amdgcn_s_sleep(127);
+#endif
     const L0Pre l0_at = load_l0<NT>(a.actor_t);  // in flight under the sampling
     // target policy smoothing noise of (row, output) tid % TM, tid / TM: clamp(policy_noise * eps,
     // +-noise_clip), formed while the sampled rows are in flight
