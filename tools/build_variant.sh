@@ -14,12 +14,12 @@ FL="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unus
 objs="$B/env_kernels.o $B/learner_kernels.o $B/mlp_kernels.o"
 for n in 1 2 3 4 5 6 7 8; do objs="$objs $B/mlp_nt$n.o"; done
 case $unit in
-  learner) /opt/rocm/bin/hipcc $FL $flags -c $P/csrc/learner_kernels.hip -o abl/$name.o
+  learner) /opt/rocm/bin/hipcc $FL -mllvm -amdgpu-sched-strategy=max-ilp $flags -c $P/csrc/learner_kernels.hip -o abl/$name.o
            objs=${objs/$B\/learner_kernels.o/abl\/$name.o} ;;
   env) /opt/rocm/bin/hipcc $FL $flags -c $P/csrc/env_kernels.hip -o abl/$name.o
        objs=${objs/$B\/env_kernels.o/abl\/$name.o} ;;
   mlp[1-8]) n=${unit#mlp}
-        /opt/rocm/bin/hipcc $FL -mllvm -amdgpu-mfma-vgpr-form=1 $flags -DNAV_MLP_PART=$n -c $P/csrc/mlp_kernels.hip -o abl/$name.o
+        /opt/rocm/bin/hipcc $FL -mllvm -amdgpu-mfma-vgpr-form=1 -mllvm -amdgpu-sched-strategy=max-ilp $flags -DNAV_MLP_PART=$n -c $P/csrc/mlp_kernels.hip -o abl/$name.o
         objs=${objs/$B\/mlp_nt$n.o/abl\/$name.o} ;;
   mlp8agpr) /opt/rocm/bin/hipcc $FL $flags -DNAV_MLP_PART=8 -c $P/csrc/mlp_kernels.hip -o abl/$name.o
         objs=${objs/$B\/mlp_nt8.o/abl\/$name.o} ;;
