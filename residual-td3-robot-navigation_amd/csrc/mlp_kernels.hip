@@ -15,6 +15,9 @@
 
 namespace {
 
+#ifndef NAV_STAGE_DB1
+#define NAV_STAGE_DB1 1  // 32-row blocks: double-buffered split stage, one barrier per k step
+#endif
 #ifndef NAV_GEMM_SCHED
 #define NAV_GEMM_SCHED 0  // interleave hints in gemm_cols (A/B)
 #endif
@@ -89,8 +92,14 @@ NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const bf16x8* __rest
     float4 x = sp ? *reinterpret_cast<const float4*>(src) : make_float4(0.f, 0.f, 0.f, 0.f);
     typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
     // split of step q's share (x) into the stage, the next x from the LDS rows, B planes ahead
+    // 32-row blocks (small batches: latency-bound, one wave per SIMD) double-buffer the stage and
+    // pass one barrier per step: step q + 1's stores go to the buffer step q - 1 was read from,
+    // which every wave finished reading (and consumed in its MFMAs) before step q's barrier
+    constexpr bool DB = RT == 1 && NAV_STAGE_DB1;
+    constexpr int SB = 3 * PP;  // bf16 per stage buffer
     auto produce = [&](int q) {
         if (sp) {
+            __bf16* const dq = dst + (DB ? (q & 1) * SB : 0);
             const float v[4] = {x.x, x.y, x.z, x.w};
             bf16x4 ph, pm, pl;
 #pragma unroll
@@ -101,9 +110,9 @@ NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const bf16x8* __rest
                 pm[j] = mm;
                 pl[j] = ll;
             }
-            *reinterpret_cast<bf16x4*>(dst) = ph;
-            *reinterpret_cast<bf16x4*>(dst + PP) = pm;
-            *reinterpret_cast<bf16x4*>(dst + 2 * PP) = pl;
+            *reinterpret_cast<bf16x4*>(dq) = ph;
+            *reinterpret_cast<bf16x4*>(dq + PP) = pm;
+            *reinterpret_cast<bf16x4*>(dq + 2 * PP) = pl;
             if (q + 1 < nq) x = *reinterpret_cast<const float4*>(src + 16 * (q + 1));
         }
         // production of step q runs during step q - 1's MFMAs: the B planes loaded here are
@@ -118,20 +127,22 @@ NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const bf16x8* __rest
         }
     };
     Split3 sa[RT];
-    // two barriers per step: the stage is written, then read (the next step may overwrite it)
-    auto consume = [&]() {
+    // two barriers per step (one buffer): the stage is written, then read (the next step may
+    // overwrite it); one barrier with the double buffer
+    auto consume = [&](int q) {
         __syncthreads();
+        const __bf16* fq = frag + (DB ? (q & 1) * SB : 0);
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) {
-            const __bf16* f = frag + rt * 32 * 16;
+            const __bf16* f = fq + rt * 32 * 16;
             sa[rt].h = *reinterpret_cast<const bf16x8*>(f);
             sa[rt].m = *reinterpret_cast<const bf16x8*>(f + PP);
             sa[rt].l = *reinterpret_cast<const bf16x8*>(f + 2 * PP);
         }
-        __syncthreads();
+        if (!DB) __syncthreads();
     };
     produce(0);
-    consume();
+    consume(0);
 #pragma unroll
     for (int q = 0; q < nq; ++q) {
         // step q + 1's production comes first in program order, so the scheduler can place it
@@ -162,7 +173,7 @@ NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const bf16x8* __rest
             }
         }
 #endif
-        if (q + 1 < nq) consume();
+        if (q + 1 < nq) consume(q + 1);
     }
 }
 
@@ -228,7 +239,9 @@ struct FwdArgs {
 __host__ __device__ constexpr int red_floats(int tm) { return 2 * kWaves * tm; }
 
 // bytes of gemm_cols' split stage for TM rows: [3 planes][TM][16] bf16
-__host__ __device__ constexpr size_t stage_bytes(int tm) { return (size_t)3 * tm * 16 * 2; }
+__host__ __device__ constexpr size_t stage_bytes(int tm) {
+    return (size_t)(tm == 32 && NAV_STAGE_DB1 ? 2 : 1) * 3 * tm * 16 * 2;
+}
 
 // rows [tm][hp+4] + input/dy staging [tm][4] + output-layer partial sums, then the split stage
 __host__ __device__ constexpr size_t lds_floats(int hp, int tm) {
