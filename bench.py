@@ -35,12 +35,12 @@ from nav import prof  # noqa: E402
 
 EVENT_SAMPLE = 8             # timed region: event pairs around 1 launch in 8 of the dominant kernel
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-FP32_MFMA_PEAK_TFS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
 FP64_VALU_PEAK_TFS = 78.6    # MI355X spec FP64 vector
 BF16_MFMA_PEAK_TFS = 2516.6  # MI355X_MICROARCH.md: 1024 FLOP/clk/SIMD x 1024 SIMDs x 2.4 GHz (dense)
-# hidden x hidden GEMM passes per launch of each row kernel (network forwards + row backwards):
-# these run on the bf16 matrix cores as six partial products of the exact 3-way split
-HIDDEN_PASSES = {"critic_rows": 7, "actor_rows": 4, "act": 1, "act_tick": 1}
+# bf16 MFMA partial products per hidden x hidden layer of each row kernel: one entry per network
+# pass (forwards + row backwards). A pass with both operands split three ways (hi + mid + lo)
+# runs 6 products; these are the bf16 FLOPs the matrix cores execute for the f32 GEMM
+HIDDEN_PRODUCTS = {"critic_rows": [6] * 7, "actor_rows": [6] * 4, "act": [6], "act_tick": [6]}
 # HBM bytes per launch from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this same
 # command (tools/pmc_traffic.py, gfx950 correction applied); bench regions -> kernel names
 PMC_TRAFFIC = os.path.join(HERE, "profiles", "pmc_traffic.json")
@@ -48,8 +48,7 @@ REGION_KERNEL = {"critic_rows": "k_td3_critic_rows", "actor_rows": "k_td3_actor_
                  "mlp_bwd": "k_mlp_bwd", "mlp_wgrad": "k_wgrad", "act": "k_mlp_fwd",
                  "agent_step": "k_agent_step", "env_step": "k_env_step",
                  "act_tick": "k_mlp_fwd<tick>", "env_step_k": "k_env_step_k",
-                 "grad_reduce": "k_grad_reduce", "demo_reward": "k_demo_reward_idx",
-                 "wgrad_step": "k_wgrad_step"}
+                 "grad_reduce": "k_grad_reduce", "demo_reward": "k_demo_reward_idx"}
 
 
 def pmc_traffic(region):
@@ -368,26 +367,38 @@ def main():
                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
                     "traffic_source": traffic_src}
-        else:
+        elif dominant == "demo_reward":
             tf = ach / 1e12
-            peak = FP64_VALU_PEAK_TFS if dominant == "demo_reward" else FP32_MFMA_PEAK_TFS
+            roof = {"bound": "valu", "kernel": dominant, "achieved": round(tf, 2),
+                    "peak": FP64_VALU_PEAK_TFS, "unit": "TFLOP/s",
+                    "frac": round(tf / FP64_VALU_PEAK_TFS, 4), "traffic": traffic,
+                    "traffic_source": traffic_src, "avg_us": round(d["avg_us"], 2)}
+        else:
+            # the matrix-core view: the bf16 FLOPs the kernel's hidden x hidden GEMMs execute
+            # (each f32 product as bf16 partial products of the exact split) against the bf16
+            # dense peak; the f32-equivalent rate of all its FLOPs is a separate key
             hp = (args.hidden + 31) // 32 * 32
             rows = args.envs if dominant in ("act", "act_tick") else rank_batch
-            hidden = (HIDDEN_PASSES.get(dominant, 0) * (args.layers - 1) * 2.0 * rows * hp * hp)
-            bf16 = 6.0 * hidden / (d["avg_us"] * 1e-6) / 1e12
-            roof = {"bound": "valu" if dominant == "demo_reward" else "mfma",
-                    "kernel": dominant, "achieved": round(tf, 2), "peak": peak,
-                    "peak_note": "f32 MFMA peak: the path computes in f32 (its hidden x hidden "
-                                 "GEMMs on the bf16 matrix cores as six partial products of an "
-                                 "exact 3-way bf16 split, f32 accuracy); achieved counts f32 FLOPs",
-                    "bf16_pipe": {"hidden_gemm_flop_per_launch": hidden,
-                                  "bf16_flop_per_launch": 6.0 * hidden,
-                                  "achieved_TFs": round(bf16, 1), "peak_TFs": BF16_MFMA_PEAK_TFS,
-                                  "frac": round(bf16 / BF16_MFMA_PEAK_TFS, 4)},
-                    "unit": "TFLOP/s", "frac": round(tf / peak, 4), "traffic": traffic,
-                    "traffic_source": traffic_src,
-                    "flop_per_launch": d["work_per_launch"], "avg_us": round(d["avg_us"], 2),
-                    "launches_timed": d["launches"],
+            layer = (args.layers - 1) * 2.0 * rows * hp * hp
+            prods = HIDDEN_PRODUCTS.get(dominant, [])
+            hidden = len(prods) * layer
+            bf16_flop = sum(prods) * layer
+            bf16 = bf16_flop / (d["avg_us"] * 1e-6) / 1e12
+            roof = {"bound": "mfma", "kernel": dominant, "achieved": round(bf16, 1),
+                    "peak": BF16_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                    "frac": round(bf16 / BF16_MFMA_PEAK_TFS, 4),
+                    "peak_note": "bf16 dense MFMA peak: the hidden x hidden f32 GEMMs run on the "
+                                 "bf16 matrix cores as partial products of an exact 3-way bf16 "
+                                 "split (f32 accuracy); achieved = those bf16 FLOPs per launch / "
+                                 "the launch's event-timed duration",
+                    "bf16_flop_per_launch": bf16_flop,
+                    "hidden_gemm_f32_flop_per_launch": hidden,
+                    "f32_equiv": {"flop_per_launch": d["work_per_launch"],
+                                  "achieved_TFs": round(ach / 1e12, 2),
+                                  "note": "all of the kernel's f32 FLOPs (SURVEY 8(d)) / launch "
+                                          "time; the f32 MFMA peak is 157.3 TF"},
+                    "traffic": traffic, "traffic_source": traffic_src,
+                    "avg_us": round(d["avg_us"], 2), "launches_timed": d["launches"],
                     "launches": timer.seen[dominant], "event_sample": EVENT_SAMPLE}
         forms = None if ws > 1 else tick_forms(tr)
         sweep = None if (args.no_sweep or ws > 1) else step_kernel_sweep(

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define NAV_ABI_VERSION 8
+#define NAV_ABI_VERSION 9
 #define NAV_EINVAL (-100000)
 
 #define NAV_WORLD_CELLS 100 /* field = float32 [100][100][2] (speed, angle), x-major: cell cx*100+cy
@@ -77,9 +77,13 @@ typedef struct nav_step_out {
     double* next_state;   /* [n][2] next state BEFORE any auto-reset (Environment.step return) */
     double* goal_term;    /* [n] -||s'-goal|| (robot.py:741), consumed by nav_demo_reward      */
     uint8_t* flags;       /* [n] bit0 done, bit1 goal, bit2 stuck, bit3 ended, bit4 demo term  */
-    float* block_stats;   /* nullable: [ceil(n/64)][8], row k = envs [64k, 64k+64): sum reward
-                             (w/o demo term), n_done, n_goal, n_stuck, n_ended, 0, 0, 0
-                             (one wave's shuffle tree per row: deterministic)                 */
+    float* block_stats;   /* nullable: [ceil(n/64)][8], row k = envs [64k, 64k+64): sum of the
+                             reward pushed to the replay rows, n_done, n_goal, n_stuck, n_ended,
+                             0, 0, 0 (one wave's shuffle tree per row: deterministic). The sum
+                             includes the demo term wherever the demo pass runs in the same
+                             launch (nav_agent_step_indexed, nav_act_tick); after nav_agent_step
+                             with demo_pending it lacks the flagged envs' demo term, which
+                             nav_demo_reward(_indexed) adds to their rows later                 */
 } nav_step_out;
 
 /* Replay ring (device): rows [capacity][8] float32 (robot.py:58-124 ReplayBuffer). */
@@ -318,7 +322,10 @@ int nav_mlp_forward(const nav_mlp* nets, int32_t n_nets, int64_t M, const float*
  * edge_slabs, acts/save_mask, masks). With row_backward != 0 each online critic's row backward
  * (robot.py:361) follows its forward in the same launch, as nav_mlp_backward of dq with the
  * batch's (s, a) columns as input: W0 / bias partials into edge_slabs, dz rows of dz_save_mask
- * layers into dz[i] — the caller then skips nav_mlp_backward. */
+ * layers into dz[i] — the caller then skips nav_mlp_backward. split_twins: 1 = the twin online
+ * critics in separate workgroups (grid.y = 2, each repeating the target passes: the small-batch
+ * form), 0 = both in one workgroup, < 0 = the library's choice (split for B <= 2048); the
+ * results are bit-identical either way. */
 int nav_td3_critic_rows(const nav_mlp* target_actor, const nav_mlp* target_critics,
                         const nav_mlp* critics, const nav_replay* replay, int64_t size,
                         int64_t B, const int64_t* idx, uint32_t seed_lo, uint32_t seed_hi,
@@ -327,7 +334,7 @@ int nav_td3_critic_rows(const nav_mlp* target_actor, const nav_mlp* target_criti
                         float* const* dq, float* const* loss_part, float* const* edge_slabs,
                         float* const* acts, uint32_t save_mask, uint16_t* const* masks,
                         int32_t row_backward, float* const* dz, uint32_t dz_save_mask,
-                        void* stream);
+                        int32_t split_twins, void* stream);
 /* train_actor's row-local part (robot.py:382-390) in one launch: sample rows (Philox
  * NAV_TAG_SAMPLE at 2*counter + 1, or idx) into batch [B][8]; actor forward on s (ReLU bits to
  * masks_actor, activations to acts for save_mask bits; the top layer's dWo partials come
@@ -410,27 +417,6 @@ int nav_grad_reduce_adam_polyak(const nav_mlp* nets, int32_t n_nets,
                                 const float* bc2_sqrt, const nav_mlp* net_targets,
                                 const nav_mlp* targets, const nav_mlp* sources, int32_t n_pairs,
                                 float tau, void* stream);
-/* nav_mlp_wgrad + nav_grad_reduce_adam(_polyak) in ONE launch (the product path of
- * robot.py:236-239, 357-363, 283-285): the weight-gradient tiles, the edge-slab reduce and the Adam
- * step (and the soft updates) as one grid in which no workgroup waits on another — the last
- * workgroup to finish a tile (an arrival counter in `tickets`) reduces its split slabs and steps
- * its hidden weights, the last of all steps the edge parameters (which every tile reads).
- * Arguments as nav_mlp_wgrad followed by nav_grad_reduce_adam_polyak; grads[i] (required) receive
- * the reduced gradients. m == NULL: no Adam (the reduce of nav_grad_reduce_multi for the shared
- * policy's collective; net_targets NULL and n_pairs 0). net_targets NULL / n_pairs 0: no soft
- * update. tickets: NAV_WGRAD_TICKETS int32, zero before the first launch and left zero by every
- * launch (one buffer per stream; launches on one stream may share it). Bit-identical to the
- * unfused launches. */
-#define NAV_WGRAD_TICKETS 256
-int nav_mlp_wgrad_step(const nav_mlp* nets, int32_t n_nets, int64_t M, const float* in,
-                       int32_t ld_in, int32_t in_col, const float* const* acts,
-                       const float* const* dz, const float* const* dy, int32_t ld_dy,
-                       const uint16_t* const* masks, float* const* slabs, int32_t splits,
-                       const float* const* edge_slabs, int64_t edge_blocks, float* const* grads,
-                       float* const* m, float* const* v, float beta1, float beta2, float eps,
-                       const float* step_size, const float* bc2_sqrt, const nav_mlp* net_targets,
-                       const nav_mlp* targets, const nav_mlp* sources, int32_t n_pairs, float tau,
-                       int32_t* tickets, void* stream);
 /* nav_grad_reduce of 1 or 2 same-shape networks in one launch (the twin critics' gradients into
  * one contiguous bucket for the shared-policy all-reduce). */
 int nav_grad_reduce_multi(const nav_mlp* nets, int32_t n_nets, const float* const* hidden_slabs,

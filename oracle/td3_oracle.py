@@ -44,13 +44,17 @@ class MLP:
             out += [W, b]
         return out
 
-    def forward(self, x):
+    def forward(self, x, bits=None):
+        """bits (optional, test injection): per hidden layer a bool [rows][width] ReLU decision
+        to use instead of (z > 0) — h = z * bits — so a gradient comparison is not moved by a
+        pre-activation within rounding of 0 taking the other branch (the values differ from
+        relu(z) only inside that band)."""
         h = x
         n = len(self.params)
         for i, (W, b) in enumerate(self.params):
             h = torch.nn.functional.linear(h, W, b)
             if i < n - 1:
-                h = torch.relu(h)
+                h = torch.relu(h) if bits is None else h * bits[i].to(h.dtype)
         return h
 
 
@@ -97,11 +101,13 @@ class TD3Oracle:
         self.last_grads = {}
 
     @staticmethod
-    def _q(net, s, a):
-        return net.forward(torch.cat([s, a], dim=1))
+    def _q(net, s, a, bits=None):
+        return net.forward(torch.cat([s, a], dim=1), bits)
 
-    def train_critic(self, batch, noise):
-        """robot.py:312-366. batch = (s, a, r, s2, d) numpy; noise = standard normal [B,2] f32."""
+    def train_critic(self, batch, noise, bits=None):
+        """robot.py:312-366. batch = (s, a, r, s2, d) numpy; noise = standard normal [B,2] f32;
+        bits (optional): {"c1": [...], "c2": [...]} injected ReLU decisions of the online critics
+        (MLP.forward)."""
         s, a, r, s2, d = batch
         s = torch.tensor(np.asarray(s), dtype=torch.float32)
         a = torch.tensor(np.asarray(a), dtype=torch.float32)
@@ -119,7 +125,7 @@ class TD3Oracle:
             ts = net.tensors()
             for t in ts:
                 t.requires_grad_(True)
-            q = self._q(net, s, a)
+            q = self._q(net, s, a, None if bits is None else bits[key])
             loss = torch.nn.functional.mse_loss(q, y)
             grads = torch.autograd.grad(loss, ts)
             for t in ts:
@@ -130,14 +136,15 @@ class TD3Oracle:
         self.last_y = y.squeeze(1).clone()
         return losses
 
-    def train_actor(self, states):
-        """robot.py:369-398 (critic-1 grads are discarded, as zero_grad does in the reference)."""
+    def train_actor(self, states, bits=None):
+        """robot.py:369-398 (critic-1 grads are discarded, as zero_grad does in the reference);
+        bits (optional): {"actor": [...], "c1": [...]} injected ReLU decisions (MLP.forward)."""
         s = torch.tensor(np.asarray(states), dtype=torch.float32)
         ts = self.actor.tensors()
         for t in ts:
             t.requires_grad_(True)
-        a = self.actor.forward(s)
-        loss = -self._q(self.critic1, s, a).mean()
+        a = self.actor.forward(s, None if bits is None else bits["actor"])
+        loss = -self._q(self.critic1, s, a, None if bits is None else bits["c1"]).mean()
         grads = torch.autograd.grad(loss, ts)
         for t in ts:
             t.requires_grad_(False)

@@ -921,8 +921,10 @@ __global__ __launch_bounds__(kBlock) void k_agent_step(nav_params p, nav_env_soa
                               demo_pending != 0, pend);
     if (DEMO) {
         __shared__ DemoScratch<kBlock, kBlock> scratch;
-        demo_pass<kBlock, kBlock>(p, d, scratch, pend, e, reinterpret_cast<float*>(rows), cap,
-                                  base, reward_out);
+        const double r = demo_pass<kBlock, kBlock>(p, d, scratch, pend, e,
+                                                   reinterpret_cast<float*>(rows), cap, base,
+                                                   reward_out);
+        if (pend.need) st.r = (float)r;  // the final reward of a flagged env
     }
     if (out.block_stats && e - (threadIdx.x & 63) < env.n) wave_stats(st, out.block_stats, e);
 }
@@ -1067,9 +1069,7 @@ int nav_env_step(const nav_params* p, const nav_env_soa* env, const float* field
     // Non-temporal state/action streams once the 48 B/env working set is past the 256 MB MALL
     // (>= 4 Mi envs): 219 -> 204 us at 2^24 envs (profiles/r01p_step_ab.log). Below that the
     // state stays cache-resident between steps, so default-policy accesses.
-    // NAV_ENV_STEP_NT=0/1 forces either (A/B only).
-    static const int nt_env = getenv("NAV_ENV_STEP_NT") ? atoi(getenv("NAV_ENV_STEP_NT")) : -1;
-    const bool nt = nt_env >= 0 ? nt_env != 0 : env->n >= (int64_t(1) << 22);
+    const bool nt = env->n >= (int64_t(1) << 22);
     hipLaunchKernelGGL(nt ? k_env_step<true> : k_env_step<false>, dim3(blocks_for(env->n)),
                        dim3(kBlock), 0, S(stream), env->n,
                        reinterpret_cast<double2*>(env->state),

@@ -44,17 +44,8 @@ struct WgradArgs {
     int64_t per_wave;       // rows per wave (multiple of 64)
 };
 
-#ifndef NAV_WG_WAVES
-#define NAV_WG_WAVES 8
-#endif
-#ifndef NAV_WG_TOTAL
-#define NAV_WG_TOTAL 256
-#endif
-#ifndef NAV_WG_EXP
-#define NAV_WG_EXP 0  // tuning probes: 1 = operands without VALU math, 2 = without LDS reads,
-                      // 4 = no row loop, 5 = no global loads, 6 = no operand split
-#endif
-constexpr int WG_WAVES = NAV_WG_WAVES;
+constexpr int WG_WAVES = 8;
+constexpr int WG_TOTAL = 256;  // workgroups that fill the chip (one 8-wave workgroup per CU)
 constexpr int WG_THREADS = WG_WAVES * 64;
 constexpr int WG_TILE = 64;
 constexpr int WG_CHUNK = 64;  // rows per staged chunk (lane = row)
@@ -195,170 +186,6 @@ NAV_DEV void wgrad_rows(const WgradArgs& a, int y, int L, int n0, int k0, int64_
     }
 }
 
-// The fast path of wgrad_rows for a full 64 x 64 tile of a 2-hidden-layer network (P and Q both
-// recomputed — the bench shape): branch-free and software-pipelined. Step s's 4 MFMAs are issued
-// interleaved with the VALU that forms step s+1's operands (sched_group_barrier: 1 MFMA, then a
-// quarter of the VALU), and the LDS row data is read two steps ahead, so neither the operand
-// math nor the LDS latency sits between two MFMAs of the wave. The row data is double-buffered
-// per wave: the next chunk is parked into the other slot half-way through the current one.
-NAV_DEV void wgrad_rows_fast(const WgradArgs& a, int y, int n0, int k0, int64_t r_lo,
-                             int64_t r_hi, float* stage, f32x16 (&acc)[2][2]) {
-    const MlpDev& net = a.net[y];
-    const int hp = net.hp, nh = net.n_hidden, d_in = net.d_in, d_out = net.d_out;
-    const int lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
-    const int64_t M = a.M;
-    const int cn[2] = {n0 + l32, n0 + 32 + l32};
-    const int ck[2] = {k0 + l32, k0 + 32 + l32};
-    float wo[2][2], w0[2][4], b0[2];
-    {
-        const float* Wo = net.params + net.w_off[nh];
-        const float* W0 = net.params + net.w_off[0];
-        const float* bb = net.params + net.b_off[0];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            wo[i][0] = Wo[cn[i]];
-            wo[i][1] = d_out > 1 ? Wo[hp + cn[i]] : 0.f;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) w0[i][k] = k < d_in ? W0[ck[i] * d_in + k] : 0.f;
-            b0[i] = bb[ck[i]];
-        }
-    }
-    const int NTm = hp >> 5;
-    const uint16_t* mk = a.masks[y] + (size_t)(nh - 1) * mask_rowtiles(M) * NTm * 64;
-    const int tm0 = n0 >> 5;
-    // the next chunk's raw loads stay untouched in registers until park(): anything computed
-    // from them here would pin a memory-latency wait at the top of the chunk
-    const bool xv4 = ((a.in_col | a.ld_in) & 3) == 0 && (reinterpret_cast<uintptr_t>(a.in) & 15) == 0;
-    const int nxl = a.ld_in - a.in_col < 4 ? a.ld_in - a.in_col : 4;  // x loads in bounds
-    float4 rx = make_float4(0.f, 0.f, 0.f, 0.f);
-    float rg0 = 0.f, rg1 = 0.f;
-    uint32_t rm[2][2][2];
-    int64_t rbl = r_lo;  // first row of the chunk the raw registers hold
-    auto load = [&](int64_t rb) {
-        rbl = rb;
-        const int64_t r = rb + lane;
-        const int64_t rc = r < r_hi ? r : r_lo;
-        const float* x = a.in + rc * a.ld_in + a.in_col;
-        if (xv4) {
-            rx = *reinterpret_cast<const float4*>(x);
-        } else {
-            rx.x = x[0];
-            if (nxl > 1) rx.y = x[1];
-            if (nxl > 2) rx.z = x[2];
-            if (nxl > 3) rx.w = x[3];
-        }
-        const float* g = a.dy[y] + rc * a.ld_dy;
-        rg0 = g[0];
-        if (d_out > 1) rg1 = g[1];
-        const int64_t rt0 = rb >> 5;
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                const uint16_t* w = mk + ((rt0 + t) * NTm + tm0 + i) * 64 + l32;
-                rm[i][t][0] = w[0];
-                rm[i][t][1] = w[32];
-            }
-    };
-    // slot b: x [64][4] then dy [64][2]; rows past r_hi and inputs past d_in / d_out are zero;
-    // mwo receives the chunk's mask words shifted by the lane half's row parity
-    auto park = [&](int b, uint32_t (&mwo)[2][2]) {
-        const bool ok = rbl + lane < r_hi;
-        float* sl = stage + b * WG_STAGE_FLOATS;
-        const float4 x = make_float4(ok ? rx.x : 0.f, ok && d_in > 1 ? rx.y : 0.f,
-                                     ok && d_in > 2 ? rx.z : 0.f, ok && d_in > 3 ? rx.w : 0.f);
-        *reinterpret_cast<float4*>(sl + lane * 4) = x;
-        *reinterpret_cast<float2*>(sl + WG_CHUNK * 4 + lane * 2) =
-            make_float2(ok ? rg0 : 0.f, ok && d_out > 1 ? rg1 : 0.f);
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int t = 0; t < 2; ++t) mwo[i][t] = (rm[i][t][0] | (rm[i][t][1] << 16)) >> h;
-    };
-    struct Row {
-        float4 x;
-        float2 g;
-    };
-    auto read = [&](int b, int s) {
-        const float* sl = stage + b * WG_STAGE_FLOATS;
-        const int rr = 2 * s + h;
-        Row r;
-        if (NAV_WG_EXP == 2) {
-            r.x = make_float4(wo[0][0] + s, wo[0][1], wo[1][0], wo[1][1]);
-            r.g = make_float2(b0[0] + s, b0[1]);
-            return r;
-        }
-        r.x = *reinterpret_cast<const float4*>(sl + rr * 4);
-        r.g = *reinterpret_cast<const float2*>(sl + WG_CHUNK * 4 + rr * 2);
-        return r;
-    };
-    // operands of chunk step s from its row data and the chunk's (h-shifted) mask words
-    auto operands = [&](const Row& r, const uint32_t (&m)[2][2], int s, float (&p)[2],
-                        float (&q)[2]) {
-        if (NAV_WG_EXP == 1) {
-            p[0] = r.g.x; p[1] = r.g.y; q[0] = r.x.x; q[1] = r.x.y;
-            return;
-        }
-        const int sh = 16 * ((s >> 1) & 1) + 2 * (s & 1) + 4 * ((s & 15) >> 2);
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const float v = top_unit(r.g.x, r.g.y, wo[i][0], wo[i][1]);
-            p[i] = (m[i][(s >> 4) & 1] >> sh) & 1u ? v : 0.f;
-            q[i] = layer0_unit(r.x, w0[i][0], w0[i][1], w0[i][2], w0[i][3], b0[i]);
-        }
-    };
-    if (r_lo >= r_hi) return;
-    uint32_t mw[2][2], mwn[2][2];
-    load(r_lo);
-    park(0, mw);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int t = 0; t < 2; ++t) mwn[i][t] = mw[i][t];
-    float p[2], q[2];
-    Row ra = read(0, 0), rb1 = read(0, 1);
-    operands(ra, mw, 0, p, q);
-    ra = rb1;  // row data of step 1
-    int buf = 0;
-    for (int64_t rb = r_lo; rb < r_hi; rb += WG_CHUNK) {
-        const bool more = rb + WG_CHUNK < r_hi;
-        if (more) load(rb + WG_CHUNK);
-#pragma unroll
-        for (int s = 0; s < WG_CHUNK / 2; ++s) {
-            if (s == WG_CHUNK / 4 && more) park(buf ^ 1, mwn);
-            __builtin_amdgcn_sched_barrier(0);
-            // LDS read of step s + 2 (the next chunk's slot for the last two steps)
-            Row rn = ra;
-            if (s + 2 < WG_CHUNK / 2) rn = read(buf, s + 2);
-            else if (more) rn = read(buf ^ 1, s + 2 - WG_CHUNK / 2);
-            // operands of step s + 1 from the row data read one step earlier
-            float pn[2] = {0.f, 0.f}, qn[2] = {0.f, 0.f};
-            if (s + 1 < WG_CHUNK / 2) operands(ra, mw, s + 1, pn, qn);
-            else if (more) operands(ra, mwn, 0, pn, qn);
-            acc[0][0] = mfma(p[0], q[0], acc[0][0]);
-            acc[0][1] = mfma(p[0], q[1], acc[0][1]);
-            acc[1][0] = mfma(p[1], q[0], acc[1][0]);
-            acc[1][1] = mfma(p[1], q[1], acc[1][1]);
-            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // the 2 LDS reads first
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
-                __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);  // up to 6 VALU
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            p[0] = pn[0]; p[1] = pn[1]; q[0] = qn[0]; q[1] = qn[1];
-            ra = rn;
-        }
-        if (more) {
-            buf ^= 1;
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int t = 0; t < 2; ++t) mw[i][t] = mwn[i][t];
-        }
-    }
-}
-
 // The MFMA-operand path for a full 64 x 64 tile of a 2-hidden-layer network (the bench shape).
 // The operands are produced by MFMAs too: per 32-row tile, dz = dy . Wo (K = d_out <= 2, one
 // v_mfma_f32_32x32x2_f32 per 32 columns) and h_0 = x . W0^T + b0 (K = d_in <= 4, two MFMAs on
@@ -418,10 +245,7 @@ NAV_DEV void wgrad_rows_mfma(const WgradArgs& a, int y, int n0, int k0, int64_t 
     int64_t rl = r_lo;  // first row of the next tile to load
     auto load = [&](int64_t) {
         Raw v;
-        if (NAV_WG_EXP == 5) {  // tuning probe: no global loads in the row loop
-            v.g = wob[0] + (float)rl; v.x0 = w0b[0][0]; v.x1 = w0b[1][1];
-            v.m0 = (uint32_t)rl * 2654435761u; v.m1 = v.m0 >> 7;
-        } else if (rl + 32 <= r_hi) {
+        if (rl + 32 <= r_hi) {
             v.g = *gp;
             v.x0 = xp[xk0];
             v.x1 = xp[xk1];
@@ -471,7 +295,7 @@ NAV_DEV void wgrad_rows_mfma(const WgradArgs& a, int y, int n0, int k0, int64_t 
             Q[1][e] = __int_as_float(max(__float_as_int(Q[1][e]), 0));
         }
     };
-    if (r_lo >= r_hi || NAV_WG_EXP == 4) return;  // 4: tuning probe, no row loop
+    if (r_lo >= r_hi) return;
     // per 32-row tile: the operand MFMAs, their ReLU epilogue, then the tile's two 16-deep k steps
     // of the bf16 product (the partner wave on the SIMD keeps the matrix pipe busy while this one
     // waits for its operand MFMAs; double-buffering the operand tiles would not fit the 256
@@ -494,13 +318,6 @@ NAV_DEV void wgrad_rows_mfma(const WgradArgs& a, int y, int n0, int k0, int64_t 
             Split3 sp[2], sq[2];
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                if (NAV_WG_EXP == 6) {  // tuning probe: operands without the split
-                    sp[i].h = __builtin_bit_cast(bf16x8, make_float4(P[i][8 * s2], P[i][8 * s2 + 1], P[i][8 * s2 + 2], P[i][8 * s2 + 3]));
-                    sp[i].m = sp[i].l = sp[i].h;
-                    sq[i].h = __builtin_bit_cast(bf16x8, make_float4(Q[i][8 * s2], Q[i][8 * s2 + 1], Q[i][8 * s2 + 2], Q[i][8 * s2 + 3]));
-                    sq[i].m = sq[i].l = sq[i].h;
-                    continue;
-                }
                 sp[i] = split8(make_float4(P[i][8 * s2], P[i][8 * s2 + 1], P[i][8 * s2 + 2], P[i][8 * s2 + 3]),
                                make_float4(P[i][8 * s2 + 4], P[i][8 * s2 + 5], P[i][8 * s2 + 6], P[i][8 * s2 + 7]));
                 sq[i] = split8(make_float4(Q[i][8 * s2], Q[i][8 * s2 + 1], Q[i][8 * s2 + 2], Q[i][8 * s2 + 3]),
@@ -536,26 +353,8 @@ NAV_DEV TileJob wgrad_job(const WgradArgs& a, int b, int total) {
     return t;
 }
 
-// device-scope (coherent across the XCDs' L2s) 32-bit store / load: what the fused step's
-// workgroups hand each other goes through these, so no L2 writeback or invalidate is needed
-NAV_DEV void st_dev(float* p, float v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-NAV_DEV float ld_dev(const float* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-NAV_DEV void st_dev4(float4* p, float4 v) {
-    float* q = reinterpret_cast<float*>(p);
-    st_dev(q, v.x); st_dev(q + 1, v.y); st_dev(q + 2, v.z); st_dev(q + 3, v.w);
-}
-NAV_DEV float4 ld_dev4(const float4* p) {
-    const float* q = reinterpret_cast<const float*>(p);
-    return make_float4(ld_dev(q), ld_dev(q + 1), ld_dev(q + 2), ld_dev(q + 3));
-}
-
 // The tile job's partial over its split's rows, written as one slab tile (8 waves' partials
-// summed in wave order); DEV: with device-scope stores (the fused step's tile tail reads them)
-template <bool DEV>
+// summed in wave order)
 NAV_DEV void wgrad_tile(const WgradArgs& a, const TileJob& t, float* smem) {
     const int y = t.y, split = t.split, L = t.L, n0 = t.n0, k0 = t.k0;
     const MlpDev& net = a.net[y];
@@ -577,11 +376,7 @@ NAV_DEV void wgrad_tile(const WgradArgs& a, const TileJob& t, float* smem) {
             for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
     const bool pr = L == nh - 1, qr = L == 1;
     const bool full = n0 + WG_TILE <= hp && k0 + WG_TILE <= hp;
-#if NAV_WG_EXP == 3
-    if (pr && qr && full) wgrad_rows_fast(a, y, n0, k0, r_lo, r_hi, stage, acc);
-#else
     if (pr && qr && full) wgrad_rows_mfma(a, y, n0, k0, r_lo, r_hi, acc);
-#endif
     else if (pr && qr) wgrad_rows<true, true>(a, y, L, n0, k0, r_lo, r_hi, stage, acc);
     else if (pr) wgrad_rows<true, false>(a, y, L, n0, k0, r_lo, r_hi, stage, acc);
     else if (qr) wgrad_rows<false, true>(a, y, L, n0, k0, r_lo, r_hi, stage, acc);
@@ -602,17 +397,14 @@ NAV_DEV void wgrad_tile(const WgradArgs& a, const TileJob& t, float* smem) {
         float s = red[idx];
 #pragma unroll
         for (int w = 1; w < WG_WAVES; ++w) s += red[w * WG_TILE * WG_TILE + idx];
-        if (n0 + m < hp && k0 + c < hp) {
-            if (DEV) st_dev(o + (int64_t)(n0 + m) * hp + k0 + c, s);
-            else o[(int64_t)(n0 + m) * hp + k0 + c] = s;
-        }
+        if (n0 + m < hp && k0 + c < hp) o[(int64_t)(n0 + m) * hp + k0 + c] = s;
     }
 }
 
 // grid: nets x tile jobs x splits workgroups of 8 waves
 __global__ __launch_bounds__(WG_THREADS) void k_wgrad(WgradArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    wgrad_tile<false>(a, wgrad_job(a, blockIdx.x, gridDim.x), smem);
+    wgrad_tile(a, wgrad_job(a, blockIdx.x, gridDim.x), smem);
 }
 
 // ---------------- optimizer / target update, refreshing the packed images ----------------
@@ -836,164 +628,6 @@ __global__ __launch_bounds__(kBlock) void k_grad_reduce(RedArgs a) {
     red_out<ADAM>(a, rn, edge_to_flat(net, 4 * o) / 4, r);
 }
 
-// ---------------- weight gradients + reduce + Adam in one launch ----------------
-// k_wgrad, k_grad_reduce's two parts and (optionally) the soft updates as one grid of 8-wave
-// workgroups, with no workgroup ever waiting on another (arrival counters, no spinning):
-//  - edge workgroups [0, E): two 256-thread halves, each one k_grad_reduce edge block (same
-//    columns, same order), writing the finished edge gradient to grads;
-//  - tile workgroups [E, E + W): k_wgrad's tile jobs. After its slab tile a workgroup takes a
-//    ticket on its tile; the one that arrives last (splits - 1 before it) sums the tile's split
-//    slabs in k_grad_reduce's order and applies Adam (+ the net's own target soft update) to the
-//    tile's hidden weights;
-//  - soft-update workgroups [E + W, E + W + P): the extra (target, source) pairs (grid stride).
-// The edge parameters (W0, the biases, Wo) are read by every tile workgroup (h_0 and dz of the
-// top layer are recomputed from them), so their Adam step waits for the last arrival of ALL edge
-// and tile workgroups (a second ticket): that workgroup reads the edge gradients back and steps
-// them. Tickets reset themselves (the last arrival zeroes its counter). The slabs and edge
-// gradients cross XCDs (each with its own L2): they are stored and read back with device-scope
-// accesses, and a workgroup's stores complete before its ticket (take_ticket).
-// Everything is bit-identical to nav_mlp_wgrad + nav_grad_reduce(_adam)(_polyak).
-struct WgradStepArgs {
-    WgradArgs w;
-    RedArgs r;
-    int* tickets;     // [n_nets * n_hid] tile arrivals, then [1] all arrivals
-    int edge_wgs, tile_wgs, poly_wgs;
-    int edge_virt;    // k_grad_reduce edge blocks over all nets (two per edge workgroup)
-    int n_nets;
-};
-
-// Arrival on a counter: every wave waits until its device-scope stores have completed, then one
-// device-scope atomic; the returned count goes to every thread through LDS. (A C++ device-scope
-// fence here would write back and invalidate the XCD's whole L2 per wave, thrashing the
-// workgroups still in their row loops: +100 us per launch, profiles/r03y.)
-NAV_DEV int take_ticket(int* counter, int* slot) {
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-    if (threadIdx.x == 0)
-        *slot = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    const int t = *slot;
-    __syncthreads();  // the slot may be reused by the next ticket
-    return t;
-}
-
-template <bool ADAM>
-__global__ __launch_bounds__(WG_THREADS) void k_wgrad_step(WgradStepArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    __shared__ int s_ticket;
-    const RedArgs& ra = a.r;
-    int b = blockIdx.x;
-    int* all_ctr = a.tickets + a.n_nets * a.w.n_hid;
-    const int participants = a.edge_wgs + a.tile_wgs;
-    // the last of all edge and tile workgroups: Adam on every edge parameter
-    auto edge_adam = [&]() {
-        for (int q = 0; q < 2; ++q) {
-            const RedNet& rn = ra.n[q];
-            if (rn.nbe == 0) continue;
-            const int64_t e4 = edge_count(rn.net) / 4;
-            for (int64_t o = threadIdx.x; o < e4; o += WG_THREADS) {
-                const int64_t f4 = edge_to_flat(rn.net, 4 * o) / 4;
-                adam_out(ra, rn, f4, ld_dev4(rn.grad + f4));
-            }
-        }
-        if (threadIdx.x == 0) __hip_atomic_store(all_ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    };
-    if (b < a.edge_wgs) {
-        // k_grad_reduce's edge block 2b + half over 256 threads
-        const int half = threadIdx.x >> 8, t = threadIdx.x & 255;
-        int ve = 2 * b + half;
-        const bool valid = ve < a.edge_virt;
-        const bool second = ve >= ra.n[0].nbe;
-        const RedNet& rn = second ? ra.n[1] : ra.n[0];
-        if (second) ve -= ra.n[0].nbe;
-        const int64_t e4 = valid ? edge_count(rn.net) / 4 : 0;
-        const int ec = t & 15, eg = t >> 4;
-        const int64_t o = (int64_t)ve * 16 + ec;
-        float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (o < e4) {
-            // k_grad_reduce's order, 16 loads in flight per trip (the few edge workgroups hold
-            // CUs that tile workgroups wait for: their time is latency, not bandwidth)
-            const float4* col = rn.es + o;
-            int64_t k = eg;
-#pragma unroll 1
-            for (; k + 240 < ra.nblk; k += 256) {
-                float4 v[16];
-#pragma unroll
-                for (int u = 0; u < 16; ++u) v[u] = col[(k + 16 * u) * e4];
-#pragma unroll
-                for (int u = 0; u < 16; ++u) {
-                    s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w;
-                }
-            }
-            for (; k < ra.nblk; k += 16) {
-                const float4 v = col[k * e4];
-                s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-            }
-        }
-        float4* gp = reinterpret_cast<float4*>(smem) + half * 256;  // [16 groups][16 columns]
-        gp[eg * 16 + ec] = s;
-        __syncthreads();
-        if (eg == 0 && o < e4) {
-            float4 r = gp[ec];
-#pragma unroll
-            for (int q = 1; q < 16; ++q) {
-                const float4 v = gp[q * 16 + ec];
-                r.x += v.x; r.y += v.y; r.z += v.z; r.w += v.w;
-            }
-            st_dev4(rn.grad + edge_to_flat(rn.net, 4 * o) / 4, r);
-        }
-        if (ADAM && take_ticket(all_ctr, &s_ticket) == participants - 1) edge_adam();
-        return;
-    }
-    b -= a.edge_wgs;
-    if (b >= a.tile_wgs) {  // the extra soft-update pairs
-        b -= a.tile_wgs;
-        for (int64_t i = (int64_t)b * WG_THREADS + threadIdx.x; i < ra.poly.total4;
-             i += (int64_t)a.poly_wgs * WG_THREADS)
-            polyak_elem(ra.poly, i);
-        return;
-    }
-    const TileJob t = wgrad_job(a.w, b, a.tile_wgs);
-    wgrad_tile<true>(a.w, t, smem);
-    const int tile = t.y * a.w.n_hid + t.job;
-    const bool last = take_ticket(a.tickets + tile, &s_ticket) == a.w.splits - 1;
-    // this workgroup's reads of the edge parameters are done: count it for their Adam step
-    const bool all_last = ADAM && take_ticket(all_ctr, &s_ticket) == participants - 1;
-    if (last) {
-        const RedNet& rn = ra.n[t.y];
-        const MlpDev& net = rn.net;
-        const int hp = net.hp;
-        const int64_t hw4 = hidden_w_count(net) / 4, per = (int64_t)hp * hp / 4;
-        for (int idx = threadIdx.x; idx < WG_TILE * WG_TILE / 4; idx += WG_THREADS) {
-            const int m = idx / (WG_TILE / 4), c = 4 * (idx % (WG_TILE / 4));
-            if (t.n0 + m >= hp || t.k0 + c >= hp) continue;
-            const int64_t i = ((int64_t)(t.L - 1) * hp * hp + (int64_t)(t.n0 + m) * hp + t.k0 + c) / 4;
-            // k_grad_reduce's order: group g = split % 4 summed in split order, then the groups
-            const float4* col = rn.hs + i;
-            float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0, s2 = s0, s3 = s0;
-            auto add = [](float4& d, const float4 v) { d.x += v.x; d.y += v.y; d.z += v.z; d.w += v.w; };
-            int k = 0;
-            for (; k + 3 < a.w.splits; k += 4) {
-                add(s0, ld_dev4(col + (int64_t)k * hw4));
-                add(s1, ld_dev4(col + (int64_t)(k + 1) * hw4));
-                add(s2, ld_dev4(col + (int64_t)(k + 2) * hw4));
-                add(s3, ld_dev4(col + (int64_t)(k + 3) * hw4));
-            }
-            if (k < a.w.splits) add(s0, ld_dev4(col + (int64_t)k * hw4));
-            if (k + 1 < a.w.splits) add(s1, ld_dev4(col + (int64_t)(k + 1) * hw4));
-            if (k + 2 < a.w.splits) add(s2, ld_dev4(col + (int64_t)(k + 2) * hw4));
-            float4 r = s0;
-            add(r, s1);
-            add(r, s2);
-            add(r, s3);
-            red_out<ADAM>(ra, rn, net.w_off[t.L] / 4 + i % per, r);
-        }
-        if (threadIdx.x == 0) __hip_atomic_store(a.tickets + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (all_last) edge_adam();
-}
-
-
 __global__ __launch_bounds__(kBlock) void k_adam(float4* __restrict__ p,
                                                  const float4* __restrict__ g, float4* m,
                                                  float4* v, int64_t n4, float b1w, float b2,
@@ -1150,8 +784,8 @@ int32_t nav_mlp_wgrad_splits(int32_t n_nets, int32_t hidden_pad, int32_t n_hidde
     if (n_hidden < 2) return 1;
     const int TT = (hidden_pad + WG_TILE - 1) / WG_TILE;
     const int64_t jobs = (int64_t)n_nets * (n_hidden - 1) * TT * TT;
-    // NAV_WG_TOTAL workgroups (256: one 8-wave workgroup per CU), at least 512 rows per split
-    int64_t s = NAV_WG_TOTAL / jobs;
+    // WG_TOTAL workgroups (256: one 8-wave workgroup per CU), at least 512 rows per split
+    int64_t s = WG_TOTAL / jobs;
     const int64_t by_rows = (M + 511) / 512;
     if (s > by_rows) s = by_rows;
     return (int32_t)(s < 1 ? 1 : s);
@@ -1367,52 +1001,6 @@ static int grad_reduce_adam_impl(const nav_mlp* nets, int32_t n_nets, const floa
     if (rc) return rc;
     hipLaunchKernelGGL(k_grad_reduce<true>, dim3((unsigned)blocks), dim3(kBlock), 0, S(stream),
                        a);
-    NAV_CHECK_LAUNCH();
-    return 0;
-}
-
-int nav_mlp_wgrad_step(const nav_mlp* nets, int32_t n_nets, int64_t M, const float* in,
-                       int32_t ld_in, int32_t in_col, const float* const* acts,
-                       const float* const* dz, const float* const* dy, int32_t ld_dy,
-                       const uint16_t* const* masks, float* const* slabs, int32_t splits,
-                       const float* const* edge_slabs, int64_t edge_blocks, float* const* grads,
-                       float* const* m, float* const* v, float beta1, float beta2, float eps,
-                       const float* step_size, const float* bc2_sqrt, const nav_mlp* net_targets,
-                       const nav_mlp* targets, const nav_mlp* sources, int32_t n_pairs, float tau,
-                       int32_t* tickets, void* stream) {
-    WgradStepArgs a{};
-    int rblocks = 0;
-    if (!tickets || !grads) return NAV_EINVAL;
-    int rc = wgrad_args(nets, n_nets, M, in, ld_in, in_col, acts, dz, dy, ld_dy, masks, slabs,
-                        splits, a.w);
-    if (rc) return rc;
-    rc = red_args(nets, n_nets, reinterpret_cast<const float* const*>(slabs), splits, edge_slabs,
-                  edge_blocks, grads, m, v, beta1, beta2, eps, step_size, bc2_sqrt, net_targets,
-                  targets, sources, n_pairs, tau, a.r, &rblocks);
-    if (rc) return rc;
-    if (n_nets * a.w.n_hid + 1 > NAV_WGRAD_TICKETS) return NAV_EINVAL;
-    a.tickets = tickets;
-    a.n_nets = n_nets;
-    a.tile_wgs = n_nets * a.w.n_hid * splits;
-    a.edge_virt = 0;
-    for (int i = 0; i < n_nets; ++i) a.edge_virt += a.r.n[i].nbe;
-    a.edge_wgs = (a.edge_virt + 1) / 2;
-    a.poly_wgs = n_pairs ? (int)((a.r.poly.total4 + WG_THREADS - 1) / WG_THREADS < 64
-                                     ? (a.r.poly.total4 + WG_THREADS - 1) / WG_THREADS : 64)
-                         : 0;
-    const int64_t blocks = (int64_t)a.edge_wgs + a.tile_wgs + a.poly_wgs;
-    const size_t lds = wgrad_lds_bytes();
-    if (m) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wgrad_step<true>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL(k_wgrad_step<true>, dim3((unsigned)blocks), dim3(WG_THREADS), lds,
-                           S(stream), a);
-    } else {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wgrad_step<false>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL(k_wgrad_step<false>, dim3((unsigned)blocks), dim3(WG_THREADS), lds,
-                           S(stream), a);
-    }
     NAV_CHECK_LAUNCH();
     return 0;
 }

@@ -12,11 +12,6 @@ namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kMaxLayers = 9;
-// train_actor keeps the actor's top hidden layer in registers for its dWo partials (1) or writes
-// it to `acts` and reads it back (0; A/B builds)
-#ifndef NAV_ACTOR_TOP_REGS
-#define NAV_ACTOR_TOP_REGS 1
-#endif
 // workgroups hold RT row tiles of 32 rows (RT = 2; RT = 1 for small batches, row_tiles_for)
 
 struct MlpDev {

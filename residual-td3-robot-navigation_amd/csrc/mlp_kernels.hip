@@ -1,26 +1,26 @@
 // mlp_kernels.hip — the residual-TD3 actor/critic MLPs (robot.py:128-206) and their learner
 // (robot.py:209-398) on gfx950.
 //
-// Forward / row-backward: one 256-thread workgroup = 4 waves = a 128-row block kept in LDS (fp32,
-// row stride hp+4 so b128 fragment reads are conflict-free) across all layers. Hidden x hidden
-// layers run on v_mfma_f32_32x32x2_f32 (exact fp32): every wave owns 1-2 32-column tiles of all
-// 128 rows; A fragments come from the shared LDS rows, B fragments stream from the L2-resident
-// pre-packed weight image with a 2-step register prefetch, so the K loop has no barrier. The thin
-// input layer (K = 2 or 4) and output layer (N = 1 or 2) run on the VALU; ReLU derivatives travel
-// from forward to backward as C-layout bit masks. Weight gradients: one launch per network over
-// row splits writing deterministic partial slabs, reduced in a fixed order.
+// Forward / row-backward: one 256-thread workgroup = 4 waves = a block of 64 rows (32 for small
+// batches) kept in LDS as fp32 (row stride hp+4) across all layers. Hidden x hidden layers run on
+// the bf16 matrix cores (v_mfma_f32_32x32x16_bf16) at fp32 accuracy: both fp32 operands are split
+// exactly into three bf16 planes (hi + mid + lo == x) and the six partial products that carry
+// 2^-24-relative weight are accumulated in fp32 (mlp_common.h; tests/test_gpu_mlp.py pins the
+// result against an fp64 reference at 2e-6 of scale). Every wave owns 1-2 32-column tiles of all
+// the block's rows; the A operand is split once per k step into an LDS stage shared by the 4
+// waves, the B operand streams from the L2-resident split weight image (refreshed by Adam /
+// Polyak). The thin input layer (K = d_in <= 4) and the bias run on f32 MFMA (layer0_unit's fma
+// chain bit for bit), the output layer (N = 1 or 2) on the VALU with a lane-transpose reduce; ReLU
+// derivatives travel from forward to backward as C-layout bit masks. The cross-row weight
+// gradients and the reduce + Adam are learner_kernels.hip.
 #include "mlp_common.h"
 #include "nav_tick.h"
 
 
 namespace {
 
-#ifndef NAV_STAGE_DB1
-#define NAV_STAGE_DB1 1  // 32-row blocks: double-buffered split stage, one barrier per k step
-#endif
-#ifndef NAV_GEMM_SCHED
-#define NAV_GEMM_SCHED 0  // interleave hints in gemm_cols (A/B)
-#endif
+// 32-row blocks double-buffer the split stage and pass one barrier per k step (r03zt)
+constexpr bool kStageDb1 = true;
 
 template <int NT>
 struct WaveCols {
@@ -95,7 +95,7 @@ NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const bf16x8* __rest
     // 32-row blocks (small batches: latency-bound, one wave per SIMD) double-buffer the stage and
     // pass one barrier per step: step q + 1's stores go to the buffer step q - 1 was read from,
     // which every wave finished reading (and consumed in its MFMAs) before step q's barrier
-    constexpr bool DB = RT == 1 && NAV_STAGE_DB1;
+    constexpr bool DB = RT == 1 && kStageDb1;
     constexpr int SB = 3 * PP;  // bf16 per stage buffer
     auto produce = [&](int q) {
         if (sp) {
@@ -151,7 +151,6 @@ NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const bf16x8* __rest
         Split3 cur[RT];
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) cur[rt] = sa[rt];
-#ifndef NAV_AB_SKIP_GEMM
         if (wc.has0) {  // wave-uniform
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt) {
@@ -160,19 +159,6 @@ NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const bf16x8* __rest
                     acc[rt][1] = mfma_x6(cur[rt], bq1[q % (PF + 1)], acc[rt][1]);
             }
         }
-#endif
-#if NAV_GEMM_SCHED
-        // interleave: 1 MFMA, then 2 of the production's VALU / LDS / VMEM instructions
-        if constexpr (NT >= 8 && RT == 2) {
-            if (q + 1 < nq) {
-#pragma unroll
-                for (int g = 0; g < 24; ++g) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x002 | 0x020 | 0x100 | 0x200, 2, 0);
-                }
-            }
-        }
-#endif
         if (q + 1 < nq) consume(q + 1);
     }
 }
@@ -240,7 +226,7 @@ __host__ __device__ constexpr int red_floats(int tm) { return 2 * kWaves * tm; }
 
 // bytes of gemm_cols' split stage for TM rows: [3 planes][TM][16] bf16
 __host__ __device__ constexpr size_t stage_bytes(int tm) {
-    return (size_t)(tm == 32 && NAV_STAGE_DB1 ? 2 : 1) * 3 * tm * 16 * 2;
+    return (size_t)(tm == 32 && kStageDb1 ? 2 : 1) * 3 * tm * 16 * 2;
 }
 
 // rows [tm][hp+4] + input/dy staging [tm][4] + output-layer partial sums, then the split stage
@@ -770,23 +756,24 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
         }
         __syncthreads();
         DemoPend pend{false, false, 0.0, make_double2(0.0, 0.0)};
-        if (tid < TM) {
-            TickStats st{0.f, 0.f, 0.f, 0.f, 0.f};
-            if (r < M) {
-                const double2 av = make_double2(act_lds[tid * 2], act_lds[tid * 2 + 1]);
-                st = a.demo.cand ? agent_tick<true>(a.p, a.env, a.field, r, av, a.rows, a.cap,
-                                                    a.base, a.sout, true, pend)
-                                 : agent_tick<false>(a.p, a.env, a.field, r, av, a.rows, a.cap,
-                                                     a.base, a.sout, false, pend);
-            }
-            if (a.sout.block_stats && row0 + (tid & ~63) < M) wave_stats(st, a.sout.block_stats, r);
+        TickStats st{0.f, 0.f, 0.f, 0.f, 0.f};
+        if (tid < TM && r < M) {
+            const double2 av = make_double2(act_lds[tid * 2], act_lds[tid * 2 + 1]);
+            st = a.demo.cand ? agent_tick<true>(a.p, a.env, a.field, r, av, a.rows, a.cap, a.base,
+                                                a.sout, true, pend)
+                             : agent_tick<false>(a.p, a.env, a.field, r, av, a.rows, a.cap,
+                                                 a.base, a.sout, false, pend);
         }
         if (a.demo.cand) {  // block-uniform: the demo pass of the block's envs, all threads
             // the LDS rows are done with (the actions live in xin)
             auto* scratch = reinterpret_cast<DemoScratch<TM, kBlock>*>(act);
-            demo_pass<TM, kBlock>(a.p, a.demo, *scratch, pend, r, reinterpret_cast<float*>(a.rows),
-                                  a.cap, a.base, a.reward_out);
+            const double rd = demo_pass<TM, kBlock>(a.p, a.demo, *scratch, pend, r,
+                                                    reinterpret_cast<float*>(a.rows), a.cap,
+                                                    a.base, a.reward_out);
+            if (pend.need) st.r = (float)rd;  // the final reward of a flagged env
         }
+        if (tid < TM && a.sout.block_stats && row0 + (tid & ~63) < M)
+            wave_stats(st, a.sout.block_stats, r);
         return;
     }
     if (r >= M || j >= d_out) return;
@@ -1189,12 +1176,6 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
     float* dys = qv + TM;          // [TM][4] dL/dq rows of the row backward
     __bf16* stage = reinterpret_cast<__bf16*>(dys + TM * 4);  // gemm_cols' split stage
     NAV_MARK(0);
-#ifdef NAV_STAGGER_SEL
-    // A/B probe: half of the workgroups start ~NAV_STAGGER_N x 8 k cycles late (desynchronising
-    // the two workgroups of a CU, so one's epilogues overlap the other's GEMMs)
-    if (NAV_STAGGER_SEL((int)blockIdx.x))
-        for (int i = 0; i < NAV_STAGGER_N; ++i) __builtin_amdgcn_s_sleep(127);
-#endif
     const L0Pre l0_at = load_l0<NT>(a.actor_t);  // in flight under the sampling
     // target policy smoothing noise of (row, output) tid % TM, tid / TM: clamp(policy_noise * eps,
     // +-noise_clip), formed while the sampled rows are in flight
@@ -1348,13 +1329,8 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_actor_rows(ActorRowsArgs a) {
     __syncthreads();
     // the actor's top hidden layer stays in registers until dL/da is known (its dWo partials)
     f32x16 topa[RT][2];
-#if NAV_ACTOR_TOP_REGS
     fwd_net<NT, RT>(a.actor, act, stage, xin, red, a.masks_a, n_rt, a.acts, a.save_mask, row0, B, rt0,
                     topa);
-#else
-    fwd_net<NT, RT>(a.actor, act, stage, xin, red, a.masks_a, n_rt, a.acts,
-                    a.save_mask | (1u << (a.actor.n_hidden - 1)), row0, B, rt0, topa);
-#endif
     if (tid < 2 * TM) {
         const int rloc = tid % TM, j = tid / TM;
         xin[rloc * 4 + 2 + j] = row0 + rloc < B ? out_y<RT>(a.actor, red, rloc, j) : 0.f;
@@ -1380,7 +1356,6 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_actor_rows(ActorRowsArgs a) {
     // the actor's output layer gradient partials: dWo from its top-layer registers, dbo = column
     // sums of dL/da (bwd_net's order)
     float* es = a.eslab + (int64_t)blockIdx.x * a.ecount;
-#if NAV_ACTOR_TOP_REGS
     wo_grad_regs<NT, RT>(a.actor, topa, dys2, 4, es);
     if (tid < 4) {
         float sb = 0.f;
@@ -1390,11 +1365,6 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_actor_rows(ActorRowsArgs a) {
     }
     bwd_net<NT, RT>(a.actor, act, stage, dys2, xin, a.masks_a, n_rt, es, nullptr, a.dz, a.dz_save_mask,
                     row0, B, rt0);
-#else
-    bwd_net<NT, RT>(a.actor, act, stage, dys2, xin, a.masks_a, n_rt, es,
-                    a.acts + (int64_t)(a.actor.n_hidden - 1) * B * hp, a.dz, a.dz_save_mask,
-                    row0, B, rt0);
-#endif
 }
 
 
@@ -1405,15 +1375,9 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_actor_rows(ActorRowsArgs a) {
 // Small batches take RT = 1 (32-row workgroups): at M <= kSmallRows the 64-row grid leaves CUs
 // idle (config 1's 100 rows: 2 workgroups), and a 32-row block halves each wave's MFMA chain per
 // layer, so the latency-bound small-batch learner runs twice the workgroups at half the chain.
-// Not for the fused tick (its demo pass works on whole waves of envs). NAV_MLP_RT1_MAX overrides
-// the threshold (tuning only; 0 disables).
-int row_tiles_for(int64_t M, bool tick) {
-    static const int64_t small = [] {
-        const char* e = getenv("NAV_MLP_RT1_MAX");
-        return e ? (int64_t)atoll(e) : (int64_t)16384;
-    }();
-    return (!tick && M <= small) ? 1 : 2;
-}
+// Not for the fused tick (its demo pass works on whole waves of envs).
+constexpr int64_t kSmallRows = 16384;
+int row_tiles_for(int64_t M, bool tick) { return (!tick && M <= kSmallRows) ? 1 : 2; }
 
 // The row kernels (forward, row backward, critic_rows, actor_rows) are instantiated per NT in
 // their own objects (this file built with NAV_MLP_PART = NT, see the Makefile) so the heavy
@@ -1766,7 +1730,7 @@ int nav_td3_critic_rows(const nav_mlp* target_actor, const nav_mlp* target_criti
                         float* const* dq, float* const* loss_part, float* const* edge_slabs,
                         float* const* acts, uint32_t save_mask, uint16_t* const* masks,
                         int32_t row_backward, float* const* dz, uint32_t dz_save_mask,
-                        void* stream) {
+                        int32_t split_twins, void* stream) {
     CriticRowsArgs a{};
     if (row_backward && dz_save_mask && !dz) return NAV_EINVAL;
     if (!target_actor || !target_critics || !critics || !replay || !replay->rows || B < 1 ||
@@ -1798,11 +1762,8 @@ int nav_td3_critic_rows(const nav_mlp* target_actor, const nav_mlp* target_criti
     // Small batches leave most CUs idle and each workgroup's chain of network passes sets the
     // time: the twin online critics then run in separate workgroups (grid.y = 2), each repeating
     // the sampling, target actor and twin target critics (identical values) — 5 instead of 7
-    // passes per workgroup. NAV_CRITIC_SPLIT_MAX overrides the batch threshold, read at every
-    // call (tuning, and the test that runs one batch both ways).
-    const char* split_env = getenv("NAV_CRITIC_SPLIT_MAX");
-    const int64_t split_max = split_env ? (int64_t)atoll(split_env) : (int64_t)2048;
-    a.split_twins = B <= split_max ? 1 : 0;
+    // passes per workgroup. split_twins < 0 picks that form for B <= 2048 (profiles/r02aq).
+    a.split_twins = split_twins < 0 ? (B <= 2048 ? 1 : 0) : (split_twins ? 1 : 0);
     a.B = B;
     a.rows = replay->rows;
     a.rsize = size;

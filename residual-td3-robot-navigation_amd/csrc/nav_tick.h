@@ -272,9 +272,9 @@ struct DemoScratch {
 
 // All NT threads of the block call this (it synchronises). Threads 0..NE-1 own env slots; `pend`
 // of a non-owner or an env past n has need = false. Writes the final reward of every flagged env
-// into its replay row (word 4) and reward_out.
+// into its replay row (word 4) and reward_out, and returns it to the owner (0 elsewhere).
 template <int NE, int NT>
-NAV_DEV void demo_pass(const nav_params& p, const DemoIdx& d, DemoScratch<NE, NT>& S,
+NAV_DEV double demo_pass(const nav_params& p, const DemoIdx& d, DemoScratch<NE, NT>& S,
                        const DemoPend& pend, int64_t e, float* __restrict__ rows, int64_t cap,
                        int64_t base, double* __restrict__ reward_out) {
     static_assert(NE % 64 == 0 && NE <= NT, "env slots: whole waves, at most one per thread");
@@ -380,11 +380,14 @@ NAV_DEV void demo_pass(const nav_params& p, const DemoIdx& d, DemoScratch<NE, NT
         const double r = demo_reward_of(p, pend.gt, m2, pend.stuck);
         rows[((base + e) % cap) * NAV_ROW + 4] = (float)r;
         if (reward_out) reward_out[e] = r;
+        return r;
     }
+    return 0.0;
 }
 
 // Per-64-env statistics row (one wave = 64 consecutive envs): wave shuffles, lane 0 writes row
-// e0/64 of block_stats [ceil(n/64)][8] = sum reward, n_done, n_goal, n_stuck, n_ended, 0, 0, 0.
+// e0/64 of block_stats [ceil(n/64)][8] = sum reward, n_done, n_goal, n_stuck, n_ended, 0, 0, 0
+// (the reward as pushed: with the demo term when the demo pass ran in the same launch).
 // Deterministic (fixed xor tree), no LDS and no barrier. Call from every lane of the wave.
 NAV_DEV void wave_stats(const TickStats& st, float* block_stats, int64_t e0) {
     const float v0 = wave_sum(st.r), v1 = wave_sum(st.done), v2 = wave_sum(st.goal);

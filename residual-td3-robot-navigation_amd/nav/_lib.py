@@ -13,7 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # NAV_LIB: load another build of the same ABI instead (A/B timing of kernel variants only)
 LIB_PATH = os.environ.get("NAV_LIB") or os.path.join(HERE, "libnavenv.so")
 NAV_EINVAL = -100000
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 _dp = C.POINTER(C.c_double)
 _vp = C.c_void_p
@@ -112,7 +112,8 @@ SIGNATURES = [
                                       C.c_int64, C.c_int64, _vp, C.c_uint32, C.c_uint32,
                                       C.c_uint32, _vp, C.c_float, C.c_float, C.c_float, C.c_float,
                                       _vp, _P(_vp), _P(_vp), _P(_vp), _P(_vp), C.c_uint32,
-                                      _P(_vp), C.c_int32, _P(_vp), C.c_uint32, _vp]),
+                                      _P(_vp), C.c_int32, _P(_vp), C.c_uint32, C.c_int32,
+                                      _vp]),
     ("nav_td3_actor_rows", C.c_int, [_P(NavMlp), _P(NavMlp), _P(NavReplay), C.c_int64,
                                      C.c_int64, _vp, C.c_uint32, C.c_uint32, C.c_uint32, _vp,
                                      _vp, _vp, _vp, C.c_uint32, _vp, C.c_uint32, _vp, _vp, _vp,
@@ -139,11 +140,6 @@ SIGNATURES = [
      [_P(NavMlp), C.c_int32, _P(_vp), C.c_int32, _P(_vp), C.c_int64, _P(_vp), _P(_vp), _P(_vp),
       C.c_float, C.c_float, C.c_float, _P(C.c_float), _P(C.c_float), _P(NavMlp), _P(NavMlp),
       _P(NavMlp), C.c_int32, C.c_float, _vp]),
-    ("nav_mlp_wgrad_step", C.c_int,
-     [_P(NavMlp), C.c_int32, C.c_int64, _vp, C.c_int32, C.c_int32, _P(_vp), _P(_vp), _P(_vp),
-      C.c_int32, _P(_vp), _P(_vp), C.c_int32, _P(_vp), C.c_int64, _P(_vp), _P(_vp), _P(_vp),
-      C.c_float, C.c_float, C.c_float, _P(C.c_float), _P(C.c_float), _P(NavMlp), _P(NavMlp),
-      _P(NavMlp), C.c_int32, C.c_float, _vp, _vp]),
     ("nav_grad_reduce_multi", C.c_int, [_P(NavMlp), C.c_int32, _P(_vp), C.c_int32, _P(_vp),
                                         C.c_int64, _P(_vp), _vp]),
     ("nav_adam_multi", C.c_int, [_P(NavMlp), C.c_int32, _P(_vp), _P(_vp), _P(_vp), C.c_float,

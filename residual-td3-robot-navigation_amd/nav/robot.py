@@ -123,16 +123,26 @@ class TD3(_GpuTD3):
         B, dev = self.batch_size, self.device
         if len(replay_buffer) < B:
             raise TypeError("cannot unpack non-iterable NoneType object")  # robot.py:326
+        # the reference's attributes are the live hyper-parameters (a caller may set them between
+        # updates, as the reference's own td3_update reads self.* each time)
+        c = self.cfg
+        c.batch_size, c.gamma, c.tau = B, self.gamma, self.tau
+        c.policy_noise, c.noise_clip = self.policy_noise, self.noise_clip
+        c.policy_update_delay, c.num_epochs = self.policy_update_delay, self.num_epochs
         L = len(replay_buffer)
         n_idx = self.num_epochs + (self.num_epochs + self.policy_update_delay - 1) // \
             self.policy_update_delay
+        # the previous update's kernels read the pinned slots through raw pointers: wait for them
+        # before the slots are rewritten OR freed (torch's caching host allocator may hand a freed
+        # block straight to the next pin_memory())
+        if getattr(self, "_pin_done", None) is not None:
+            self._pin_done.synchronize()
+            self._pin_done = None
         pin = getattr(self, "_pin", None)
         if pin is None or pin[0].shape != (n_idx, B) or pin[1].shape[0] != self.num_epochs:
             pin = (torch.empty(n_idx, B, dtype=torch.int64).pin_memory(),
                    torch.empty(self.num_epochs, B, 2).pin_memory())
-            self._pin, self._pin_done = pin, None
-        if self._pin_done is not None:  # the previous update's kernels have read the slots
-            self._pin_done.synchronize()
+            self._pin = pin
         h_idx, h_eps = pin
         cnt = {"i": 0, "e": 0}
 

@@ -87,13 +87,14 @@ class TD3:
         # a policy epoch's soft updates inside the actor's reduce + Adam launch
         # (NAV_FUSE_SOFT_UPDATE=0: their own launch; A/B only)
         self.fuse_soft_update = os.environ.get("NAV_FUSE_SOFT_UPDATE", "1") != "0"
-        # weight gradients, reduce and Adam (+ the soft updates) in one launch
-        # (nav_mlp_wgrad_step; NAV_FUSE_WGRAD_STEP=0: nav_mlp_wgrad + the reduce launch, A/B only)
-        self.fuse_wgrad_step = os.environ.get("NAV_FUSE_WGRAD_STEP", "0") == "1"
-        # the step's arrival counters (zero, and left zero by every launch)
-        self.tickets = torch.zeros(256, dtype=torch.int32, device=self.device)
+        # the twin online critics in separate workgroups: -1 = the library's choice by batch size
+        # (1 / 0 force either form; the results are bit-identical)
+        self.split_twins = -1
         self._B = 0
-        self._st = None  # the per-epoch launches' constant ctypes arguments (_static)
+        # the per-epoch launches' constant ctypes arguments (_static), rebuilt when the batch
+        # size, the seed or a hyper-parameter they carry changes (_static_key)
+        self._st = None
+        self._st_key = None
         self._rd = (None, None)
         self.actor_losses, self.critic_losses = [], []
 
@@ -157,42 +158,6 @@ class TD3:
         return sum(4.0 * (splits * (x.count - e.shape[1]) + e.numel() +
                           (4 if adam else 1) * x.count) for x, e in zip(nets, eslabs))
 
-    def _grads_and_step(self, nets, opts, M, inp, ld_in, in_col, acts, dz, dy, ld_dy, masks,
-                        eslabs, grads, hslabs, s, stream, soft_update=False):
-        """Weight gradients, the fixed-order reduce of those and the fwd/bwd edge partials, and
-        each net's Adam step (robot.py:236-239) of 1-2 nets: one launch (nav_mlp_wgrad_step).
-        With a grad_hook (shared policy) the launch writes the flat gradient bucket without
-        Adam, the hook all-reduces it, and one multi-net Adam launch applies bucket /
-        world_size."""
-        if not self.fuse_wgrad_step:
-            return self._grads_and_step_unfused(nets, opts, M, inp, ld_in, in_col, acts, dz, dy,
-                                                ld_dy, masks, eslabs, grads, hslabs, s, stream,
-                                                soft_update)
-        net = nets[0]
-        splits = self.splits_a if net is self.actor_network else self.splits_c
-        n = len(nets)
-        wg = (descs(*nets), n, M, ptr(inp), ld_in, in_col, parr(*acts), parr(*dz), parr(*dy),
-              ld_dy, parr(*masks), parr(*hslabs), splits, parr(*eslabs), self.nblk, parr(*grads))
-        work = n * prof.mlp_wgrad_flops(net.hidden, net.n_hidden, M)
-        if self.grad_hook is None:
-            coeffs = [o.advance() for o in opts]
-            adam = (parr(*[o.m for o in opts]), parr(*[o.v for o in opts]), opts[0].b1,
-                    opts[0].b2, opts[0].eps, (C.c_float * n)(*[c[0] for c in coeffs]),
-                    (C.c_float * n)(*[c[1] for c in coeffs]))
-            if soft_update:  # the actor's step and all three soft updates in the same launch
-                tail = (descs(self.target_actor),
-                        descs(self.target_critic_network_1, self.target_critic_network_2),
-                        descs(self.critic_network_1, self.critic_network_2), 2, self.cfg.tau)
-            else:
-                tail = (None, None, None, 0, 0.0)
-            with prof.region("wgrad_step", work):
-                lib().nav_mlp_wgrad_step(*wg, *adam, *tail, ptr(self.tickets), s)
-            return
-        with prof.region("wgrad_step", work):
-            lib().nav_mlp_wgrad_step(*wg, None, None, 0.9, 0.999, 1e-8, None, None, None, None,
-                                     None, 0, 0.0, ptr(self.tickets), s)
-        self._hook_and_adam(nets, opts, grads, s, stream, soft_update)
-
     def _hook_and_adam(self, nets, opts, grads, s, stream, soft_update):
         bucket = self.grad_c if len(nets) == 2 else grads[0]
         # the collective runs on torch's current stream: make it the launch stream, so it
@@ -203,10 +168,13 @@ class TD3:
         if soft_update:
             self.soft_update_all(stream)
 
-    def _grads_and_step_unfused(self, nets, opts, M, inp, ld_in, in_col, acts, dz, dy, ld_dy,
-                                masks, eslabs, grads, hslabs, s, stream, soft_update=False):
-        """The same as two launches: nav_mlp_wgrad, then the reduce fused with Adam (or the
-        reduce alone before the hook)."""
+    def _grads_and_step(self, nets, opts, M, inp, ld_in, in_col, acts, dz, dy, ld_dy, masks,
+                        eslabs, grads, hslabs, s, stream, soft_update=False):
+        """Weight gradients (nav_mlp_wgrad), then the fixed-order reduce of those and the fwd/bwd
+        edge partials fused with each net's Adam step (robot.py:236-239) of 1-2 nets (and on a
+        policy epoch the three soft updates). With a grad_hook (shared policy) the reduce writes
+        the flat gradient bucket without Adam, the hook all-reduces it, and one multi-net Adam
+        launch applies bucket / world_size."""
         splits = self._wgrad(nets, M, inp, ld_in, in_col, acts, dz, dy, ld_dy, masks, hslabs, s)
         if self.grad_hook is None:
             coeffs = [o.advance() for o in opts]
@@ -254,13 +222,17 @@ class TD3:
     # ---- the per-epoch launches with their constant arguments built once (the small-batch
     # learner of config 1 is bound by the host's issue of ~450 launches per td3_update)
     def _fast(self):
-        return (prof._active is None and self.grad_hook is None and self.row_backward and
-                not self.fuse_wgrad_step)
+        return prof._active is None and self.grad_hook is None and self.row_backward
+
+    def _static_key(self):
+        c = self.cfg
+        return (c.batch_size, self.seed, c.policy_noise, c.noise_clip, c.max_action, c.gamma,
+                c.tau, self.split_twins)
 
     def _static(self):
-        st = self._st
-        if st is not None:
-            return st
+        key = self._static_key()
+        if self._st is not None and self._st_key == key:
+            return self._st
         c = self.cfg
         B = c.batch_size
         c1, c2, a = self.critic_network_1, self.critic_network_2, self.actor_network
@@ -277,7 +249,8 @@ class TD3:
             "cr_tail": (c.policy_noise, c.noise_clip, c.max_action, c.gamma, ptr(self.batch),
                         parr(self.dq1, self.dq2), parr(self.loss_part[0], self.loss_part[1]),
                         parr(self.eslab1, self.eslab2), parr(self.acts1, self.acts2), mid,
-                        parr(self.mask1, self.mask2), 1, parr(self.dz1, self.dz2), mid),
+                        parr(self.mask1, self.mask2), 1, parr(self.dz1, self.dz2), mid,
+                        self.split_twins),
             "ar_head": (C.byref(ca), C.byref(c1d)),
             "ar_tail": (ptr(self.batch2), ptr(self.q1), ptr(self.da), ptr(self.acts_a), mida,
                         ptr(self.dz_a), mida, ptr(self.mask_a), ptr(self.mask1),
@@ -300,7 +273,7 @@ class TD3:
                       descs(self.target_critic_network_1, self.target_critic_network_2),
                       descs(c1, c2), 2, c.tau)
         st["wgrad"] = c1.n_hidden > 1
-        self._st = st
+        self._st, self._st_key = st, key
         return st
 
     def _replay_ref(self, replay):
@@ -366,7 +339,7 @@ class TD3:
                 parr(self.dq1, self.dq2), parr(self.loss_part[0], self.loss_part[1]),
                 parr(self.eslab1, self.eslab2), parr(self.acts1, self.acts2), mid,
                 parr(self.mask1, self.mask2), int(self.row_backward), parr(self.dz1, self.dz2),
-                mid, s)
+                mid, self.split_twins, s)
         if not self.row_backward:  # separate backward launch (A/B of the fusion)
             self._bwd([c1, c2], B, [self.dq1, self.dq2], 1, [self.mask1, self.mask2], s,
                       inp=self.batch, ld_in=8, in_col=0, dz=[self.dz1, self.dz2], save_mask=mid,

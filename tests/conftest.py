@@ -39,3 +39,35 @@ def _seeded_torch():
     import torch
     torch.manual_seed(0)
     yield
+
+
+def golden_grad_check(g, name, tensors, rtol, atol_frac):
+    """Compare per-tensor gradients (torch Linear order W0, b0, W1, ...; logical sizes) with the
+    reference's own first param.grad in td3_grads.npz (make_golden.py): small tensors whole, the
+    hidden x hidden weights at their 4096 sampled entries and through three whole-tensor digests
+    (sum, sum of squares, a fixed random projection). Every compared entry within rtol + atol_frac
+    of the tensor's max; returns the scale <g, g_ref> / |g_ref|^2 over the compared entries."""
+    import numpy as np
+    dot = nrm = 0.0
+    for t, x in enumerate(tensors):
+        a = np.asarray(x, np.float64)
+        key = f"{name}_{t}"
+        if key in g.files:
+            ref = g[key].astype(np.float64)
+            got = a.reshape(ref.shape)
+        else:
+            assert tuple(g[key + "_shape"]) == a.shape, key
+            ix = g[key + "_idx"]
+            ref = g[key + "_val"].astype(np.float64)
+            got = a.ravel()[ix]
+            d = g[key + "_dig"]
+            proj = np.random.default_rng(1000 + t).standard_normal(a.size)
+            mine = np.array([a.sum(), (a * a).sum(), (a.ravel() * proj).sum()])
+            # the digests are sums of 40 000 terms: compare against the sum of magnitudes
+            mag = np.array([np.abs(a).sum(), (a * a).sum(), np.abs(a.ravel() * proj).sum()])
+            assert np.all(np.abs(mine - d) <= rtol * mag), (key, mine, d)
+        tol = rtol * np.abs(ref) + atol_frac * np.abs(ref).max()
+        assert np.all(np.abs(got - ref) <= tol), (key, float(np.abs(got - ref).max()))
+        dot += float((got * ref).sum())
+        nrm += float((ref * ref).sum())
+    return dot / nrm

@@ -12,6 +12,9 @@ Writes small .npz files next to this script:
                 set, per-step (s, a, r, s', done), tick types, Robot counters and flags
   actions.npz   Robot.get_next_action_training/testing with generator-defined actor weights
   td3.npz       TD3.td3_update(4 epochs) with generator weights, injected batches and randn noise
+  td3_grads.npz the same run's first param.grad of each optimizer (train_critic's two
+                loss.backward(), robot.py:355-363; train_actor's, robot.py:393-395): the small
+                tensors whole, the hidden x hidden weights as 4096 sampled entries + digests
 
 Usage: python tests/golden/make_golden.py   (skips cleanly when /root/reference is absent)
 """
@@ -262,6 +265,22 @@ def gen_td3(robot, epochs=4, B=100, n_trans=300):
 
     closs, aloss = [], []
     agent_train_critic, agent_train_actor = agent.train_critic, agent.train_actor
+    # the gradients the reference forms in loss.backward(), read at each optimizer's first step
+    first_grads = {}
+
+    def record(name, opt):
+        step = opt.step
+
+        def wrapped(*a, **k):
+            if name not in first_grads:
+                first_grads[name] = [p.grad.detach().clone() for g in opt.param_groups
+                                     for p in g["params"]]
+            return step(*a, **k)
+        opt.step = wrapped
+
+    record("critic1", agent.critic_optimizer_1)
+    record("critic2", agent.critic_optimizer_2)
+    record("actor", agent.actor_optimizer)
 
     def tc(rb):
         r = agent_train_critic(rb)
@@ -300,6 +319,24 @@ def gen_td3(robot, epochs=4, B=100, n_trans=300):
         out["probe_actor"] = agent.actor_network(torch.tensor(probe)).numpy()
         out["probe_q1"] = agent.critic_network_1(torch.tensor(probe), torch.tensor(probe_a)).numpy()
     np.savez_compressed(os.path.join(OUT, "td3.npz"), **out)
+    gout = dict(critic_idx=idx[0], actor_idx=idx[1], noise=noise[0])
+    grng = np.random.default_rng(99)
+    for name, grads in first_grads.items():
+        for t, g in enumerate(grads):
+            a = g.numpy().astype(np.float32)
+            key = f"{name}_{t}"
+            if a.size <= 1024:
+                gout[key] = a
+            else:  # a hidden x hidden weight: sampled entries + whole-tensor digests
+                ix = grng.integers(0, a.size, 4096)
+                proj = np.random.default_rng(1000 + t).standard_normal(a.size)
+                gout[key + "_idx"] = ix
+                gout[key + "_val"] = a.ravel()[ix]
+                gout[key + "_shape"] = np.array(a.shape)
+                gout[key + "_dig"] = np.array([a.astype(np.float64).sum(),
+                                               (a.astype(np.float64) ** 2).sum(),
+                                               (a.astype(np.float64).ravel() * proj).sum()])
+    np.savez_compressed(os.path.join(OUT, "td3_grads.npz"), **gout)
 
 
 def main():

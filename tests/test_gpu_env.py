@@ -234,6 +234,7 @@ def test_agent_step_vs_oracle_per_step(nav, orc):
     ost = VecAgentState(n)
     rng = np.random.default_rng(0)
     rows_o = np.zeros((rep.capacity, 8), np.float32)
+    checked_demo = 0
     for t in range(40):
         # push some envs towards their goals so goal hits happen, freeze others to get stuck
         s = env.state.cpu().numpy(); gl = env.goal.cpu().numpy()
@@ -248,6 +249,7 @@ def test_agent_step_vs_oracle_per_step(nav, orc):
         # oracle: per-group demo set
         ns_o = np.zeros((n, 2))
         flags_o = np.zeros(n, np.int64)
+        r_o = np.zeros(n)
         for grp in range(G):
             sl = slice(grp * epg, (grp + 1) * epg)
             sub = VecAgentState(epg)
@@ -261,6 +263,7 @@ def test_agent_step_vs_oracle_per_step(nav, orc):
                 # the oracle tick was called with env index j: redo its reset draw for env e
                 ns_o[e] = ns
                 flags_o[e] = fl
+                r_o[e] = r
                 rows_o[(base + e) % rep.capacity] = row
             for k in ("state", "goal", "region", "hist", "meta", "plan_index", "path_length",
                       "episodes", "noise_scale"):
@@ -283,8 +286,19 @@ def test_agent_step_vs_oracle_per_step(nav, orc):
         idx = (base + np.arange(n)) % rep.capacity
         close = np.abs(got[idx] - rows_o[idx]) <= 1e-5 * np.maximum(1, np.abs(rows_o[idx]))
         assert close.all(), t
-    st = env.block_stats.sum(0).cpu().numpy()
-    assert st[1] == (flags_o & 1).sum() and st[3] == ((flags_o & 4) != 0).sum()
+        # the launch's reward / done reduction (north_star: reduced by wavefront shuffles), every
+        # column of every 64-env row: the pushed reward (demo term included: the fused launch)
+        # within 1e-5 relative, the done / goal / stuck / ended counts exact
+        bs = env.block_stats.cpu().numpy().astype(np.float64)
+        rows64 = lambda v: v.reshape(-1, 64).sum(1)  # noqa: E731
+        cols = (r_o, flags_o & 1, (flags_o >> 1) & 1, (flags_o >> 2) & 1, (flags_o >> 3) & 1)
+        ref = np.stack([rows64(np.asarray(c, np.float64)) for c in cols], 1)
+        mag = rows64(np.abs(r_o))
+        assert np.all(np.abs(bs[:, 0] - ref[:, 0]) <= 1e-5 * np.maximum(1.0, mag)), t
+        assert np.array_equal(bs[:, 1:5], ref[:, 1:5]), t
+        assert (bs[:, 5:] == 0).all()
+        checked_demo += int(((fl_dev & 16) != 0).sum())
+    assert checked_demo > 0  # the demo term was part of the checked sums
 
 
 def test_agent_step_replays_reference_trace(nav):

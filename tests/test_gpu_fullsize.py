@@ -206,3 +206,72 @@ def test_td3_update_at_bench_config_vs_oracle():
         # MI355X: <= 3e-8; the two paths only differ in the order the batch rows are summed)
         print(f"{name}: max |diff| {float(d.max()):.3e}")
         assert float(d.max()) <= 2e-7, name
+
+
+def _flat_vs_tensors(net, flat, ref_tensors, tag):
+    """Compare a device-layout flat gradient with per-tensor reference gradients ([W0, b0, W1,
+    ...] at logical sizes): every entry within rtol 1e-4 + 1e-6 of the tensor's max, padding
+    exactly zero; returns (<g, g_ref>, |g_ref|^2) over the whole net."""
+    from nav.mlp import layer_offsets
+    offs, _ = layer_offsets(net.d_in, net.d_out, net.hp, net.n_hidden)
+    dot, nrm = 0.0, 0.0
+    for l, (w_off, b_off, fo, fi) in enumerate(offs):
+        for ref, got in ((ref_tensors[2 * l], flat[w_off:w_off + fo * fi].view(fo, fi)),
+                         (ref_tensors[2 * l + 1], flat[b_off:b_off + fo].view(fo))):
+            ref = ref.detach().double()
+            sl = tuple(slice(0, n) for n in ref.shape)
+            g = got[sl].double()
+            bad = (g - ref).abs() > 1e-4 * ref.abs() + 1e-6 * ref.abs().max()
+            print(f"{tag} layer {l} {tuple(ref.shape)}: max rel {float(((g - ref).abs() / (ref.abs() + 1e-30)).max()):.2e}, "
+                  f"outside tol {int(bad.sum())}")
+            assert not bad.any(), (tag, l, tuple(ref.shape))
+            pad = got.clone()
+            pad[sl] = 0
+            assert (pad == 0).all(), (tag, l)
+            dot += float((g * ref).sum())
+            nrm += float((ref * ref).sum())
+    return dot, nrm
+
+
+def test_learner_gradients_at_bench_config_vs_oracle():
+    """The learner's gradients themselves at the bench configuration (2x256, B = 32 768: the
+    64-row row-kernel form, 8 / 16 weight-gradient splits) against the oracle's autograd of
+    robot.py:341-363 / 382-395 on the same batch and noise, BEFORE any Adam step — Adam's first
+    step is lr * sign(g) and later ones are scale-invariant, so a parameter comparison cannot see
+    a uniform gradient-scale error (a wrong 2/B, -1/B or split count); this does. The oracle uses
+    the kernels' own ReLU decisions (pre-activations within rounding of 0 may branch either way).
+    Every entry within rtol 1e-4; scale <g, g_ref> / |g_ref|^2 within 1e-5 of 1 per net."""
+    from test_gpu_mlp import relu_bits
+    from test_gpu_shared_policy import make_learner, replay_rows, ring_of
+    from oracle.td3_oracle import TD3Oracle, make_mlp_params
+    B, hidden, nh = 32768, 256, 2
+    sizes = lambda di, do: [di] + [hidden] * nh + [do]  # noqa: E731
+    params = (make_mlp_params(91, sizes(2, 2)), make_mlp_params(92, sizes(4, 1)),
+              make_mlp_params(93, sizes(4, 1)))
+    td3 = make_learner(B, hidden, nh, params)
+    rows = replay_rows(4 * B, 19)
+    rep = ring_of(rows)
+    rng = np.random.default_rng(23)
+    ic, ia = rng.integers(0, len(rows), B), rng.integers(0, len(rows), B)
+    noise = rng.standard_normal((B, 2)).astype(np.float32)
+    T = lambda x, dt=None: torch.tensor(x, dtype=dt, device=DEV)  # noqa: E731
+    gc = td3.critic_gradients(rep, idx=T(ic, torch.int64), eps=T(noise)).cpu()
+    hp = td3.critic_network_1.hp
+    bits = {"c1": relu_bits(td3.mask1, nh, hp, hidden, B), "c2": relu_bits(td3.mask2, nh, hp, hidden, B)}
+    ora = TD3Oracle(*params)
+    r = rows[ic]
+    ora.train_critic((r[:, 0:2], r[:, 2:4], r[:, 4], r[:, 5:7], r[:, 7] > 0.5), noise, bits=bits)
+    cc = td3.critic_network_1.count
+    for k, (key, net) in enumerate((("c1", td3.critic_network_1), ("c2", td3.critic_network_2))):
+        dot, nrm = _flat_vs_tensors(net, gc[k * cc:(k + 1) * cc], ora.last_grads[key], key)
+        print(f"{key}: scale {dot / nrm:.8f}")
+        assert abs(dot / nrm - 1.0) <= 1e-5, key
+    # the critics' Adam step from that bucket (train_critic's), then train_actor's gradient
+    td3.critic_step()
+    ga = td3.actor_gradients(rep, idx=T(ia, torch.int64)).cpu()
+    bits = {"actor": relu_bits(td3.mask_a, nh, hp, hidden, B),
+            "c1": relu_bits(td3.mask1, nh, hp, hidden, B)}
+    ora.train_actor(rows[ia][:, 0:2], bits=bits)
+    dot, nrm = _flat_vs_tensors(td3.actor_network, ga, ora.last_grads["actor"], "actor")
+    print(f"actor: scale {dot / nrm:.8f}")
+    assert abs(dot / nrm - 1.0) <= 1e-5

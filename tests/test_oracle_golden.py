@@ -158,3 +158,26 @@ def test_cpu_demo_index_equals_brute_force(orc):
         for x, y in q:
             want = orc.lib().orc_demo_min(orc.ptr(d, orc._dp), len(d), float(x), float(y))
             assert ix.min(float(x), float(y)) == want
+
+
+def test_td3_oracle_gradients_vs_reference():
+    """The oracle's autograd gradients (TD3Oracle.last_grads) of the first train_critic and
+    train_actor equal the reference's own param.grad (td3_grads.npz, robot.py:355-363, 393-395)
+    on the same weights, batches and noise: the oracle is pinned at the gradient level, where
+    Adam's sign-like first step hides a gradient scale."""
+    from conftest import golden_grad_check
+    from oracle.td3_oracle import TD3Oracle, make_mlp_params
+    g, gg = golden("td3.npz"), golden("td3_grads.npz")
+    ora = TD3Oracle(make_mlp_params(21, [2, 200, 200, 200, 2]),
+                    make_mlp_params(22, [4, 200, 200, 200, 1]),
+                    make_mlp_params(23, [4, 200, 200, 200, 1]))
+    S, A, R, S2, D = (g[k] for k in ("S", "A", "R", "S2", "D"))
+    i = gg["critic_idx"]
+    assert np.array_equal(i, g["idx"][0]) and np.array_equal(gg["noise"], g["noise"][0])
+    ora.train_critic((S[i], A[i], R[i], S2[i], D[i]), gg["noise"])
+    for name, key in (("critic1", "c1"), ("critic2", "c2")):
+        sc = golden_grad_check(gg, name, [t.numpy() for t in ora.last_grads[key]], 1e-6, 1e-7)
+        assert abs(sc - 1) <= 1e-6, (name, sc)
+    ora.train_actor(S[gg["actor_idx"]])
+    sc = golden_grad_check(gg, "actor", [t.numpy() for t in ora.last_grads["actor"]], 1e-6, 1e-7)
+    assert abs(sc - 1) <= 1e-6, sc
