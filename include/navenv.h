@@ -385,8 +385,10 @@ int nav_mlp_backward(const nav_mlp* nets, int32_t n_nets, int64_t M, const float
  * [s*P, (s+1)*P), P = ceil(M/splits) rounded up to 64). h_0 is recomputed from `in`,
  * dz_{n_hidden-1} from dy[i] and masks[i]; acts[i] / dz[i] (saved layers 1 .. n_hidden-2) are
  * read only for n_hidden > 2. Any splits >= 1 is valid; nav_mlp_wgrad_splits gives the count
- * that fills the chip (one 64 x 64 tile workgroup per CU). */
-int32_t nav_mlp_wgrad_splits(int32_t n_nets, int32_t hidden_pad, int32_t n_hidden, int64_t M);
+ * that fills the chip (one tile workgroup per CU; the tile is 128 x 64 for d_out = 1 at
+ * n_hidden = 2 and hidden_pad % 128 == 0, else 64 x 64). */
+int32_t nav_mlp_wgrad_splits(int32_t n_nets, int32_t d_out, int32_t hidden_pad, int32_t n_hidden,
+                             int64_t M);
 int nav_mlp_wgrad(const nav_mlp* nets, int32_t n_nets, int64_t M, const float* in,
                   int32_t ld_in, int32_t in_col, const float* const* acts,
                   const float* const* dz, const float* const* dy, int32_t ld_dy,

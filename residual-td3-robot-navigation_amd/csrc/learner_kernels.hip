@@ -11,13 +11,15 @@ namespace {
 // dW_L = dz_L^T h_{L-1} for L = 1 .. nh-1 over the rows of each split. The thin layers' gradients
 // (W0, every bias, Wo, bo) are edge partials of the forward / backward kernels instead.
 //
-// Work decomposition: one workgroup = 8 waves = one 64 x 64 output tile (n0.., k0..) of one
+// Work decomposition: one workgroup = 8 waves = one tn x 64 output tile (n0.., k0..) of one
 // layer of one network over the rows of one split; each wave takes 1/8 of the split's rows and
-// keeps the tile in 4 v_mfma_f32_32x32x2_f32 accumulators (the MFMA K dimension is the batch
-// row), the 8 partial tiles are summed through LDS in wave order and the workgroup writes ONE
-// 16 KB partial slab tile. 256 workgroups (one per CU, 2 waves per SIMD) cover the twin critics
-// at 8 splits or the actor at 16, so the slabs are 4 MB per launch (was 64 row splits x 128 x 128
-// tiles = 27 MB) and the reduce reads 8-16 slabs instead of 64.
+// keeps the tile in 32 x 32 accumulators (the MFMA K dimension is the batch row), the 8 partial
+// tiles are summed through LDS in a fixed order and the workgroup writes ONE partial slab tile.
+// 256 workgroups (one per CU, 2 waves per SIMD) fill the chip, so the slabs are 4-8 MB per
+// launch and the reduce reads 8-16 slabs.
+// 2-hidden-layer networks with whole tiles (the bench shape) take the factored path
+// (wgrad_rows_fact: the ReLU bit as an exact bf16 A operand, Wo applied after the sum, tn = 128
+// for d_out = 1). Every other shape takes the f32 MFMA path below (tn = 64).
 // Operands come straight from registers, no panel staging and no barrier in the row loop: for
 // the batch rows (2 per MFMA step: lane half h = row parity) every lane forms its own A element
 // P[row][n0 + 32 i + lane] and B element Q[row][k0 + 32 j + lane]. P = dz of the top hidden
@@ -38,8 +40,11 @@ struct WgradArgs {
     const uint16_t* masks[2];  // the forward's ReLU bit image
     float* slabs[2];        // [splits][(nh-1) hp hp]
     int splits;
-    int TT;                 // 64-wide tiles across hp
-    int n_hid;              // tile jobs per network = (nh - 1) * TT * TT
+    int TT;                 // 64-wide tiles across hp (the k side of a tile)
+    int tn;                 // tile height on the n side: 64, or 128 (wgrad_tile_fact, d_out = 1)
+    int TN;                 // tn-high tiles across hp
+    int n_hid;              // tile jobs per network = (nh - 1) * TN * TT
+    int fact;               // 1: the factored-Wo path (wgrad_tile_fact) for every tile
     int64_t per_split;      // rows per split (multiple of 64)
     int64_t per_wave;       // rows per wave (multiple of 64)
 };
@@ -53,6 +58,15 @@ constexpr int WG_CHUNK = 64;  // rows per staged chunk (lane = row)
 constexpr int WG_STAGE_FLOATS = WG_CHUNK * 6;  // one slot; 2 slots per wave (double buffer)
 inline size_t wgrad_lds_bytes() {
     return ((size_t)WG_WAVES * WG_TILE * WG_TILE + (size_t)WG_WAVES * 2 * WG_STAGE_FLOATS) * 4;
+}
+// The factored path's tile height: 128 rows of n for d_out = 1 when hp allows (NI = 4 column
+// tiles per wave at 128 accumulator registers), else 64. The path itself needs a 2-hidden-layer
+// network with whole 64 x 64 tiles.
+__host__ __device__ inline bool wgrad_fact_ok(int hp, int n_hidden) {
+    return n_hidden == 2 && hp % WG_TILE == 0;
+}
+__host__ __device__ inline int wgrad_tile_n(int d_out, int hp, int n_hidden) {
+    return wgrad_fact_ok(hp, n_hidden) && d_out == 1 && hp % 128 == 0 ? 128 : WG_TILE;
 }
 
 // rows [r_lo, r_hi) of one wave into acc (tile n0.., k0.. of layer L of net y)
@@ -186,150 +200,256 @@ NAV_DEV void wgrad_rows(const WgradArgs& a, int y, int L, int n0, int k0, int64_
     }
 }
 
-// The MFMA-operand path for a full 64 x 64 tile of a 2-hidden-layer network (the bench shape).
-// The operands are produced by MFMAs too: per 32-row tile, dz = dy . Wo (K = d_out <= 2, one
-// v_mfma_f32_32x32x2_f32 per 32 columns) and h_0 = x . W0^T + b0 (K = d_in <= 4, two MFMAs on
-// the bias as C) land in the C layout, where lane (l32, h) register e holds row
-// acc_row(e, h) of column l32. Taking the weight-gradient MFMA's K (batch-row) order as
-// step e <-> rows {acc_row(e, 0), acc_row(e, 1)}, register e of those tiles IS the A / B operand
-// of step e, and bit e of the lane's own ReLU mask word (the forward's C-layout image) is the
-// ReLU derivative of exactly that element. Per 64 weight-gradient MFMAs a wave issues 6 operand
-// MFMAs and ~100 VALU (mask, relu) instead of ~320 VALU: the f32 MFMA shares the SIMD's issue
-// with the VALU, so the VALU count per MFMA is what sets the rate. No LDS, no barrier in the
-// row loop. h_0 and dz are the forward's / backward's values as fused f32 chains in the same
-// order (layer0_unit: b + x0 w0 + x1 w1 + ..., top_unit: g0 w0 + g1 w1).
-NAV_DEV void wgrad_rows_mfma(const WgradArgs& a, int y, int n0, int k0, int64_t r_lo,
-                             int64_t r_hi, f32x16 (&acc)[2][2]) {
+// ---- the factored form for 2-hidden-layer networks (the bench shape) ----
+// With e the forward's ReLU bit of the top hidden layer and g_d = dL/dy_d,
+//   dz_1[r][n] = e[r][n] sum_d g_d[r] Wo[d][n]        (robot.py:355-363 autograd, d < d_out)
+//   dW_1[n][k] = sum_r dz_1[r][n] h_0[r][k] = sum_d Wo[d][n] S_d[n][k],
+//   S_d[n][k]  = sum_r e[r][n] Q_d[r][k],   Q_d[r][k] = g_d[r] h_0[r][k].
+// The A operand of S_d is the ReLU bit itself, exact in bf16 (as 2.0: one bit of the pattern, so
+// a dword of two elements is a shift and an AND of the mask word; the 0.5 goes into Wo), and
+// only the B operand Q_d is split — three bf16 planes, exactly, so the product carries f32
+// accuracy with 3 MFMAs per 16-deep k step and 32 x 32 tile instead of the 6 of a product with
+// both operands split, and nothing per element on the n side. That frees a wave to own NI = 4
+// column tiles of n (128 x 64) at D = 1 — the twin critics — for 128 accumulator registers.
+
+// bits b .. b+7 of a C-layout mask word (w2 = w | w << 15: bit b+1 sits 16 above bit b) as the 8
+// bf16 elements of an A fragment: 2.0 (0x4000) where the bit is set, else 0
+NAV_DEV bf16x8 bits_frag(uint32_t w2, int b) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 r;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) r[d] = (w2 << (14 - b - 2 * d)) & 0x40004000u;
+    return __builtin_bit_cast(bf16x8, r);
+}
+
+template <int NI, int D>
+NAV_DEV void wgrad_rows_fact(const WgradArgs& a, int y, int n0, int k0, int64_t r_lo,
+                             int64_t r_hi, f32x16 (&out)[NI][2]) {
     const MlpDev& net = a.net[y];
-    const int hp = net.hp, nh = net.n_hidden, d_in = net.d_in, d_out = net.d_out;
+    const int hp = net.hp, d_in = net.d_in;
     const int lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
     const int64_t M = a.M;
     const int NTm = hp >> 5;
-    // constant B operands of the operand MFMAs: Wo rows (k = output j = h), W0 columns (k = h,
-    // then 2 + h), and the bias through a K = 2 MFMA of (1, 0) x (b, 0): the C tile starts at b
-    // exactly, so h_0 accumulates in layer0_unit's order b + x0 w0 + x1 w1 + x2 w2 + x3 w3
-    float wob[2], w0b[2][2], bob[2];
+    f32x16 acc[D][NI][2];
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) acc[d][i][j][e] = 0.f;
+    // h_0 = relu(x . W0^T + b0) by f32 MFMAs in the C layout, where lane (l32, h) register e
+    // holds row acc_row(e, h) of column l32. Constant B operands: W0 columns (k = h, then 2 + h),
+    // and the bias through a K = 2 MFMA of (1, 0) x (b, 0), so the C tile starts at b exactly and
+    // h_0 accumulates in layer0_unit's order b + x0 w0 + x1 w1 + x2 w2 + x3 w3
+    float w0b[2][2], bob[2];
     {
-        const float* Wo = net.params + net.w_off[nh];
         const float* W0 = net.params + net.w_off[0];
         const float* bb = net.params + net.b_off[0];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            wob[i] = h < d_out ? Wo[h * hp + n0 + 32 * i + l32] : 0.f;
-            const int c = k0 + 32 * i + l32;
-            w0b[i][0] = h < d_in ? W0[c * d_in + h] : 0.f;
-            w0b[i][1] = 2 + h < d_in ? W0[c * d_in + 2 + h] : 0.f;
-            bob[i] = h == 0 ? bb[c] : 0.f;
+        for (int j = 0; j < 2; ++j) {
+            const int c = k0 + 32 * j + l32;
+            w0b[j][0] = h < d_in ? W0[c * d_in + h] : 0.f;
+            w0b[j][1] = 2 + h < d_in ? W0[c * d_in + 2 + h] : 0.f;
+            bob[j] = h == 0 ? bb[c] : 0.f;
         }
     }
     const float one = h == 0 ? 1.f : 0.f;
-    const uint16_t* mk = a.masks[y] + (size_t)(nh - 1) * mask_rowtiles(M) * NTm * 64 +
-                         (size_t)(n0 >> 5) * 64 + lane;
+    const bool x23 = d_in > 2;
     const size_t mstride = (size_t)NTm * 64;
+    const uint16_t* mp = a.masks[y] + (size_t)mask_rowtiles(M) * mstride +  // layer 1's bits
+                         (size_t)(n0 >> 5) * 64 + lane + (size_t)(r_lo >> 5) * mstride;
     const float* dyp = a.dy[y];
     const int ld_dy = a.ld_dy, ld_in = a.ld_in;
-    const float* xin = a.in + a.in_col;
-    // raw loads of a 32-row tile (A operands: lane l32 = row, h = k; the lane's 2 mask words),
-    // in tile order through running per-lane pointers (a 64-bit add per stream and tile: the
-    // address math is VALU, which the f32 MFMA waits for); a partial last tile reads clamped rows,
-    // and what does not exist is zeroed where it is used
-    const int gk = h < d_out ? h : 0, xk0 = h < d_in ? h : 0, xk1 = 2 + h < d_in ? 2 + h : 0;
+    const int xk0 = h < d_in ? h : 0, xk1 = 2 + h < d_in ? 2 + h : 0;
+    // the tile's own A operands (x row of lane l32, inputs k = h and 2 + h) and the lane's NI
+    // mask words; the main loop keeps the next full tile's in flight
     struct Raw {
-        float g, x0, x1;
-        uint32_t m0, m1;
+        float x0, x1;
+        uint32_t m[NI];
     };
-    const float* gp = dyp + (r_lo + l32) * ld_dy + gk;
-    const float* xp = xin + (r_lo + l32) * ld_in;
-    const uint16_t* mp = mk + (size_t)(r_lo >> 5) * mstride;
-    const int64_t gstep = 32 * (int64_t)ld_dy, xstep = 32 * (int64_t)ld_in;
-    int64_t rl = r_lo;  // first row of the next tile to load
-    auto load = [&](int64_t) {
-        Raw v;
-        if (rl + 32 <= r_hi) {
-            v.g = *gp;
-            v.x0 = xp[xk0];
-            v.x1 = xp[xk1];
-            v.m0 = mp[0];
-            v.m1 = mp[64];
-        } else {  // rows past r_hi read row r_lo (the values are not used)
-            const bool ok = rl + l32 < r_hi;
-            const float* g = ok ? gp : dyp + r_lo * ld_dy + gk;
-            const float* x = ok ? xp : xin + r_lo * ld_in;
-            v.g = *g;
-            v.x0 = x[xk0];
-            v.x1 = x[xk1];
-            v.m0 = mp[0];
-            v.m1 = mp[64];
+    auto load_raw = [&](int64_t rt, Raw& v) {
+        const int64_t rx = rt + l32 < r_hi ? rt + l32 : r_lo;  // absent rows read row r_lo
+        const float* x = a.in + a.in_col + rx * ld_in;
+        v.x0 = x[xk0];
+        v.x1 = x[xk1];
+        const uint16_t* m = mp + (size_t)((rt - r_lo) >> 5) * mstride;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) v.m[i] = m[i * 64];
+    };
+    // one 32-row tile: h_0 by the f32 MFMAs, Q_d = relu(h_0) g_d split per k step, 3 MFMAs per
+    // (i, j, d) and step. gs[s2][d][t]: g_d of the row of register e = 8 s2 + t
+    auto tile = [&](const Raw& cur, const float (&gs)[2][D][8]) {
+        const float x0 = h < d_in ? cur.x0 : 0.f, x1 = 2 + h < d_in ? cur.x1 : 0.f;
+        // one 32-column half j of the k side at a time (16 registers of h_0 live)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const f32x16 zero = {};
+            f32x16 Z = mfma(one, bob[j], zero);
+            Z = mfma(x0, w0b[j][0], Z);
+            if (x23) Z = mfma(x1, w0b[j][1], Z);
+            // registers 8s .. 8s+7 of the C layout are k step s (rows 16s + 8(t>>2) + 4h +
+            // (t&3)), the same rows as bits 8s .. 8s+7 of the lane's mask words
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+                for (int d = 0; d < D; ++d) {
+                    float q[8];
+#pragma unroll
+                    for (int t = 0; t < 8; ++t)
+                        q[t] = __int_as_float(max(__float_as_int(Z[8 * s2 + t]), 0)) * gs[s2][d][t];
+                    const Split3 sq = split8(make_float4(q[0], q[1], q[2], q[3]),
+                                             make_float4(q[4], q[5], q[6], q[7]));
+#pragma unroll
+                    for (int i = 0; i < NI; ++i) {
+                        // formed right before its 3 MFMAs in every pass (2 VALU per dword): an
+                        // opaque copy of the mask word keeps the compiler from holding all the
+                        // fragments live across the passes
+                        uint32_t mw;
+                        asm volatile("v_mov_b32 %0, %1" : "=v"(mw) : "v"(cur.m[i]));
+                        const bf16x8 pi = bits_frag(mw | (mw << 15), 8 * s2);
+                        acc[d][i][j] = mfma16(pi, sq.l, acc[d][i][j]);
+                        acc[d][i][j] = mfma16(pi, sq.m, acc[d][i][j]);
+                        acc[d][i][j] = mfma16(pi, sq.h, acc[d][i][j]);
+                    }
+                }
         }
-        gp += gstep;
-        xp += xstep;
-        mp += mstride;
-        rl += 32;
-        return v;
     };
-    // operand MFMAs of one tile (results in the C layout, masked later by finish())
-    auto issue = [&](int64_t rt, const Raw& v, f32x16 (&P)[2], f32x16 (&Q)[2]) {
-        const bool ok = rt + l32 < r_hi && h < d_out;  // rows past r_hi: dz = 0, add nothing
-        const float g = ok ? v.g : 0.f;
-        const float x0 = h < d_in ? v.x0 : 0.f, x1 = 2 + h < d_in ? v.x1 : 0.f;
-        const f32x16 zero = {};
+    // whole tiles: dy rows as float4 (ld_dy = d_out and 16-B aligned, else element loads), one
+    // tile ahead like the x rows and mask words
+    const bool gvec = ld_dy == D && ((uintptr_t)dyp & 15) == 0;
+    const int64_t r_full = r_lo + ((r_hi - r_lo) & ~(int64_t)31);
+    auto load_g = [&](int64_t rt, float (&gs)[2][D][8]) {
+        const float* gp = dyp + (rt + 4 * h) * ld_dy;  // row rt + 4h
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            P[i] = mfma(g, wob[i], zero);
-            Q[i] = mfma(one, bob[i], zero);
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+            for (int qq = 0; qq < 2; ++qq) {
+                const float* g = gp + (16 * s2 + 8 * qq) * ld_dy;
+                if (gvec && D == 1) {
+                    const float4 u = *reinterpret_cast<const float4*>(g);
+                    gs[s2][0][4 * qq] = u.x; gs[s2][0][4 * qq + 1] = u.y;
+                    gs[s2][0][4 * qq + 2] = u.z; gs[s2][0][4 * qq + 3] = u.w;
+                } else if (gvec) {
+                    const float4 u0 = *reinterpret_cast<const float4*>(g);
+                    const float4 u1 = *reinterpret_cast<const float4*>(g + 4);
+                    gs[s2][0][4 * qq] = u0.x; gs[s2][D - 1][4 * qq] = u0.y;
+                    gs[s2][0][4 * qq + 1] = u0.z; gs[s2][D - 1][4 * qq + 1] = u0.w;
+                    gs[s2][0][4 * qq + 2] = u1.x; gs[s2][D - 1][4 * qq + 2] = u1.y;
+                    gs[s2][0][4 * qq + 3] = u1.z; gs[s2][D - 1][4 * qq + 3] = u1.w;
+                } else {
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)
+#pragma unroll
+                        for (int d = 0; d < D; ++d) gs[s2][d][4 * qq + t] = g[t * ld_dy + d];
+                }
+            }
+    };
+    if (r_lo < r_full) {
+        // d_out = 2 loads its 32 g values at the tile (prefetched they do not fit the registers)
+        constexpr bool GPF = D == 1;
+        Raw cur, nxt;
+        float gc[2][D][8], gn[2][D][8];
+        load_raw(r_lo, cur);
+        if (GPF) load_g(r_lo, gc);
+        for (int64_t rt = r_lo; rt < r_full; rt += 32) {
+            if (rt + 32 < r_full) {
+                load_raw(rt + 32, nxt);
+                if (GPF) load_g(rt + 32, gn);
+            }
+            if (!GPF) load_g(rt, gc);
+            tile(cur, gc);
+            cur = nxt;
+            if (GPF) {
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+                    for (int d = 0; d < D; ++d)
+#pragma unroll
+                        for (int t = 0; t < 8; ++t) gc[s2][d][t] = gn[s2][d][t];
+            }
         }
-#pragma unroll
-        for (int i = 0; i < 2; ++i) Q[i] = mfma(x0, w0b[i][0], Q[i]);
-#pragma unroll
-        for (int i = 0; i < 2; ++i) Q[i] = mfma(x1, w0b[i][1], Q[i]);
-    };
-    // ReLU derivative of the top layer on P (bit e of the lane's word as an all-ones mask) and
-    // the layer-0 ReLU on Q (an integer max of the bit pattern: one v_max_i32)
-    auto finish = [&](const Raw& v, f32x16 (&P)[2], f32x16 (&Q)[2]) {
+    }
+    if (r_full < r_hi) {  // the last, partial tile of the rows (M % 32 rows)
+        Raw cur;
+        load_raw(r_full, cur);
+        float gs[2][D][8];
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-            // v_bfe_i32 of one bit: 0 or all ones
-            P[0][e] = __int_as_float(__float_as_int(P[0][e]) & __builtin_amdgcn_sbfe((int)v.m0, e, 1));
-            P[1][e] = __int_as_float(__float_as_int(P[1][e]) & __builtin_amdgcn_sbfe((int)v.m1, e, 1));
-            Q[0][e] = __int_as_float(max(__float_as_int(Q[0][e]), 0));
-            Q[1][e] = __int_as_float(max(__float_as_int(Q[1][e]), 0));
+            const int64_t r = r_full + acc_row(e, h);
+#pragma unroll
+            for (int d = 0; d < D; ++d) gs[e >> 3][d][e & 7] = r < r_hi ? dyp[r * ld_dy + d] : 0.f;
         }
-    };
-    if (r_lo >= r_hi) return;
-    // per 32-row tile: the operand MFMAs, their ReLU epilogue, then the tile's two 16-deep k steps
-    // of the bf16 product (the partner wave on the SIMD keeps the matrix pipe busy while this one
-    // waits for its operand MFMAs; double-buffering the operand tiles would not fit the 256
-    // registers of two waves per SIMD next to the split fragments). The raw loads run two tiles
-    // ahead.
-    Raw cur = load(r_lo);
-    Raw nxt = cur;
-    if (r_lo + 32 < r_hi) nxt = load(r_lo + 32);
-    for (int64_t rt = r_lo; rt < r_hi; rt += 32) {
-        Raw nn = nxt;
-        if (rt + 64 < r_hi) nn = load(rt + 64);
-        f32x16 P[2], Q[2];
-        issue(rt, cur, P, Q);
-        finish(cur, P, Q);
-        // registers 8s .. 8s+7 of the C-layout operands are k step s (rows 16s + 8(j>>2) + 4h +
-        // (j&3), the same for P and Q), each split three ways (mlp_common.h) right before its six
-        // partial products
+        tile(cur, gs);
+    }
+    // dW tile = sum_d (Wo[d][n] / 2) S_d: register e of tile (i, j) is row n = n0 + 32 i +
+    // acc_row(e, h)
+    const float* Wo = net.params + net.w_off[net.n_hidden];
 #pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-            Split3 sp[2], sq[2];
+    for (int i = 0; i < NI; ++i) {
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                sp[i] = split8(make_float4(P[i][8 * s2], P[i][8 * s2 + 1], P[i][8 * s2 + 2], P[i][8 * s2 + 3]),
-                               make_float4(P[i][8 * s2 + 4], P[i][8 * s2 + 5], P[i][8 * s2 + 6], P[i][8 * s2 + 7]));
-                sq[i] = split8(make_float4(Q[i][8 * s2], Q[i][8 * s2 + 1], Q[i][8 * s2 + 2], Q[i][8 * s2 + 3]),
-                               make_float4(Q[i][8 * s2 + 4], Q[i][8 * s2 + 5], Q[i][8 * s2 + 6], Q[i][8 * s2 + 7]));
+        for (int q = 0; q < 4; ++q) {
+            const int n = n0 + 32 * i + 8 * q + 4 * h;
+            float4 wv[D];
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                const float* w = Wo + d * hp + n;
+                wv[d] = make_float4(w[0], w[1], w[2], w[3]);
             }
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
+            for (int t = 0; t < 4; ++t) {
+                const int e = 4 * q + t;
 #pragma unroll
-                for (int j = 0; j < 2; ++j) acc[i][j] = mfma_x6s(sp[i], sq[j], acc[i][j]);
+                for (int j = 0; j < 2; ++j) {
+                    const float w0 = (t == 0 ? wv[0].x : t == 1 ? wv[0].y : t == 2 ? wv[0].z : wv[0].w) * 0.5f;
+                    float v = w0 * acc[0][i][j][e];
+                    if (D > 1) {
+                        const float w1 = (t == 0 ? wv[D - 1].x : t == 1 ? wv[D - 1].y
+                                          : t == 2 ? wv[D - 1].z : wv[D - 1].w) * 0.5f;
+                        v = fmaf(w1, acc[D - 1][i][j][e], v);
+                    }
+                    out[i][j][e] = v;
+                }
+            }
         }
-        cur = nxt;
-        nxt = nn;
+    }
+}
+
+// The NI tiles of each wave summed across the 8 waves through LDS (R slots of NI*32 x 64 floats
+// in 128 KB: waves w and w + R share slot w % R, in wave order) and written as one slab tile.
+template <int NI>
+NAV_DEV void wgrad_reduce_write(const WgradArgs& a, int y, int split, int L, int n0, int k0,
+                                const f32x16 (&acc)[NI][2], float* red) {
+    constexpr int T = NI * 32 * WG_TILE;
+    constexpr int R = (WG_WAVES * WG_TILE * WG_TILE) / T < WG_WAVES
+                          ? (WG_WAVES * WG_TILE * WG_TILE) / T : WG_WAVES;
+    const MlpDev& net = a.net[y];
+    const int hp = net.hp;
+    const int wv = wave_id(), lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
+    float* mine = red + (wv % R) * T;
+#pragma unroll
+    for (int round = 0; round < WG_WAVES / R; ++round) {
+        if (wv / R == round) {
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) {
+                        float* p = mine + (32 * i + acc_row(e, h)) * WG_TILE + 32 * j + l32;
+                        *p = round ? *p + acc[i][j][e] : acc[i][j][e];
+                    }
+        }
+        __syncthreads();
+    }
+    float* o = a.slabs[y] + (int64_t)split * hidden_w_count(net) + (int64_t)(L - 1) * hp * hp;
+    for (int idx = threadIdx.x; idx < T; idx += WG_THREADS) {
+        const int m = idx / WG_TILE, c = idx % WG_TILE;
+        float s = red[idx];
+#pragma unroll
+        for (int w = 1; w < R; ++w) s += red[w * T + idx];
+        if (n0 + m < hp && k0 + c < hp) o[(int64_t)(n0 + m) * hp + k0 + c] = s;
     }
 }
 
@@ -342,29 +462,43 @@ struct TileJob {
 };
 NAV_DEV TileJob wgrad_job(const WgradArgs& a, int b, int total) {
     const int v = (total % 8 == 0) ? (b % 8) * (total / 8) + b / 8 : b;
-    const int grp = v / a.n_hid, TT = a.TT;
+    const int grp = v / a.n_hid, TT = a.TT, TN = a.TN;
     TileJob t;
     t.job = v % a.n_hid;
     t.y = grp / a.splits;
     t.split = grp % a.splits;
-    t.L = t.job / (TT * TT) + 1;
-    t.n0 = ((t.job % (TT * TT)) / TT) * WG_TILE;
+    t.L = t.job / (TN * TT) + 1;
+    t.n0 = ((t.job % (TN * TT)) / TT) * a.tn;
     t.k0 = (t.job % TT) * WG_TILE;
     return t;
+}
+
+// split s's rows for wave wv: [r_lo, r_hi)
+NAV_DEV void wave_rows(const WgradArgs& a, int split, int wv, int64_t& r_lo, int64_t& r_hi) {
+    const int64_t M = a.M;
+    const int64_t s_lo = (int64_t)split * a.per_split < M ? (int64_t)split * a.per_split : M;
+    const int64_t s_hi = s_lo + a.per_split < M ? s_lo + a.per_split : M;
+    r_lo = s_lo + wv * a.per_wave < s_hi ? s_lo + wv * a.per_wave : s_hi;
+    r_hi = r_lo + a.per_wave < s_hi ? r_lo + a.per_wave : s_hi;
+}
+
+template <int NI, int D>
+NAV_DEV void wgrad_tile_fact(const WgradArgs& a, const TileJob& t, float* smem) {
+    int64_t r_lo, r_hi;
+    wave_rows(a, t.split, wave_id(), r_lo, r_hi);
+    f32x16 out[NI][2];
+    wgrad_rows_fact<NI, D>(a, t.y, t.n0, t.k0, r_lo, r_hi, out);
+    wgrad_reduce_write<NI>(a, t.y, t.split, t.L, t.n0, t.k0, out, smem);
 }
 
 // The tile job's partial over its split's rows, written as one slab tile (8 waves' partials
 // summed in wave order)
 NAV_DEV void wgrad_tile(const WgradArgs& a, const TileJob& t, float* smem) {
     const int y = t.y, split = t.split, L = t.L, n0 = t.n0, k0 = t.k0;
-    const MlpDev& net = a.net[y];
-    const int hp = net.hp, nh = net.n_hidden;
-    const int wv = wave_id(), lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
-    const int64_t M = a.M;
-    const int64_t s_lo = (int64_t)split * a.per_split < M ? (int64_t)split * a.per_split : M;
-    const int64_t s_hi = s_lo + a.per_split < M ? s_lo + a.per_split : M;
-    const int64_t r_lo = s_lo + wv * a.per_wave < s_hi ? s_lo + wv * a.per_wave : s_hi;
-    const int64_t r_hi = r_lo + a.per_wave < s_hi ? r_lo + a.per_wave : s_hi;
+    const int nh = a.net[y].n_hidden;
+    const int wv = wave_id();
+    int64_t r_lo, r_hi;
+    wave_rows(a, split, wv, r_lo, r_hi);
     float* red = smem;                                          // [8][64][64]
     float* stage = smem + WG_WAVES * WG_TILE * WG_TILE + wv * 2 * WG_STAGE_FLOATS;
     f32x16 acc[2][2];
@@ -375,36 +509,24 @@ NAV_DEV void wgrad_tile(const WgradArgs& a, const TileJob& t, float* smem) {
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
     const bool pr = L == nh - 1, qr = L == 1;
-    const bool full = n0 + WG_TILE <= hp && k0 + WG_TILE <= hp;
-    if (pr && qr && full) wgrad_rows_mfma(a, y, n0, k0, r_lo, r_hi, acc);
-    else if (pr && qr) wgrad_rows<true, true>(a, y, L, n0, k0, r_lo, r_hi, stage, acc);
+    if (pr && qr) wgrad_rows<true, true>(a, y, L, n0, k0, r_lo, r_hi, stage, acc);
     else if (pr) wgrad_rows<true, false>(a, y, L, n0, k0, r_lo, r_hi, stage, acc);
     else if (qr) wgrad_rows<false, true>(a, y, L, n0, k0, r_lo, r_hi, stage, acc);
     else wgrad_rows<false, false>(a, y, L, n0, k0, r_lo, r_hi, stage, acc);
     // the 8 partial tiles meet in LDS, summed in wave order
-    float* mine = red + wv * WG_TILE * WG_TILE;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int e = 0; e < 16; ++e)
-                mine[(32 * i + acc_row(e, h)) * WG_TILE + 32 * j + l32] = acc[i][j][e];
-    __syncthreads();
-    float* o = a.slabs[y] + (int64_t)split * hidden_w_count(net) + (int64_t)(L - 1) * hp * hp;
-    for (int idx = threadIdx.x; idx < WG_TILE * WG_TILE; idx += WG_THREADS) {
-        const int m = idx / WG_TILE, c = idx % WG_TILE;
-        float s = red[idx];
-#pragma unroll
-        for (int w = 1; w < WG_WAVES; ++w) s += red[w * WG_TILE * WG_TILE + idx];
-        if (n0 + m < hp && k0 + c < hp) o[(int64_t)(n0 + m) * hp + k0 + c] = s;
-    }
+    wgrad_reduce_write<2>(a, y, split, L, n0, k0, acc, red);
 }
 
-// grid: nets x tile jobs x splits workgroups of 8 waves
+// grid: nets x tile jobs x splits workgroups of 8 waves (one kernel per path: each gets its own
+// register allocation)
 __global__ __launch_bounds__(WG_THREADS) void k_wgrad(WgradArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     wgrad_tile(a, wgrad_job(a, blockIdx.x, gridDim.x), smem);
+}
+template <int NI, int D>
+__global__ __launch_bounds__(WG_THREADS) void k_wgrad_fact(WgradArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    wgrad_tile_fact<NI, D>(a, wgrad_job(a, blockIdx.x, gridDim.x), smem);
 }
 
 // ---------------- optimizer / target update, refreshing the packed images ----------------
@@ -777,13 +899,16 @@ bool red_net(const nav_mlp* net, const float* hs, int splits, const float* es, f
 
 extern "C" {
 
-int32_t nav_mlp_wgrad_splits(int32_t n_nets, int32_t hidden_pad, int32_t n_hidden, int64_t M) {
-    if (n_nets < 1 || n_nets > 2 || hidden_pad < 32 || hidden_pad > 256 || (hidden_pad & 31) ||
-        n_hidden < 1 || M < 0)
+int32_t nav_mlp_wgrad_splits(int32_t n_nets, int32_t d_out, int32_t hidden_pad, int32_t n_hidden,
+                             int64_t M) {
+    if (n_nets < 1 || n_nets > 2 || d_out < 1 || d_out > 2 || hidden_pad < 32 ||
+        hidden_pad > 256 || (hidden_pad & 31) || n_hidden < 1 || M < 0)
         return NAV_EINVAL;
     if (n_hidden < 2) return 1;
     const int TT = (hidden_pad + WG_TILE - 1) / WG_TILE;
-    const int64_t jobs = (int64_t)n_nets * (n_hidden - 1) * TT * TT;
+    const int tn = wgrad_tile_n(d_out, hidden_pad, n_hidden);
+    const int TN = (hidden_pad + tn - 1) / tn;
+    const int64_t jobs = (int64_t)n_nets * (n_hidden - 1) * TN * TT;
     // WG_TOTAL workgroups (256: one 8-wave workgroup per CU), at least 512 rows per split
     int64_t s = WG_TOTAL / jobs;
     const int64_t by_rows = (M + 511) / 512;
@@ -818,8 +943,12 @@ static int wgrad_args(const nav_mlp* nets, int32_t n_nets, int64_t M, const floa
     a.in_col = in_col;
     a.ld_dy = ld_dy;
     a.splits = splits;
-    a.TT = (a.net[0].hp + WG_TILE - 1) / WG_TILE;
-    a.n_hid = (a.net[0].n_hidden - 1) * a.TT * a.TT;
+    const int hp = a.net[0].hp, nh = a.net[0].n_hidden;
+    a.TT = (hp + WG_TILE - 1) / WG_TILE;
+    a.tn = wgrad_tile_n(a.net[0].d_out, hp, nh);
+    a.TN = (hp + a.tn - 1) / a.tn;
+    a.n_hid = (nh - 1) * a.TN * a.TT;
+    a.fact = wgrad_fact_ok(hp, nh);
     // 64-row aligned splits and per-wave ranges: a chunk's mask row tiles start on a tile boundary
     a.per_split = ((M + splits - 1) / splits + WG_CHUNK - 1) / WG_CHUNK * WG_CHUNK;
     a.per_wave = ((a.per_split + WG_WAVES - 1) / WG_WAVES + WG_CHUNK - 1) / WG_CHUNK * WG_CHUNK;
@@ -839,9 +968,12 @@ int nav_mlp_wgrad(const nav_mlp* nets, int32_t n_nets, int64_t M, const float* i
     if (a.net[0].n_hidden < 2) return 0;
     const int64_t blocks = (int64_t)n_nets * a.n_hid * splits;
     const size_t lds = wgrad_lds_bytes();
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wgrad),
+    void (*k)(WgradArgs) = !a.fact ? k_wgrad
+                           : a.tn == 128 ? k_wgrad_fact<4, 1>
+                           : a.net[0].d_out == 1 ? k_wgrad_fact<2, 1> : k_wgrad_fact<2, 2>;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(k_wgrad, dim3((unsigned)blocks), dim3(WG_THREADS), lds, S(stream), a);
+    hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(WG_THREADS), lds, S(stream), a);
     NAV_CHECK_LAUNCH();
     return 0;
 }

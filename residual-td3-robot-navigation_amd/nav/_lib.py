@@ -131,7 +131,8 @@ SIGNATURES = [
     ("nav_mlp_wgrad", C.c_int, [_P(NavMlp), C.c_int32, C.c_int64, _vp, C.c_int32, C.c_int32,
                                 _P(_vp), _P(_vp), _P(_vp), C.c_int32, _P(_vp), _P(_vp), C.c_int32,
                                 _vp]),
-    ("nav_mlp_wgrad_splits", C.c_int32, [C.c_int32, C.c_int32, C.c_int32, C.c_int64]),
+    ("nav_mlp_wgrad_splits", C.c_int32, [C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                          C.c_int64]),
     ("nav_grad_reduce", C.c_int, [_P(NavMlp), _vp, C.c_int32, _vp, C.c_int64, _vp, _vp]),
     ("nav_grad_reduce_adam", C.c_int, [_P(NavMlp), C.c_int32, _P(_vp), C.c_int32, _P(_vp),
                                        C.c_int64, _P(_vp), _P(_vp), _P(_vp), C.c_float, C.c_float,

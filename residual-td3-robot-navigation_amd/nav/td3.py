@@ -125,8 +125,8 @@ class TD3:
         # row splits of the weight-gradient launch (partial slabs): critic twins and actor
         # separately, as many as fill the chip (NAV_WGRAD_SPLITS="critic,actor" overrides;
         # tuning only)
-        sc = L.nav_mlp_wgrad_splits(2, hp, nh, B)
-        sa = L.nav_mlp_wgrad_splits(1, hp, nh, B)
+        sc = L.nav_mlp_wgrad_splits(2, self.critic_network_1.d_out, hp, nh, B)
+        sa = L.nav_mlp_wgrad_splits(1, self.actor_network.d_out, hp, nh, B)
         env = os.environ.get("NAV_WGRAD_SPLITS")
         if env:
             sc, sa = (max(1, min(int(v), max(1, B // 32))) for v in env.split(","))

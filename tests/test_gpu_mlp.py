@@ -186,7 +186,11 @@ def relu_bits(masks, nh, hp, hidden, M):
                                                     (4, 1, 64, 1, 300), (2, 2, 96, 4, 333),
                                                     # 64-row blocks (RT = 2, > 16 384 rows)
                                                     (4, 1, 256, 2, 16421), (2, 2, 200, 3, 16421),
-                                                    (4, 1, 64, 1, 16421)])
+                                                    (4, 1, 64, 1, 16421),
+                                                    # factored weight gradient, 64-high n tiles
+                                                    # (hp 192), and the f32 path at n_hidden 2
+                                                    # with partial tiles (hp 96)
+                                                    (4, 1, 192, 2, 3001), (2, 2, 96, 2, 1000)])
 def test_backward_and_weight_grads_vs_autograd(nav, d_in, d_out, hidden, nh, M):
     """Row backward + per-block edge partials + recomputing hidden weight gradients + reduce
     against torch autograd; every gradient entry must be written (NaN-filled buffers)."""
@@ -687,7 +691,7 @@ def _f64_forward(layers, x):
 
 
 @pytest.mark.parametrize("d_in,d_out,hidden,nh", [(2, 2, 200, 3), (4, 1, 200, 3), (2, 2, 256, 2),
-                                                  (4, 1, 256, 2)])
+                                                  (4, 1, 256, 2), (4, 1, 192, 2)])
 @pytest.mark.parametrize("M", [4097, 16421])
 def test_split_gemm_f32_accuracy_vs_fp64(nav, d_in, d_out, hidden, nh, M):
     """nav_mlp_forward and the row backward (nav_mlp_backward: dz rows and dx) against an fp64

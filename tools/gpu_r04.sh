@@ -1,0 +1,52 @@
+#!/bin/bash
+# One gpurun call of round 4 (run from the repo root through gpurun): the named steps in order,
+# each under its own time limit; a fault / abort / timeout (exit status other than 0 or 1) ends
+# the call there. Output under gpurun_out/TAG/.
+#   tests     GPU test suite
+#   mlptests  the MLP / learner GPU tests only
+#   smoke     __graft_entry__.smoke()
+#   wgrad     tools/wgrad_bench.py on this tree and on abl/head (the previous HEAD, if present)
+#   ab        interleaved same-box bench A/B: this tree vs abl/head, 3 rounds
+#   bench     the default bench line
+#   prof      rocprofv3 kernel trace + stats of a short bench
+#   pmc       FETCH_SIZE / WRITE_SIZE / SQ passes of a short bench (separate runs)
+# usage: bash tools/gpu_r04.sh TAG step...
+set -u
+TAG=$1; shift
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+ROOT=$(pwd)
+O=$ROOT/gpurun_out/$TAG
+mkdir -p "$O"
+: > "$O/status.txt"
+SHORT="--steps 20 --warmup 3 --no-cpu-baseline --no-utd-sweep --no-sweep --long-steps 0"
+PMCB="--steps 4 --warmup 2 --no-cpu-baseline --no-utd-sweep --no-sweep --long-steps 0"
+run() {
+  local name=$1 t=$2; shift 2
+  local t0=$(date +%s)
+  timeout -k 10 "$t" "$@" > "$O/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc $(( $(date +%s) - t0 ))s" | tee -a "$O/status.txt"
+  if [ "$rc" -ne 0 ] && [ "$rc" -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit "$rc"; fi
+  return 0
+}
+for step in "$@"; do
+  case "$step" in
+    tests) run gputest 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
+    mlptests) run mlptest 300 python -u -m pytest tests/test_gpu_mlp.py tests/test_gpu_fullsize.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    wgrad) run wgrad_new 200 python tools/wgrad_bench.py
+           if [ -d abl/head ]; then (cd abl/head && run wgrad_old 200 python tools/wgrad_bench.py); fi ;;
+    ab) for r in 1 2 3; do
+          run ab_new_$r 200 python bench.py $SHORT --steps 60 --warmup 5 --no-timed-events
+          (cd abl/head && run ab_old_$r 200 python bench.py $SHORT --steps 60 --warmup 5 --no-timed-events)
+        done ;;
+    bench) run bench 500 python bench.py ;;
+    prof) run prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace" -o run -- python bench.py $SHORT ;;
+    pmc) run pmc_fetch 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/fetch" -o run -- python bench.py $PMCB &&
+         run pmc_write 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/write" -o run -- python bench.py $PMCB &&
+         run pmc_sq 150 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$O/sq" -o run -- python bench.py $PMCB ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo done >> "$O/status.txt"
