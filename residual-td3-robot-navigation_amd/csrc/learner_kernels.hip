@@ -200,6 +200,154 @@ NAV_DEV void wgrad_rows(const WgradArgs& a, int y, int L, int n0, int k0, int64_
     }
 }
 
+// The MFMA-operand path for a full 64 x 64 tile of a 2-hidden-layer network with d_out = 2 (the
+// actor; d_out = 1 takes the factored path below).
+// The operands are produced by MFMAs too: per 32-row tile, dz = dy . Wo (K = d_out <= 2, one
+// v_mfma_f32_32x32x2_f32 per 32 columns) and h_0 = x . W0^T + b0 (K = d_in <= 4, two MFMAs on
+// the bias as C) land in the C layout, where lane (l32, h) register e holds row
+// acc_row(e, h) of column l32. Taking the weight-gradient MFMA's K (batch-row) order as
+// step e <-> rows {acc_row(e, 0), acc_row(e, 1)}, register e of those tiles IS the A / B operand
+// of step e, and bit e of the lane's own ReLU mask word (the forward's C-layout image) is the
+// ReLU derivative of exactly that element. Per 64 weight-gradient MFMAs a wave issues 6 operand
+// MFMAs and ~100 VALU (mask, relu) instead of ~320 VALU: the f32 MFMA shares the SIMD's issue
+// with the VALU, so the VALU count per MFMA is what sets the rate. No LDS, no barrier in the
+// row loop. h_0 and dz are the forward's / backward's values as fused f32 chains in the same
+// order (layer0_unit: b + x0 w0 + x1 w1 + ..., top_unit: g0 w0 + g1 w1).
+NAV_DEV void wgrad_rows_mfma(const WgradArgs& a, int y, int n0, int k0, int64_t r_lo,
+                             int64_t r_hi, f32x16 (&acc)[2][2]) {
+    const MlpDev& net = a.net[y];
+    const int hp = net.hp, nh = net.n_hidden, d_in = net.d_in, d_out = net.d_out;
+    const int lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
+    const int64_t M = a.M;
+    const int NTm = hp >> 5;
+    // constant B operands of the operand MFMAs: Wo rows (k = output j = h), W0 columns (k = h,
+    // then 2 + h), and the bias through a K = 2 MFMA of (1, 0) x (b, 0): the C tile starts at b
+    // exactly, so h_0 accumulates in layer0_unit's order b + x0 w0 + x1 w1 + x2 w2 + x3 w3
+    float wob[2], w0b[2][2], bob[2];
+    {
+        const float* Wo = net.params + net.w_off[nh];
+        const float* W0 = net.params + net.w_off[0];
+        const float* bb = net.params + net.b_off[0];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            wob[i] = h < d_out ? Wo[h * hp + n0 + 32 * i + l32] : 0.f;
+            const int c = k0 + 32 * i + l32;
+            w0b[i][0] = h < d_in ? W0[c * d_in + h] : 0.f;
+            w0b[i][1] = 2 + h < d_in ? W0[c * d_in + 2 + h] : 0.f;
+            bob[i] = h == 0 ? bb[c] : 0.f;
+        }
+    }
+    const float one = h == 0 ? 1.f : 0.f;
+    const uint16_t* mk = a.masks[y] + (size_t)(nh - 1) * mask_rowtiles(M) * NTm * 64 +
+                         (size_t)(n0 >> 5) * 64 + lane;
+    const size_t mstride = (size_t)NTm * 64;
+    const float* dyp = a.dy[y];
+    const int ld_dy = a.ld_dy, ld_in = a.ld_in;
+    const float* xin = a.in + a.in_col;
+    // raw loads of a 32-row tile (A operands: lane l32 = row, h = k; the lane's 2 mask words),
+    // in tile order through running per-lane pointers (a 64-bit add per stream and tile: the
+    // address math is VALU, which the f32 MFMA waits for); a partial last tile reads clamped rows,
+    // and what does not exist is zeroed where it is used
+    const int gk = h < d_out ? h : 0, xk0 = h < d_in ? h : 0, xk1 = 2 + h < d_in ? 2 + h : 0;
+    struct Raw {
+        float g, x0, x1;
+        uint32_t m0, m1;
+    };
+    const float* gp = dyp + (r_lo + l32) * ld_dy + gk;
+    const float* xp = xin + (r_lo + l32) * ld_in;
+    const uint16_t* mp = mk + (size_t)(r_lo >> 5) * mstride;
+    const int64_t gstep = 32 * (int64_t)ld_dy, xstep = 32 * (int64_t)ld_in;
+    int64_t rl = r_lo;  // first row of the next tile to load
+    auto load = [&](int64_t) {
+        Raw v;
+        if (rl + 32 <= r_hi) {
+            v.g = *gp;
+            v.x0 = xp[xk0];
+            v.x1 = xp[xk1];
+            v.m0 = mp[0];
+            v.m1 = mp[64];
+        } else {  // rows past r_hi read row r_lo (the values are not used)
+            const bool ok = rl + l32 < r_hi;
+            const float* g = ok ? gp : dyp + r_lo * ld_dy + gk;
+            const float* x = ok ? xp : xin + r_lo * ld_in;
+            v.g = *g;
+            v.x0 = x[xk0];
+            v.x1 = x[xk1];
+            v.m0 = mp[0];
+            v.m1 = mp[64];
+        }
+        gp += gstep;
+        xp += xstep;
+        mp += mstride;
+        rl += 32;
+        return v;
+    };
+    // operand MFMAs of one tile (results in the C layout, masked later by finish())
+    auto issue = [&](int64_t rt, const Raw& v, f32x16 (&P)[2], f32x16 (&Q)[2]) {
+        const bool ok = rt + l32 < r_hi && h < d_out;  // rows past r_hi: dz = 0, add nothing
+        const float g = ok ? v.g : 0.f;
+        const float x0 = h < d_in ? v.x0 : 0.f, x1 = 2 + h < d_in ? v.x1 : 0.f;
+        const f32x16 zero = {};
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            P[i] = mfma(g, wob[i], zero);
+            Q[i] = mfma(one, bob[i], zero);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) Q[i] = mfma(x0, w0b[i][0], Q[i]);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) Q[i] = mfma(x1, w0b[i][1], Q[i]);
+    };
+    // ReLU derivative of the top layer on P (bit e of the lane's word as an all-ones mask) and
+    // the layer-0 ReLU on Q (an integer max of the bit pattern: one v_max_i32)
+    auto finish = [&](const Raw& v, f32x16 (&P)[2], f32x16 (&Q)[2]) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            // v_bfe_i32 of one bit: 0 or all ones
+            P[0][e] = __int_as_float(__float_as_int(P[0][e]) & __builtin_amdgcn_sbfe((int)v.m0, e, 1));
+            P[1][e] = __int_as_float(__float_as_int(P[1][e]) & __builtin_amdgcn_sbfe((int)v.m1, e, 1));
+            Q[0][e] = __int_as_float(max(__float_as_int(Q[0][e]), 0));
+            Q[1][e] = __int_as_float(max(__float_as_int(Q[1][e]), 0));
+        }
+    };
+    if (r_lo >= r_hi) return;
+    // per 32-row tile: the operand MFMAs, their ReLU epilogue, then the tile's two 16-deep k steps
+    // of the bf16 product (the partner wave on the SIMD keeps the matrix pipe busy while this one
+    // waits for its operand MFMAs; double-buffering the operand tiles would not fit the 256
+    // registers of two waves per SIMD next to the split fragments). The raw loads run two tiles
+    // ahead.
+    Raw cur = load(r_lo);
+    Raw nxt = cur;
+    if (r_lo + 32 < r_hi) nxt = load(r_lo + 32);
+    for (int64_t rt = r_lo; rt < r_hi; rt += 32) {
+        Raw nn = nxt;
+        if (rt + 64 < r_hi) nn = load(rt + 64);
+        f32x16 P[2], Q[2];
+        issue(rt, cur, P, Q);
+        finish(cur, P, Q);
+        // registers 8s .. 8s+7 of the C-layout operands are k step s (rows 16s + 8(j>>2) + 4h +
+        // (j&3), the same for P and Q), each split three ways (mlp_common.h) right before its six
+        // partial products
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+            Split3 sp[2], sq[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                sp[i] = split8(make_float4(P[i][8 * s2], P[i][8 * s2 + 1], P[i][8 * s2 + 2], P[i][8 * s2 + 3]),
+                               make_float4(P[i][8 * s2 + 4], P[i][8 * s2 + 5], P[i][8 * s2 + 6], P[i][8 * s2 + 7]));
+                sq[i] = split8(make_float4(Q[i][8 * s2], Q[i][8 * s2 + 1], Q[i][8 * s2 + 2], Q[i][8 * s2 + 3]),
+                               make_float4(Q[i][8 * s2 + 4], Q[i][8 * s2 + 5], Q[i][8 * s2 + 6], Q[i][8 * s2 + 7]));
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) acc[i][j] = mfma_x6s(sp[i], sq[j], acc[i][j]);
+        }
+        cur = nxt;
+        nxt = nn;
+    }
+}
+
 // ---- the factored form for 2-hidden-layer networks (the bench shape) ----
 // With e the forward's ReLU bit of the top hidden layer and g_d = dL/dy_d,
 //   dz_1[r][n] = e[r][n] sum_d g_d[r] Wo[d][n]        (robot.py:355-363 autograd, d < d_out)
@@ -224,7 +372,7 @@ NAV_DEV bf16x8 bits_frag(uint32_t w2, int b) {
 
 template <int NI, int D>
 NAV_DEV void wgrad_rows_fact(const WgradArgs& a, int y, int n0, int k0, int64_t r_lo,
-                             int64_t r_hi, f32x16 (&out)[NI][2]) {
+                             int64_t r_hi, const char* tab, f32x16 (&out)[NI][2]) {
     const MlpDev& net = a.net[y];
     const int hp = net.hp, d_in = net.d_in;
     const int lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
@@ -306,9 +454,16 @@ NAV_DEV void wgrad_rows_fact(const WgradArgs& a, int y, int n0, int k0, int64_t 
                         // formed right before its 3 MFMAs in every pass (2 VALU per dword): an
                         // opaque copy of the mask word keeps the compiler from holding all the
                         // fragments live across the passes
+#ifdef NAV_WGRAD_BITS_VALU
                         uint32_t mw;
                         asm volatile("v_mov_b32 %0, %1" : "=v"(mw) : "v"(cur.m[i]));
                         const bf16x8 pi = bits_frag(mw | (mw << 15), 8 * s2);
+#else
+                        // byte s2 of the mask word as the 16-B entry's offset
+                        uint32_t ta = (s2 == 0 ? cur.m[i] << 4 : cur.m[i] >> 4) & 0xFF0u;
+                        asm volatile("" : "+v"(ta));
+                        const bf16x8 pi = *reinterpret_cast<const bf16x8*>(tab + ta);
+#endif
                         acc[d][i][j] = mfma16(pi, sq.l, acc[d][i][j]);
                         acc[d][i][j] = mfma16(pi, sq.m, acc[d][i][j]);
                         acc[d][i][j] = mfma16(pi, sq.h, acc[d][i][j]);
@@ -316,6 +471,60 @@ NAV_DEV void wgrad_rows_fact(const WgradArgs& a, int y, int n0, int k0, int64_t 
                 }
         }
     };
+#ifdef NAV_WGRAD_SGB
+    // the same products as units u = (j, s2) with the split of unit u + 1 interleaved into unit
+    // u's 12 MFMAs by scheduling-group barriers (5 VALU per MFMA gap; A/B variant)
+    auto tile_sgb = [&](const Raw& cur, const float (&gs)[2][D][8]) {
+        const float x0 = h < d_in ? cur.x0 : 0.f, x1 = 2 + h < d_in ? cur.x1 : 0.f;
+        f32x16 Z[2];
+        const f32x16 zero = {};
+#pragma unroll
+        for (int j = 0; j < 2; ++j) Z[j] = mfma(one, bob[j], zero);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) Z[j] = mfma(x0, w0b[j][0], Z[j]);
+        if (x23) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) Z[j] = mfma(x1, w0b[j][1], Z[j]);
+        }
+        auto unit = [&](int u) {
+            const int j = u >> 1, s2 = u & 1;
+            float q[8];
+#pragma unroll
+            for (int t = 0; t < 8; ++t)
+                q[t] = __int_as_float(max(__float_as_int(Z[j][8 * s2 + t]), 0)) * gs[s2][0][t];
+            return split8(make_float4(q[0], q[1], q[2], q[3]), make_float4(q[4], q[5], q[6], q[7]));
+        };
+        Split3 sq = unit(0);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int j = u >> 1, s2 = u & 1;
+            __builtin_amdgcn_sched_barrier(0);
+            bf16x8 pf[NI];
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                uint32_t ta = (s2 == 0 ? cur.m[i] << 4 : cur.m[i] >> 4) & 0xFF0u;
+                asm volatile("" : "+v"(ta));
+                pf[i] = *reinterpret_cast<const bf16x8*>(tab + ta);
+            }
+            Split3 nx = sq;
+            if (u < 3) nx = unit(u + 1);
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                acc[0][i][j] = mfma16(pf[i], sq.l, acc[0][i][j]);
+                acc[0][i][j] = mfma16(pf[i], sq.m, acc[0][i][j]);
+                acc[0][i][j] = mfma16(pf[i], sq.h, acc[0][i][j]);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x100, NI, 0);  // the NI table reads
+#pragma unroll
+            for (int k = 0; k < 3 * NI; ++k) {
+                __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);  // 1 MFMA
+                __builtin_amdgcn_sched_group_barrier(0x2, 5, 0);  // 5 VALU
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            sq = nx;
+        }
+    };
+#endif
     // whole tiles: dy rows as float4 (ld_dy = d_out and 16-B aligned, else element loads), one
     // tile ahead like the x rows and mask words
     const bool gvec = ld_dy == D && ((uintptr_t)dyp & 15) == 0;
@@ -359,7 +568,11 @@ NAV_DEV void wgrad_rows_fact(const WgradArgs& a, int y, int n0, int k0, int64_t 
                 if (GPF) load_g(rt + 32, gn);
             }
             if (!GPF) load_g(rt, gc);
+#ifdef NAV_WGRAD_SGB
+            tile_sgb(cur, gc);
+#else
             tile(cur, gc);
+#endif
             cur = nxt;
             if (GPF) {
 #pragma unroll
@@ -484,11 +697,23 @@ NAV_DEV void wave_rows(const WgradArgs& a, int split, int wv, int64_t& r_lo, int
 
 template <int NI, int D>
 NAV_DEV void wgrad_tile_fact(const WgradArgs& a, const TileJob& t, float* smem) {
+    // the bits -> A fragment table at LDS offset 0: entry b, dword d holds bf16 2.0 in its low
+    // half when bit 2d of b is set and in its high half when bit 2d + 1 is
+    uint4* tab = reinterpret_cast<uint4*>(smem);
+    if (threadIdx.x < 256) {
+        const uint32_t b = threadIdx.x;
+        uint32_t w[4];
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+            w[d] = ((b >> (2 * d)) & 1u ? 0x4000u : 0u) | ((b >> (2 * d + 1)) & 1u ? 0x40000000u : 0u);
+        tab[b] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    __syncthreads();
     int64_t r_lo, r_hi;
     wave_rows(a, t.split, wave_id(), r_lo, r_hi);
     f32x16 out[NI][2];
-    wgrad_rows_fact<NI, D>(a, t.y, t.n0, t.k0, r_lo, r_hi, out);
-    wgrad_reduce_write<NI>(a, t.y, t.split, t.L, t.n0, t.k0, out, smem);
+    wgrad_rows_fact<NI, D>(a, t.y, t.n0, t.k0, r_lo, r_hi, reinterpret_cast<const char*>(tab), out);
+    wgrad_reduce_write<NI>(a, t.y, t.split, t.L, t.n0, t.k0, out, smem + 1024);
 }
 
 // The tile job's partial over its split's rows, written as one slab tile (8 waves' partials
@@ -509,7 +734,9 @@ NAV_DEV void wgrad_tile(const WgradArgs& a, const TileJob& t, float* smem) {
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
     const bool pr = L == nh - 1, qr = L == 1;
-    if (pr && qr) wgrad_rows<true, true>(a, y, L, n0, k0, r_lo, r_hi, stage, acc);
+    const bool full = n0 + WG_TILE <= a.net[y].hp && k0 + WG_TILE <= a.net[y].hp;
+    if (pr && qr && full) wgrad_rows_mfma(a, y, n0, k0, r_lo, r_hi, acc);
+    else if (pr && qr) wgrad_rows<true, true>(a, y, L, n0, k0, r_lo, r_hi, stage, acc);
     else if (pr) wgrad_rows<true, false>(a, y, L, n0, k0, r_lo, r_hi, stage, acc);
     else if (qr) wgrad_rows<false, true>(a, y, L, n0, k0, r_lo, r_hi, stage, acc);
     else wgrad_rows<false, false>(a, y, L, n0, k0, r_lo, r_hi, stage, acc);
@@ -948,7 +1175,10 @@ static int wgrad_args(const nav_mlp* nets, int32_t n_nets, int64_t M, const floa
     a.tn = wgrad_tile_n(a.net[0].d_out, hp, nh);
     a.TN = (hp + a.tn - 1) / a.tn;
     a.n_hid = (nh - 1) * a.TN * a.TT;
-    a.fact = wgrad_fact_ok(hp, nh);
+    // the factored path for the critics (d_out = 1); the actor's d_out = 2 would need two
+    // accumulator sets and two splits per element (measured slower than wgrad_rows_mfma: 40 vs
+    // 34 us at 2x256, profiles/r04c)
+    a.fact = wgrad_fact_ok(hp, nh) && a.net[0].d_out == 1;
     // 64-row aligned splits and per-wave ranges: a chunk's mask row tiles start on a tile boundary
     a.per_split = ((M + splits - 1) / splits + WG_CHUNK - 1) / WG_CHUNK * WG_CHUNK;
     a.per_wave = ((a.per_split + WG_WAVES - 1) / WG_WAVES + WG_CHUNK - 1) / WG_CHUNK * WG_CHUNK;
@@ -969,8 +1199,7 @@ int nav_mlp_wgrad(const nav_mlp* nets, int32_t n_nets, int64_t M, const float* i
     const int64_t blocks = (int64_t)n_nets * a.n_hid * splits;
     const size_t lds = wgrad_lds_bytes();
     void (*k)(WgradArgs) = !a.fact ? k_wgrad
-                           : a.tn == 128 ? k_wgrad_fact<4, 1>
-                           : a.net[0].d_out == 1 ? k_wgrad_fact<2, 1> : k_wgrad_fact<2, 2>;
+                           : a.tn == 128 ? k_wgrad_fact<4, 1> : k_wgrad_fact<2, 1>;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(WG_THREADS), lds, S(stream), a);

@@ -14,7 +14,9 @@ FL="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unus
 objs="$B/env_kernels.o $B/learner_kernels.o $B/mlp_kernels.o"
 for n in 1 2 3 4 5 6 7 8; do objs="$objs $B/mlp_nt$n.o"; done
 case $unit in
-  learner) /opt/rocm/bin/hipcc $FL -mllvm -amdgpu-sched-strategy=max-ilp $flags -c $P/csrc/learner_kernels.hip -o abl/$name.o
+  learner) sched="-mllvm -amdgpu-sched-strategy=max-ilp"
+           [ -n "${NOSCHED:-}" ] && sched=""  # NOSCHED=1: the default machine scheduler
+           /opt/rocm/bin/hipcc $FL $sched $flags -c $P/csrc/learner_kernels.hip -o abl/$name.o
            objs=${objs/$B\/learner_kernels.o/abl\/$name.o} ;;
   env) /opt/rocm/bin/hipcc $FL $flags -c $P/csrc/env_kernels.hip -o abl/$name.o
        objs=${objs/$B\/env_kernels.o/abl\/$name.o} ;;

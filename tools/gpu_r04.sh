@@ -10,6 +10,8 @@
 #   bench     the default bench line
 #   prof      rocprofv3 kernel trace + stats of a short bench
 #   pmc       FETCH_SIZE / WRITE_SIZE / SQ passes of a short bench (separate runs)
+#   wpmc      SQ counters and timing of tools/wgrad_bench.py for this tree's library and each
+#             abl/libnavenv_$v.so named in $WVARS (A/B variants built by tools/build_variant.sh)
 # usage: bash tools/gpu_r04.sh TAG step...
 set -u
 TAG=$1; shift
@@ -46,6 +48,13 @@ for step in "$@"; do
     pmc) run pmc_fetch 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/fetch" -o run -- python bench.py $PMCB &&
          run pmc_write 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/write" -o run -- python bench.py $PMCB &&
          run pmc_sq 150 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$O/sq" -o run -- python bench.py $PMCB ;;
+    wpmc) for v in "" $WVARS; do
+            tag=${v:-base}
+            if [ -n "$v" ]; then export NAV_LIB=$ROOT/abl/libnavenv_$v.so; else unset NAV_LIB; fi
+            run wpmc_$tag 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$O/wpmc_$tag" -o run -- python tools/wgrad_bench.py --reps 5
+            run wvar_$tag 120 python tools/wgrad_bench.py
+          done
+          unset NAV_LIB ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -50,7 +50,7 @@ def main():
     s = stream_handle()
     lb = lib()
     res = {}
-    sc, sa = (lb.nav_mlp_wgrad_splits(2, hp, L, B), lb.nav_mlp_wgrad_splits(1, hp, L, B))
+    sc, sa = (lb.nav_mlp_wgrad_splits(2, 1, hp, L, B), lb.nav_mlp_wgrad_splits(1, 2, hp, L, B))
     if args.splits:
         sc, sa = (int(v) for v in args.splits.split(","))
     hc = max(4, lb.nav_mlp_hidden_count(hp, L))
