@@ -353,22 +353,13 @@ NAV_DEV void wgrad_rows_mfma(const WgradArgs& a, int y, int n0, int k0, int64_t 
 //   dz_1[r][n] = e[r][n] sum_d g_d[r] Wo[d][n]        (robot.py:355-363 autograd, d < d_out)
 //   dW_1[n][k] = sum_r dz_1[r][n] h_0[r][k] = sum_d Wo[d][n] S_d[n][k],
 //   S_d[n][k]  = sum_r e[r][n] Q_d[r][k],   Q_d[r][k] = g_d[r] h_0[r][k].
-// The A operand of S_d is the ReLU bit itself, exact in bf16 (as 2.0: one bit of the pattern, so
-// a dword of two elements is a shift and an AND of the mask word; the 0.5 goes into Wo), and
+// The A operand of S_d is the ReLU bit itself, exact in bf16 (as 2.0, the 0.5 goes into Wo; 8
+// bits of a mask word become an A fragment by one 16-B read of a 256-entry LDS table), and
 // only the B operand Q_d is split — three bf16 planes, exactly, so the product carries f32
 // accuracy with 3 MFMAs per 16-deep k step and 32 x 32 tile instead of the 6 of a product with
 // both operands split, and nothing per element on the n side. That frees a wave to own NI = 4
 // column tiles of n (128 x 64) at D = 1 — the twin critics — for 128 accumulator registers.
 
-// bits b .. b+7 of a C-layout mask word (w2 = w | w << 15: bit b+1 sits 16 above bit b) as the 8
-// bf16 elements of an A fragment: 2.0 (0x4000) where the bit is set, else 0
-NAV_DEV bf16x8 bits_frag(uint32_t w2, int b) {
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    u32x4 r;
-#pragma unroll
-    for (int d = 0; d < 4; ++d) r[d] = (w2 << (14 - b - 2 * d)) & 0x40004000u;
-    return __builtin_bit_cast(bf16x8, r);
-}
 
 template <int NI, int D>
 NAV_DEV void wgrad_rows_fact(const WgradArgs& a, int y, int n0, int k0, int64_t r_lo,
@@ -451,19 +442,12 @@ NAV_DEV void wgrad_rows_fact(const WgradArgs& a, int y, int n0, int k0, int64_t 
                                              make_float4(q[4], q[5], q[6], q[7]));
 #pragma unroll
                     for (int i = 0; i < NI; ++i) {
-                        // formed right before its 3 MFMAs in every pass (2 VALU per dword): an
-                        // opaque copy of the mask word keeps the compiler from holding all the
-                        // fragments live across the passes
-#ifdef NAV_WGRAD_BITS_VALU
-                        uint32_t mw;
-                        asm volatile("v_mov_b32 %0, %1" : "=v"(mw) : "v"(cur.m[i]));
-                        const bf16x8 pi = bits_frag(mw | (mw << 15), 8 * s2);
-#else
-                        // byte s2 of the mask word as the 16-B entry's offset
+                        // the fragment of byte s2 of the mask word, read from the table right
+                        // before its 3 MFMAs (the opaque offset keeps the compiler from holding
+                        // all NI x 2 fragments live across the passes over j)
                         uint32_t ta = (s2 == 0 ? cur.m[i] << 4 : cur.m[i] >> 4) & 0xFF0u;
                         asm volatile("" : "+v"(ta));
                         const bf16x8 pi = *reinterpret_cast<const bf16x8*>(tab + ta);
-#endif
                         acc[d][i][j] = mfma16(pi, sq.l, acc[d][i][j]);
                         acc[d][i][j] = mfma16(pi, sq.m, acc[d][i][j]);
                         acc[d][i][j] = mfma16(pi, sq.h, acc[d][i][j]);
@@ -471,60 +455,6 @@ NAV_DEV void wgrad_rows_fact(const WgradArgs& a, int y, int n0, int k0, int64_t 
                 }
         }
     };
-#ifdef NAV_WGRAD_SGB
-    // the same products as units u = (j, s2) with the split of unit u + 1 interleaved into unit
-    // u's 12 MFMAs by scheduling-group barriers (5 VALU per MFMA gap; A/B variant)
-    auto tile_sgb = [&](const Raw& cur, const float (&gs)[2][D][8]) {
-        const float x0 = h < d_in ? cur.x0 : 0.f, x1 = 2 + h < d_in ? cur.x1 : 0.f;
-        f32x16 Z[2];
-        const f32x16 zero = {};
-#pragma unroll
-        for (int j = 0; j < 2; ++j) Z[j] = mfma(one, bob[j], zero);
-#pragma unroll
-        for (int j = 0; j < 2; ++j) Z[j] = mfma(x0, w0b[j][0], Z[j]);
-        if (x23) {
-#pragma unroll
-            for (int j = 0; j < 2; ++j) Z[j] = mfma(x1, w0b[j][1], Z[j]);
-        }
-        auto unit = [&](int u) {
-            const int j = u >> 1, s2 = u & 1;
-            float q[8];
-#pragma unroll
-            for (int t = 0; t < 8; ++t)
-                q[t] = __int_as_float(max(__float_as_int(Z[j][8 * s2 + t]), 0)) * gs[s2][0][t];
-            return split8(make_float4(q[0], q[1], q[2], q[3]), make_float4(q[4], q[5], q[6], q[7]));
-        };
-        Split3 sq = unit(0);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int j = u >> 1, s2 = u & 1;
-            __builtin_amdgcn_sched_barrier(0);
-            bf16x8 pf[NI];
-#pragma unroll
-            for (int i = 0; i < NI; ++i) {
-                uint32_t ta = (s2 == 0 ? cur.m[i] << 4 : cur.m[i] >> 4) & 0xFF0u;
-                asm volatile("" : "+v"(ta));
-                pf[i] = *reinterpret_cast<const bf16x8*>(tab + ta);
-            }
-            Split3 nx = sq;
-            if (u < 3) nx = unit(u + 1);
-#pragma unroll
-            for (int i = 0; i < NI; ++i) {
-                acc[0][i][j] = mfma16(pf[i], sq.l, acc[0][i][j]);
-                acc[0][i][j] = mfma16(pf[i], sq.m, acc[0][i][j]);
-                acc[0][i][j] = mfma16(pf[i], sq.h, acc[0][i][j]);
-            }
-            __builtin_amdgcn_sched_group_barrier(0x100, NI, 0);  // the NI table reads
-#pragma unroll
-            for (int k = 0; k < 3 * NI; ++k) {
-                __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);  // 1 MFMA
-                __builtin_amdgcn_sched_group_barrier(0x2, 5, 0);  // 5 VALU
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            sq = nx;
-        }
-    };
-#endif
     // whole tiles: dy rows as float4 (ld_dy = d_out and 16-B aligned, else element loads), one
     // tile ahead like the x rows and mask words
     const bool gvec = ld_dy == D && ((uintptr_t)dyp & 15) == 0;
@@ -568,11 +498,7 @@ NAV_DEV void wgrad_rows_fact(const WgradArgs& a, int y, int n0, int k0, int64_t 
                 if (GPF) load_g(rt + 32, gn);
             }
             if (!GPF) load_g(rt, gc);
-#ifdef NAV_WGRAD_SGB
-            tile_sgb(cur, gc);
-#else
             tile(cur, gc);
-#endif
             cur = nxt;
             if (GPF) {
 #pragma unroll
