@@ -10,6 +10,8 @@
 #   bench     the default bench line
 #   prof      rocprofv3 kernel trace + stats of a short bench
 #   pmc       FETCH_SIZE / WRITE_SIZE / SQ passes of a short bench (separate runs)
+#   vab       interleaved bench A/B (3 rounds, kernel times included): this tree's library vs
+#             each abl/libnavenv_$v.so named in $VARS
 #   wpmc      SQ counters and timing of tools/wgrad_bench.py for this tree's library and each
 #             abl/libnavenv_$v.so named in $WVARS (A/B variants built by tools/build_variant.sh)
 # usage: bash tools/gpu_r04.sh TAG step...
@@ -55,6 +57,14 @@ for step in "$@"; do
             run wvar_$tag 120 python tools/wgrad_bench.py
           done
           unset NAV_LIB ;;
+    vab) for r in 1 2 3; do
+           for v in "" $VARS; do
+             tag=${v:-base}
+             if [ -n "$v" ]; then export NAV_LIB=$ROOT/abl/libnavenv_$v.so; else unset NAV_LIB; fi
+             run vab_${tag}_$r 200 python bench.py $SHORT --steps 60 --warmup 5
+           done
+         done
+         unset NAV_LIB ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
