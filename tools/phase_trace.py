@@ -5,7 +5,8 @@ loaded through NAV_LIB. Runs the bench trainer for a few steps, then reads the s
 4 traced workgroups (blocks 0, 1, 200, 511) x 4 waves and prints each phase's duration in
 cycles of that counter, per wave, plus the per-phase mean over the 16 traced waves.
 
-NAV_LIB=abl/libnavenv_trace.so python tools/phase_trace.py
+NAV_LIB=abl/libnavenv_trace.so python tools/phase_trace.py [--batch B]
+(--batch 16448: 257 workgroups of 64 rows, so the traced ones run alone on their CU)
 """
 import ctypes as C
 import json
@@ -41,9 +42,13 @@ def mark_names():
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=32768)
+    args = ap.parse_args()
     from nav._lib import LIB_PATH
     from nav.trainer import VecTrainer
-    tr = VecTrainer(n_envs=65536, hidden=256, n_hidden=2, batch=32768, updates_per_step=2,
+    tr = VecTrainer(n_envs=65536, hidden=256, n_hidden=2, batch=args.batch, updates_per_step=2,
                     envs_per_group=1024)
     for _ in range(4):
         tr.step()
@@ -53,10 +58,11 @@ def main():
     rc = raw.nav_phase_trace_read(buf, 4 * 4 * 64)
     assert rc == 0, rc
     t = np.frombuffer(buf, dtype=np.uint64).reshape(4, 4, 64).astype(np.int64)
+    t = t[[wg for wg in range(4) if t[wg, 0, 0] != 0]]  # traced blocks past the grid: absent
     names = mark_names()
     marks = sorted(names)
     out = {"marks": {}, "total": {}}
-    for wg in range(4):
+    for wg in range(t.shape[0]):
         for w in range(4):
             out["total"][f"wg{wg}w{w}"] = int(t[wg, w, marks[-1]] - t[wg, w, 0])
     for a, b in zip(marks[:-1], marks[1:]):
