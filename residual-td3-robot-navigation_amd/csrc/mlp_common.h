@@ -194,6 +194,9 @@ __device__ unsigned long long g_phase_trace[4][kBlock / 64][64];
         if (tw_ >= 0 && (threadIdx.x & 63) == 0 && (k) >= 0 && (k) < 64)                        \
             g_phase_trace[tw_][threadIdx.x >> 6][(k)] = __builtin_readcyclecounter();          \
     } while (0)
+// marks that exist only in the trace build (no scheduling fence in the product build)
+#define NAV_TRACE_MARK(k) NAV_MARK(k)
+#define NAV_TICK_MK 52
 #elif NAV_PHASE_FENCE
 // The phase marks are scheduling fences: the scheduler may not move code across a phase boundary
 // (layer 0, the GEMM, the output layer, the epilogues). Without them it spreads one phase's
@@ -204,6 +207,12 @@ __device__ unsigned long long g_phase_trace[4][kBlock / 64][64];
 #define NAV_MARK(k) \
     do {            \
     } while (0)
+#endif
+#ifndef NAV_PHASE_TRACE
+#define NAV_TRACE_MARK(k) \
+    do {                  \
+    } while (0)
+#define NAV_TICK_MK -64
 #endif
 
 // Mask image row-tile count: independent of the workgroup height, so any RT reads what any RT

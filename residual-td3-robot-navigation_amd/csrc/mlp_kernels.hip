@@ -713,7 +713,8 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
 
     float* red = xin + TM * 4;  // [2][PARTS][TM]
     f32x16 top[RT][2];
-    fwd_net<NT, RT>(net, act, stage, xin, red, masks, n_rt, act_save, a.save_mask, row0, M, rt0, top);
+    fwd_net<NT, RT>(net, act, stage, xin, red, masks, n_rt, act_save, a.save_mask, row0, M, rt0, top,
+                    OUT_MODE == OUT_TICK ? NAV_TICK_MK : -64);
     const int rloc = tid % TM;
     const int j = tid / TM;
     const int64_t r = row0 + rloc;
@@ -755,6 +756,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
             if (a.action_out) a.action_out[r * 2 + j] = v;
         }
         __syncthreads();
+        NAV_TRACE_MARK(NAV_TICK_MK + 6);
         DemoPend pend{false, false, 0.0, make_double2(0.0, 0.0)};
         TickStats st{0.f, 0.f, 0.f, 0.f, 0.f};
         if (tid < TM && r < M) {
@@ -764,6 +766,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
                              : agent_tick<false>(a.p, a.env, a.field, r, av, a.rows, a.cap,
                                                  a.base, a.sout, false, pend);
         }
+        NAV_TRACE_MARK(NAV_TICK_MK + 7);
         if (a.demo.cand) {  // block-uniform: the demo pass of the block's envs, all threads
             // the LDS rows are done with (the actions live in xin)
             auto* scratch = reinterpret_cast<DemoScratch<TM, kBlock>*>(act);
@@ -772,8 +775,10 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
                                                     a.base, a.reward_out);
             if (pend.need) st.r = (float)rd;  // the final reward of a flagged env
         }
+        NAV_TRACE_MARK(NAV_TICK_MK + 8);
         if (tid < TM && a.sout.block_stats && row0 + (tid & ~63) < M)
             wave_stats(st, a.sout.block_stats, r);
+        NAV_TRACE_MARK(NAV_TICK_MK + 9);
         return;
     }
     if (r >= M || j >= d_out) return;

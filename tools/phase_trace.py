@@ -41,10 +41,19 @@ def mark_names():
     return n
 
 
+def tick_names():
+    # the fused act + tick launch (k_mlp_fwd OUT_TICK): fwd_net's marks from NAV_TICK_MK = 52
+    n = {52 + i: f"act fwd {s}" for i, s in enumerate(FWD)}
+    n.update({58: "action epilogue + barrier", 59: "agent tick (wave 0)", 60: "demo pass",
+              61: "block stats"})
+    return n
+
+
 def main():
     import argparse
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=32768)
+    ap.add_argument("--tick", action="store_true", help="the fused act + tick launch's marks")
     args = ap.parse_args()
     from nav._lib import LIB_PATH
     from nav.trainer import VecTrainer
@@ -59,12 +68,12 @@ def main():
     assert rc == 0, rc
     t = np.frombuffer(buf, dtype=np.uint64).reshape(4, 4, 64).astype(np.int64)
     t = t[[wg for wg in range(4) if t[wg, 0, 0] != 0]]  # traced blocks past the grid: absent
-    names = mark_names()
+    names = tick_names() if args.tick else mark_names()
     marks = sorted(names)
     out = {"marks": {}, "total": {}}
     for wg in range(t.shape[0]):
         for w in range(4):
-            out["total"][f"wg{wg}w{w}"] = int(t[wg, w, marks[-1]] - t[wg, w, 0])
+            out["total"][f"wg{wg}w{w}"] = int(t[wg, w, marks[-1]] - t[wg, w, marks[0]])
     for a, b in zip(marks[:-1], marks[1:]):
         d = t[:, :, b] - t[:, :, a]
         out["marks"][f"{b:02d} {names[b]}"] = {"mean": float(d.mean()), "min": int(d.min()),
