@@ -764,6 +764,65 @@ def test_split_gemm_f32_accuracy_vs_fp64(nav, d_in, d_out, hidden, nh, M):
         assert v <= (1e-5 if k.startswith("dW") else 2e-6), (k, v)
 
 
+@pytest.mark.parametrize("d_in,d_out,hidden", [(4, 1, 256), (4, 1, 192), (2, 2, 256)])
+@pytest.mark.parametrize("M,splits", [(1, 1), (31, 3), (33, 1), (100, 40), (2049, 7)])
+@pytest.mark.parametrize("dy_layout", ["packed", "misaligned", "strided"])
+def test_weight_grads_2layer_edge_cases(nav, d_in, d_out, hidden, M, splits, dy_layout):
+    """nav_mlp_wgrad of a 2-hidden-layer net (the factored path for d_out = 1: 128- or 64-high n
+    tiles; the MFMA-operand path for d_out = 2) on ragged row counts (a single row, one partial
+    32-row tile, a tile plus one row), more splits than rows, and dy rows that are packed,
+    misaligned (not 16-B aligned: the element-load path) or strided (ld_dy = d_out + 1): the sum
+    of the slabs against fp64 dW_1 = dz_1^T h_0 with the forward's own ReLU bits, within 1e-5 of
+    its scale, and the padded entries exactly 0."""
+    from nav._lib import descs, lib, parr, ptr, stream_handle
+    from nav.mlp import forward
+    nh = 2
+    net, layers = make_net(d_in, d_out, hidden, nh, 40 + M)
+    hp = net.hp
+    g = torch.Generator().manual_seed(3000 + M)
+    x = (torch.randn(M, d_in, generator=g) * 20).contiguous()
+    dy = torch.randn(M, d_out, generator=g) / max(M, 1)
+    xd = x.to(DEV)
+    out = torch.zeros(M, d_out, device=DEV)
+    acts = torch.zeros(nh, M, hp, device=DEV)
+    masks = net.mask_buffer(M)
+    forward([net], xd, d_in, 0, [out], d_out, 0, M, acts=[acts], masks=[masks])
+    if dy_layout == "packed":
+        ld, dyd = d_out, dy.to(DEV).contiguous()
+        dyp = ptr(dyd)
+    elif dy_layout == "misaligned":
+        ld = d_out
+        buf = torch.zeros(M * d_out + 1, device=DEV)
+        buf[1:] = dy.reshape(-1).to(DEV)
+        dyd, dyp = buf, buf.data_ptr() + 4
+    else:
+        ld = d_out + 1
+        buf = torch.zeros(M, ld, device=DEV)
+        buf[:, :d_out] = dy.to(DEV)
+        dyd, dyp = buf, ptr(buf)
+    L = lib()
+    hc = max(4, L.nav_mlp_hidden_count(hp, nh))
+    hs = torch.full((splits, hc), float("nan"), device=DEV)
+    dz = torch.zeros(nh, M, hp, device=DEV)
+    rc = L.nav_mlp_wgrad(descs(net), 1, M, ptr(xd), d_in, 0, parr(acts), parr(dz),
+                         (C.c_void_p * 1)(dyp), ld, parr(masks), parr(hs), splits,
+                         stream_handle())
+    assert rc == 0
+    torch.cuda.synchronize()
+    del dyd
+    got = hs.cpu().double().sum(0)[:hp * hp].view(hp, hp)
+    assert torch.isfinite(got).all()
+    bits = relu_bits(masks, nh, hp, hidden, M)
+    _, zs = _f64_forward(layers, x)
+    h0 = torch.relu(zs[0])
+    dz1 = (dy.double() @ layers[nh][0].double()) * bits[1].double()
+    ref = dz1.t() @ h0
+    scale = ref.abs().max().item() + 1e-30
+    err = (got[:hidden, :hidden] - ref).abs().max().item()
+    assert err <= 1e-5 * scale, (err, scale)
+    assert (got[hidden:, :] == 0).all() and (got[:, hidden:] == 0).all()
+
+
 def _split_planes(packed, off, hp):
     """The three bf16 planes of one split image (split_entry layout [3][hp/16][2][hp][8]) as
     fp32 [3][K][N]."""
