@@ -80,10 +80,21 @@ def main():
             lb.nav_grad_reduce_multi(descs(*nets), n, parr(*slabs), splits, parr(*es), nblk,
                                      parr(*grads), s)
         us_r = timeit(red, args.reps)
+        ms = [torch.zeros(x.count, device=dev) for x in nets]
+        vs = [torch.zeros(x.count, device=dev) for x in nets]
+        import ctypes as C
+        ssz = (C.c_float * n)(*([1e-9] * n))
+        bc2 = (C.c_float * n)(*([1.0] * n))
+
+        def red_adam():  # the product's reduce fused with Adam (tiny steps: the weights barely move)
+            lb.nav_grad_reduce_adam(descs(*nets), n, parr(*slabs), splits, parr(*es), nblk,
+                                    parr(*grads), parr(*ms), parr(*vs), 0.9, 0.999, 1e-8, ssz,
+                                    bc2, s)
+        us_ra = timeit(red_adam, args.reps)
         res[name] = {"splits": splits, "wgrad_us": round(us, 2),
                      "TFs": round(n * flops / us / 1e6, 1),
                      "frac_157": round(n * flops / us / 1e6 / 157.3, 3),
-                     "reduce_us": round(us_r, 2),
+                     "reduce_us": round(us_r, 2), "reduce_adam_us": round(us_ra, 2),
                      "slab_MB": round(n * splits * hc * 4 / 1e6, 2)}
     print(json.dumps(res), flush=True)
 
