@@ -709,6 +709,26 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
         }
         *reinterpret_cast<float4*>(xin + tid * 4) = make_float4(x[0], x[1], x[2], x[3]);
     }
+    // OUT_TICK: the row's tick inputs that do not depend on its action (state, goal, meta, the
+    // plan counters, the stuck ring, the field value), its noise scale and exploration noise are
+    // loaded / drawn now, so their latency hides under the network pass
+    TickIn tin{};
+    double nsc = 0.0;
+    double2 zz = make_double2(0.0, 0.0);
+    if constexpr (OUT_MODE == OUT_TICK) {
+        const int64_t r = row0 + tid;
+        if (tid < TM && r < M) {
+            tin = tick_load(a.env, a.field, r);
+            if (a.act_mode == 0) {
+                nsc = a.noise_scale[r];
+                if (a.noise_z)
+                    zz = make_double2(a.noise_z[r * 2], a.noise_z[r * 2 + 1]);
+                else
+                    zz = gauss_pair(philox(0u, (uint32_t)r, NAV_TAG_NOISE, a.step, a.p.seed_lo,
+                                           a.p.seed_hi));
+            }
+        }
+    }
     __syncthreads();
 
     float* red = xin + TM * 4;  // [2][PARTS][TM]
@@ -735,36 +755,27 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
     if constexpr (OUT_MODE == OUT_TICK) {
         // robot.py:556-567 as OUT_ACT, the action parked in LDS (the input rows are done with),
         // then the tick of env row0 + t by thread t < TM: nav_agent_step's device code
-        double* act_lds = reinterpret_cast<double*>(xin);  // [TM][2]
-        if (tid < 2 * TM && r < M) {
-            const float y = out_y<RT>(net, red, rloc, j);
-            const double s = a.state[r * 2 + j], g = a.goal[r * 2 + j];
-            double c = (s - g) + (double)y;
-            if (a.act_mode == 0) {
-                double z;
-                if (a.noise_z) {
-                    z = a.noise_z[r * 2 + j];
-                } else {
-                    const double2 zz = gauss_pair(philox(0u, (uint32_t)r, NAV_TAG_NOISE, a.step,
-                                                         a.p.seed_lo, a.p.seed_hi));
-                    z = j == 0 ? zz.x : zz.y;
-                }
-                c = c + (a.noise_scale[r] * a.max_action_d) * z;
-            }
-            const double v = clipd(c, -a.max_action_d, a.max_action_d);
-            act_lds[rloc * 2 + j] = v;
-            if (a.action_out) a.action_out[r * 2 + j] = v;
-        }
-        __syncthreads();
-        NAV_TRACE_MARK(NAV_TICK_MK + 6);
+        // the row's thread forms both action components (the same expressions per component as
+        // OUT_ACT) and runs its env's tick; no LDS round trip, no barrier in between
         DemoPend pend{false, false, 0.0, make_double2(0.0, 0.0)};
         TickStats st{0.f, 0.f, 0.f, 0.f, 0.f};
+        NAV_TRACE_MARK(NAV_TICK_MK + 6);
         if (tid < TM && r < M) {
-            const double2 av = make_double2(act_lds[tid * 2], act_lds[tid * 2 + 1]);
-            st = a.demo.cand ? agent_tick<true>(a.p, a.env, a.field, r, av, a.rows, a.cap, a.base,
-                                                a.sout, true, pend)
-                             : agent_tick<false>(a.p, a.env, a.field, r, av, a.rows, a.cap,
-                                                 a.base, a.sout, false, pend);
+            double v[2];
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj) {
+                const float y = out_y<RT>(net, red, tid, jj);
+                const double sj = jj == 0 ? tin.s.x : tin.s.y, gj = jj == 0 ? tin.g.x : tin.g.y;
+                double c = (sj - gj) + (double)y;
+                if (a.act_mode == 0) c = c + (nsc * a.max_action_d) * (jj == 0 ? zz.x : zz.y);
+                v[jj] = clipd(c, -a.max_action_d, a.max_action_d);
+                if (a.action_out) a.action_out[r * 2 + jj] = v[jj];
+            }
+            const double2 av = make_double2(v[0], v[1]);
+            st = a.demo.cand ? agent_tick_in<true>(a.p, a.env, r, tin, av, a.rows, a.cap, a.base,
+                                                   a.sout, true, pend)
+                             : agent_tick_in<false>(a.p, a.env, r, tin, av, a.rows, a.cap,
+                                                    a.base, a.sout, false, pend);
         }
         NAV_TRACE_MARK(NAV_TICK_MK + 7);
         if (a.demo.cand) {  // block-uniform: the demo pass of the block's envs, all threads

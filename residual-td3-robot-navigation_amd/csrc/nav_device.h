@@ -56,9 +56,16 @@ NAV_DEV int cell_of(double v) {
 // (atan2(a1, a0)) = (a0, a1), that is speed * R(rot) a: the same f64 displacement up to a few ulp
 // of |a| <= 5*sqrt(2) (< 1e-14 absolute, tests hold 1e-11), with one sincos of the small f32 angle
 // instead of atan2 + sqrt + sincos of the sum. a = 0, NaN and the +-5 clip behave identically.
+// the field value of state s (the cell table lookup of dynamics, separable so it can be issued early)
+NAV_DEV float2 field_at(const float2* __restrict__ field, double2 s) {
+    return field[cell_of(s.x) * 100 + cell_of(s.y)];
+}
+NAV_DEV double2 dynamics_f(float2 f, double2 s, double2 a);
 NAV_DEV double2 dynamics(const float2* __restrict__ field, double2 s, double2 a) {
+    return dynamics_f(field_at(field, s), s, a);
+}
+NAV_DEV double2 dynamics_f(float2 f, double2 s, double2 a) {
     const double a0 = clipd(a.x, -5.0, 5.0), a1 = clipd(a.y, -5.0, 5.0);
-    const float2 f = field[cell_of(s.x) * 100 + cell_of(s.y)];
     // NEP 50: float32 field value * 2 * pi is a float32 product chain
     const float rot = (f.y * 2.0f) * 3.14159274101257324f;
     double sr, cr;

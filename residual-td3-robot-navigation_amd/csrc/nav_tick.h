@@ -43,11 +43,56 @@ struct TransOut {
 // reference adds the demo term only when demonstration_states is non-empty (robot.py:749-751);
 // with demo_flag set and no demo set the reward is the goal term alone and the stuck penalty is
 // taken here.
+// The env's tick inputs that do not depend on its action, loadable ahead of it (the fused act +
+// tick launch issues them before its GEMM): state, goal, meta, plan / path counters, the stuck
+// ring and the field value at the state.
+struct TickIn {
+    double2 s, g;
+    uint32_t meta;
+    int32_t plan, path;
+    double2 hist[NAV_HIST];
+    float2 f;
+};
+NAV_DEV TickIn tick_load(const nav_env_soa& env, const float2* __restrict__ field, int64_t e) {
+    TickIn in;
+    in.s = reinterpret_cast<const double2*>(env.state)[e];
+    in.g = reinterpret_cast<const double2*>(env.goal)[e];
+    in.meta = env.meta[e];
+    in.plan = env.plan_index[e];
+    in.path = env.path_length[e];
+    const double2* hist = reinterpret_cast<const double2*>(env.hist);
+#pragma unroll
+    for (int k = 0; k < NAV_HIST; ++k) in.hist[k] = hist[(int64_t)k * env.n + e];
+    in.f = field_at(field, in.s);
+    return in;
+}
+
+NAV_DEV TransOut transition_in(const nav_params& p, const nav_env_soa& env, int64_t e,
+                               const TickIn& in, double2 a, double2 ns, bool demo_pending);
 NAV_DEV TransOut transition(const nav_params& p, const nav_env_soa& env, int64_t e, double2 s,
                             double2 a, double2 ns, uint32_t meta, int32_t plan, int32_t path,
                             bool demo_pending) {
+    TickIn in;
+    in.s = s;
+    in.g = reinterpret_cast<const double2*>(env.goal)[e];
+    in.meta = meta;
+    in.plan = plan;
+    in.path = path;
+    const double2* hist = reinterpret_cast<const double2*>(env.hist);
+    // the ring is read only when it is full (cnt >= NAV_HIST)
+    if ((int)((meta >> 8) & 7u) >= NAV_HIST) {
+#pragma unroll
+        for (int k = 0; k < NAV_HIST; ++k) in.hist[k] = hist[(int64_t)k * env.n + e];
+    }
+    return transition_in(p, env, e, in, a, ns, demo_pending);
+}
+NAV_DEV TransOut transition_in(const nav_params& p, const nav_env_soa& env, int64_t e,
+                               const TickIn& in, double2 a, double2 ns, bool demo_pending) {
+    (void)a;
     double2* hist = reinterpret_cast<double2*>(env.hist);
-    const double2 g = reinterpret_cast<const double2*>(env.goal)[e];
+    const double2 s = in.s, g = in.g;
+    const uint32_t meta = in.meta;
+    const int32_t plan = in.plan, path = in.path;
     TransOut t;
     bool goal_reached = (meta & M_GOAL) != 0;
     t.gt = -norm2(ns.x - g.x, ns.y - g.y);
@@ -66,7 +111,7 @@ NAV_DEV TransOut transition(const nav_params& p, const nav_env_soa& env, int64_t
         bool all = true;
 #pragma unroll
         for (int k = 0; k < NAV_HIST; ++k) {
-            const double2 h = hist[(int64_t)k * env.n + e];
+            const double2 h = in.hist[k];
             const double d = norm2(s.x - h.x, s.y - h.y);
             all = all && (d < p.stuck_threshold);
         }
@@ -193,20 +238,33 @@ struct TickStats {
 };
 
 template <bool DEMO>
+NAV_DEV TickStats agent_tick_in(const nav_params& p, const nav_env_soa& env, int64_t e,
+                                const TickIn& in, double2 a, float4* __restrict__ rows,
+                                int64_t cap, int64_t base, const nav_step_out& out,
+                                bool demo_pending, DemoPend& pend);
+template <bool DEMO>
 NAV_DEV TickStats agent_tick(const nav_params& p, const nav_env_soa& env,
                              const float2* __restrict__ field, int64_t e, double2 a,
                              float4* __restrict__ rows, int64_t cap, int64_t base,
                              const nav_step_out& out, bool demo_pending, DemoPend& pend) {
+    return agent_tick_in<DEMO>(p, env, e, tick_load(env, field, e), a, rows, cap, base, out,
+                               demo_pending, pend);
+}
+// the tick from its preloaded inputs (tick_load) and the action
+template <bool DEMO>
+NAV_DEV TickStats agent_tick_in(const nav_params& p, const nav_env_soa& env, int64_t e,
+                                const TickIn& in, double2 a, float4* __restrict__ rows,
+                                int64_t cap, int64_t base, const nav_step_out& out,
+                                bool demo_pending, DemoPend& pend) {
     double2* state = reinterpret_cast<double2*>(env.state);
-    const double2 s = state[e];
-    const uint32_t meta = env.meta[e];
-    int32_t plan = env.plan_index[e];
-    const int32_t path = env.path_length[e];
+    const double2 s = in.s;
+    int32_t plan = in.plan;
+    const int32_t path = in.path;
 
     // environment.py:122-127
-    double2 ns = dynamics(field, s, a);
+    double2 ns = dynamics_f(in.f, s, a);
     if (!in_world(ns)) ns = s;
-    TransOut t = transition(p, env, e, s, a, ns, meta, plan, path, DEMO || demo_pending);
+    TransOut t = transition_in(p, env, e, in, a, ns, DEMO || demo_pending);
     if (DEMO) {
         pend.need = t.demo_term;
         pend.stuck = t.stuck;

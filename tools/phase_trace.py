@@ -44,7 +44,7 @@ def mark_names():
 def tick_names():
     # the fused act + tick launch (k_mlp_fwd OUT_TICK): fwd_net's marks from NAV_TICK_MK = 52
     n = {52 + i: f"act fwd {s}" for i, s in enumerate(FWD)}
-    n.update({58: "action epilogue + barrier", 59: "agent tick (wave 0)", 60: "demo pass",
+    n.update({58: "tick preamble", 59: "action epilogue + agent tick (wave 0)", 60: "demo pass",
               61: "block stats"})
     return n
 
