@@ -1193,8 +1193,13 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
     __bf16* stage = reinterpret_cast<__bf16*>(dys + TM * 4);  // gemm_cols' split stage
     NAV_MARK(0);
     const L0Pre l0_at = load_l0<NT>(a.actor_t);  // in flight under the sampling
+    // the sampled replay row of thread tid < TM: its gather is issued first, so it is in flight
+    // while the smoothing noise below is formed
+    float4 lo = make_float4(0.f, 0.f, 0.f, 0.f), hi = lo;
+    if (tid < TM && row0 + tid < B)
+        sample_row(a.rows, a.rsize, a.idx, a.seed_lo, a.seed_hi, a.sample_ctr, row0 + tid, lo, hi);
     // target policy smoothing noise of (row, output) tid % TM, tid / TM: clamp(policy_noise * eps,
-    // +-noise_clip), formed while the sampled rows are in flight
+    // +-noise_clip)
     float tnz = 0.f;
     if (tid < 2 * TM && row0 + tid % TM < B) {
         const int64_t r = row0 + tid % TM;
@@ -1211,14 +1216,10 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
     }
     if (tid < TM) {
         const int64_t b = row0 + tid;
-        float4 lo = make_float4(0.f, 0.f, 0.f, 0.f), hi = lo;
-        if (b < B) {
-            sample_row(a.rows, a.rsize, a.idx, a.seed_lo, a.seed_hi, a.sample_ctr, b, lo, hi);
-            if (blockIdx.y == 0) {  // split twins: one writer per batch row
-                float4* dst = reinterpret_cast<float4*>(a.batch) + 2 * b;
-                dst[0] = lo;
-                dst[1] = hi;
-            }
+        if (b < B && blockIdx.y == 0) {  // split twins: one writer per batch row
+            float4* dst = reinterpret_cast<float4*>(a.batch) + 2 * b;
+            dst[0] = lo;
+            dst[1] = hi;
         }
         *reinterpret_cast<float4*>(brow + tid * 8) = lo;
         *reinterpret_cast<float4*>(brow + tid * 8 + 4) = hi;
