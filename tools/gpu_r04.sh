@@ -12,8 +12,8 @@
 #   pmc       FETCH_SIZE / WRITE_SIZE / SQ passes of a short bench (separate runs)
 #   vab       interleaved bench A/B (3 rounds, kernel times included): this tree's library vs
 #             each abl/libnavenv_$v.so named in $VARS
-#   phase     critic_rows phase trace (abl/libnavenv_trace.so) at batch 32768 (two workgroups
-#             per CU) and 16448 (one)
+#   phase     critic_rows phase trace (abl/libnavenv_$v.so for each $v in $PVARS, default
+#             trace) at batch 32768 (two workgroups per CU) and 16448 (one), and act_tick's
 #   wpmc      SQ counters and timing of tools/wgrad_bench.py for this tree's library and each
 #             abl/libnavenv_$v.so named in $WVARS (A/B variants built by tools/build_variant.sh)
 # usage: bash tools/gpu_r04.sh TAG step...
@@ -67,10 +67,12 @@ for step in "$@"; do
            done
          done
          unset NAV_LIB ;;
-    phase) export NAV_LIB=$ROOT/abl/libnavenv_trace.so
-           run phase_32768 200 python tools/phase_trace.py --batch 32768
-           run phase_16448 200 python tools/phase_trace.py --batch 16448
-           run phase_tick 200 python tools/phase_trace.py --tick
+    phase) for v in ${PVARS:-trace}; do
+             export NAV_LIB=$ROOT/abl/libnavenv_$v.so
+             run phase_${v}_32768 200 python tools/phase_trace.py --batch 32768
+             run phase_${v}_16448 200 python tools/phase_trace.py --batch 16448
+             run phase_${v}_tick 200 python tools/phase_trace.py --tick
+           done
            unset NAV_LIB ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
