@@ -1,7 +1,7 @@
 #!/bin/bash
 # Build an A/B variant of libnavenv.so with extra -D flags on one translation unit (tuning only):
 #   tools/build_variant.sh NAME learner|env|mlpN "-DFOO=1 ..."  (mlpN: the row kernels of hidden
-#   width 32*N; mlp8 = 256)
+#   width 32*N; mlp8 = 256; mlp0 = the row kernels' C-ABI object)
 # -> abl/libnavenv_NAME.so (load it with NAV_LIB=abl/libnavenv_NAME.so)
 set -eu
 cd "$(dirname "$0")/.."
@@ -20,6 +20,8 @@ case $unit in
            objs=${objs/$B\/learner_kernels.o/abl\/$name.o} ;;
   env) /opt/rocm/bin/hipcc $FL $flags -c $P/csrc/env_kernels.hip -o abl/$name.o
        objs=${objs/$B\/env_kernels.o/abl\/$name.o} ;;
+  mlp0) /opt/rocm/bin/hipcc $FL -mllvm -amdgpu-mfma-vgpr-form=1 -mllvm -amdgpu-sched-strategy=max-ilp $flags -DNAV_MLP_PART=0 -c $P/csrc/mlp_kernels.hip -o abl/$name.o
+        objs=${objs/$B\/mlp_kernels.o/abl\/$name.o} ;;
   mlp[1-8]) n=${unit#mlp}
         /opt/rocm/bin/hipcc $FL -mllvm -amdgpu-mfma-vgpr-form=1 -mllvm -amdgpu-sched-strategy=max-ilp $flags -DNAV_MLP_PART=$n -c $P/csrc/mlp_kernels.hip -o abl/$name.o
         objs=${objs/$B\/mlp_nt$n.o/abl\/$name.o} ;;
