@@ -186,11 +186,19 @@ constexpr int kWaves = kBlock / 64;
 // Phase timing probe (variant builds with -DNAV_PHASE_TRACE only; tools/phase_trace.py): s_memtime
 // at numbered marks, per wave of 4 traced workgroups of the row kernels.
 #ifdef NAV_PHASE_TRACE
-__device__ unsigned long long g_phase_trace[4][kBlock / 64][64];
+#ifdef NAV_TRACE_WIDE
+// NAV_TRACE_WIDE: blocks 0, 8, 16, ... (64 of them: one XCD's share of a 512-block grid)
+constexpr int kTraced = 64;
+#define NAV_TRACED_SLOT() (blockIdx.x % 8 == 0 && blockIdx.x / 8 < kTraced ? (int)blockIdx.x / 8 : -1)
+#else
+constexpr int kTraced = 4;
+#define NAV_TRACED_SLOT()                                                                      \
+    (blockIdx.x == 0 ? 0 : blockIdx.x == 1 ? 1 : blockIdx.x == 200 ? 2 : blockIdx.x == 511 ? 3 : -1)
+#endif
+__device__ unsigned long long g_phase_trace[kTraced][kBlock / 64][64];
 #define NAV_MARK(k)                                                                            \
     do {                                                                                       \
-        const int tw_ = blockIdx.x == 0 ? 0 : blockIdx.x == 1 ? 1 : blockIdx.x == 200 ? 2     \
-                      : blockIdx.x == 511 ? 3 : -1;                                            \
+        const int tw_ = NAV_TRACED_SLOT();                                                     \
         if (tw_ >= 0 && (threadIdx.x & 63) == 0 && (k) >= 0 && (k) < 64)                        \
             g_phase_trace[tw_][threadIdx.x >> 6][(k)] = __builtin_readcyclecounter();          \
     } while (0)

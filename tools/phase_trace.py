@@ -54,6 +54,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=32768)
     ap.add_argument("--tick", action="store_true", help="the fused act + tick launch's marks")
+    ap.add_argument("--wide", action="store_true",
+                    help="a -DNAV_TRACE_WIDE build: 64 blocks (0, 8, 16, ...), per block its start "
+                         "and end relative to the earliest traced start, plus the phase means")
     args = ap.parse_args()
     from nav._lib import LIB_PATH
     from nav.trainer import VecTrainer
@@ -63,14 +66,21 @@ def main():
         tr.step()
     torch.cuda.synchronize()
     raw = C.CDLL(LIB_PATH)
-    buf = (C.c_ulonglong * (4 * 4 * 64))()
-    rc = raw.nav_phase_trace_read(buf, 4 * 4 * 64)
+    nt = 64 if args.wide else 4
+    buf = (C.c_ulonglong * (nt * 4 * 64))()
+    rc = raw.nav_phase_trace_read(buf, nt * 4 * 64)
     assert rc == 0, rc
-    t = np.frombuffer(buf, dtype=np.uint64).reshape(4, 4, 64).astype(np.int64)
-    t = t[[wg for wg in range(4) if t[wg, 0, 0] != 0]]  # traced blocks past the grid: absent
+    t = np.frombuffer(buf, dtype=np.uint64).reshape(nt, 4, 64).astype(np.int64)
     names = tick_names() if args.tick else mark_names()
     marks = sorted(names)
+    live = [wg for wg in range(nt) if t[wg, 0, marks[0]] != 0]  # blocks past the grid: absent
+    t = t[live]
     out = {"marks": {}, "total": {}}
+    if args.wide:
+        t0 = t[:, :, marks[0]].min()
+        out["blocks"] = {str(8 * wg): {"start": int(t[i, :, marks[0]].min() - t0),
+                                       "end": int(t[i, :, marks[-1]].max() - t0)}
+                         for i, wg in enumerate(live)}
     for wg in range(t.shape[0]):
         for w in range(4):
             out["total"][f"wg{wg}w{w}"] = int(t[wg, w, marks[-1]] - t[wg, w, marks[0]])
