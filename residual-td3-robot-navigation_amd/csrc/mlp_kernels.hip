@@ -143,6 +143,13 @@ NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const bf16x8* __rest
     };
     produce(0);
     consume(0);
+    // Two workgroups share a CU at the bench shapes (blocks b and b + #CUs, dispatched together),
+    // and at equal priority the SIMD arbiter issues the older wave first: the second workgroup's
+    // GEMMs lag and it ends its last ~50 k cycles alone at the lone-workgroup MFMA rate (critic_rows:
+    // 247 k vs 297 k cycles). The upper half of the grid raises its wave priority inside its GEMMs,
+    // which balances the pair (270 k / 267 k; critic_rows 161.6 -> 153.5 us, profiles/r04y, r04z).
+    const bool favored = blockIdx.x >= (gridDim.x >> 1);
+    if (favored) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int q = 0; q < nq; ++q) {
         // step q + 1's production comes first in program order, so the scheduler can place it
@@ -161,6 +168,7 @@ NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const bf16x8* __rest
         }
         if (q + 1 < nq) consume(q + 1);
     }
+    if (favored) __builtin_amdgcn_s_setprio(0);
 }
 
 // the split B images of hidden layer L (1 .. n_hidden-1): forward (B[k][n] = W_L[n][k]) and

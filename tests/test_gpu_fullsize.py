@@ -116,7 +116,9 @@ def test_fused_demo_reward_is_bit_identical():
         assert torch.equal(net.params, b.td3.networks()[k].params), k
 
 
-@pytest.mark.parametrize("n,demos", [(8192, True), (5000, True), (1000, False)])
+# 40 000 envs: 625 row blocks, more than two workgroups per CU (512 on a 256-CU MI355X): a second
+# wave of workgroups, and the GEMM priority of the grid's upper half (gemm_cols) on both
+@pytest.mark.parametrize("n,demos", [(8192, True), (5000, True), (1000, False), (40000, True)])
 def test_fused_act_tick_is_bit_identical(n, demos):
     """nav_act_tick (actor forward + the env tick in one launch) vs nav_act followed by
     nav_agent_step_indexed: same actions, replay rows, env state, flags, next states, rewards,
