@@ -696,6 +696,8 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
     float* xin = smem + TM * SS;  // [TM][4]
     __bf16* stage = reinterpret_cast<__bf16*>(smem + lds_floats(hp, TM));
     const int d_in = net.d_in, d_out = net.d_out;
+    // layer 0's per-lane weights and bias: issued first, in flight under the input rows' loads
+    const L0Pre l0 = load_l0<NT>(net);
 
     // ---- input rows -> xin
     if (tid < TM) {
@@ -742,7 +744,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
     float* red = xin + TM * 4;  // [2][PARTS][TM]
     f32x16 top[RT][2];
     fwd_net<NT, RT>(net, act, stage, xin, red, masks, n_rt, act_save, a.save_mask, row0, M, rt0, top,
-                    OUT_MODE == OUT_TICK ? NAV_TICK_MK : -64);
+                    OUT_MODE == OUT_TICK ? NAV_TICK_MK : -64, &l0);
     const int rloc = tid % TM;
     const int j = tid / TM;
     const int64_t r = row0 + rloc;
