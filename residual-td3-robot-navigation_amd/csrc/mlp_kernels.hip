@@ -1208,12 +1208,15 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
     float4 lo = make_float4(0.f, 0.f, 0.f, 0.f), hi = lo;
     if (tid < TM && row0 + tid < B)
         sample_row(a.rows, a.rsize, a.idx, a.seed_lo, a.seed_hi, a.sample_ctr, row0 + tid, lo, hi);
-    // target policy smoothing noise of (row, output) tid % TM, tid / TM: clamp(policy_noise * eps,
-    // +-noise_clip)
+    // target policy smoothing noise of (row, output) (tid - TM) % TM, (tid - TM) / TM: clamp(
+    // policy_noise * eps, +-noise_clip) — threads past the sampling ones, so its f64 Box-Muller
+    // runs on other waves (other SIMDs) than the sampling's Philox draw and gather
+    static_assert(3 * TM <= kBlock, "sampling threads, then the noise's");
     float tnz = 0.f;
-    if (tid < 2 * TM && row0 + tid % TM < B) {
-        const int64_t r = row0 + tid % TM;
-        const int j = tid / TM;
+    const int tn = tid - TM;
+    if (tn >= 0 && tn < 2 * TM && row0 + tn % TM < B) {
+        const int64_t r = row0 + tn % TM;
+        const int j = tn / TM;
         float e;
         if (a.eps) {
             e = a.eps[r * 2 + j];
@@ -1243,8 +1246,8 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
     const L0Pre l0_ct1 = load_l0<NT>(a.critic_t[0]);
     fwd_net<NT, RT>(a.actor_t, act, stage, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0, top, 2,
                     &l0_at);
-    if (tid < 2 * TM) {
-        const int rloc = tid % TM, j = tid / TM;
+    if (tn >= 0 && tn < 2 * TM) {  // the noise's threads
+        const int rloc = tn % TM, j = tn / TM;
         const int64_t r = row0 + rloc;
         float v = 0.f;
         if (r < B) {
