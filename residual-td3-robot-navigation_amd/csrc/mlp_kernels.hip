@@ -935,6 +935,21 @@ NAV_DEV void edge_regs(const MlpDev& net, const f32x16 (&z)[RT][2], const float*
     }
 }
 
+// Masks the layer's dz registers in place (ReLU derivative bits), without the LDS rows.
+template <int NT, int RT>
+NAV_DEV void mask_regs(f32x16 (&acc)[RT][2], const uint32_t (&mbits)[RT][2]) {
+    const WaveCols<NT> wc(wave_id());
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const bool has = j == 0 ? wc.has0 : wc.has1;
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                acc[rt][j][i] = has && ((mbits[rt][j] >> i) & 1u) ? acc[rt][j][i] : 0.f;
+    }
+}
+
 // Masks the layer's dz registers in place (ReLU derivative bits) and stores them to the LDS rows.
 template <int NT, int RT>
 NAV_DEV void mask_and_store(f32x16 (&acc)[RT][2], const uint32_t (&mbits)[RT][2], float* act,
@@ -973,7 +988,7 @@ NAV_DEV void bwd_net(const MlpDev& net, float* act, __bf16* stage, const float* 
                      const uint16_t* masks, int64_t n_rt, float* es, const float* h_top,
                      float* dz, uint32_t save_mask, int64_t row0, int64_t M, int64_t rt0,
                      int mk = -64, const uint32_t* top_bits = nullptr,
-                     const WoCols* wo_in = nullptr) {
+                     const WoCols* wo_in = nullptr, bool dz0_rows = true) {
     constexpr int hp = NT * 32, SS = hp + 4, TM = RT * 32;
     NAV_MARK(mk);
     const int tid = threadIdx.x, lane = tid & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
@@ -1072,7 +1087,12 @@ NAV_DEV void bwd_net(const MlpDev& net, float* act, __bf16* stage, const float* 
         gemm_cols<NT, RT>(act, SS, img_bwd(net, L), stage, acc);
         NAV_MARK(mk + 3);
         __syncthreads();
-        mask_and_store<NT, RT>(acc, mbits, act, SS);
+        // layer 0's rows only when a reader follows (the caller's dx, the save copy); its edge
+        // partials come from the registers
+        if (L > 1 || dz0_rows || (save_mask & 1u))
+            mask_and_store<NT, RT>(acc, mbits, act, SS);
+        else
+            mask_regs<NT, RT>(acc, mbits);
         if (es) edge_regs<NT, RT>(net, acc, xin, L - 1, es);
         __syncthreads();
         NAV_MARK(mk + 4);
@@ -1298,7 +1318,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
                     make_float4(red[kWaves * TM + tid], 0.f, 0.f, 0.f);  // loss_epilogue's dq
             __syncthreads();
             bwd_net<NT, RT>(a.critic[q], act, stage, dys, xin, a.masks[q], n_rt, es, nullptr, a.dz[q],
-                            a.dz_save_mask, row0, B, rt0, 29 + 14 * q, top_bits, &wo);
+                            a.dz_save_mask, row0, B, rt0, 29 + 14 * q, top_bits, &wo, false);
             __syncthreads();  // the next forward's layer 0 overwrites the rows
         }
         NAV_MARK(35 + 14 * q);
@@ -1394,7 +1414,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_actor_rows(ActorRowsArgs a) {
         es[e_bo(a.actor) + tid] = sb;
     }
     bwd_net<NT, RT>(a.actor, act, stage, dys2, xin, a.masks_a, n_rt, es, nullptr, a.dz, a.dz_save_mask,
-                    row0, B, rt0);
+                    row0, B, rt0, -64, nullptr, nullptr, false);
 }
 
 
