@@ -1363,6 +1363,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_actor_rows(ActorRowsArgs a) {
     float* dys = red + red_floats(TM);  // [TM][4] critic dy
     float* dys2 = dys + TM * 4;      // [TM][4] actor dy = dL/da
     __bf16* stage = reinterpret_cast<__bf16*>(dys2 + TM * 4);  // gemm_cols' split stage
+    const L0Pre l0_a = load_l0<NT>(a.actor);  // in flight under the sampling
     if (tid < TM) {
         const int64_t b = row0 + tid;
         float4 lo = make_float4(0.f, 0.f, 0.f, 0.f), hi = lo;
@@ -1380,17 +1381,23 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_actor_rows(ActorRowsArgs a) {
     // the actor's top hidden layer stays in registers until dL/da is known (its dWo partials)
     f32x16 topa[RT][2];
     fwd_net<NT, RT>(a.actor, act, stage, xin, red, a.masks_a, n_rt, a.acts, a.save_mask, row0, B, rt0,
-                    topa);
+                    topa, -64, &l0_a);
+    const L0Pre l0_c = load_l0<NT>(a.critic);  // in flight under the action epilogue
     if (tid < 2 * TM) {
         const int rloc = tid % TM, j = tid / TM;
         xin[rloc * 4 + 2 + j] = row0 + rloc < B ? out_y<RT>(a.actor, red, rloc, j) : 0.f;
     }
     __syncthreads();
+    // the critic's top-layer ReLU bits and Wo columns go from its forward to its row backward in
+    // registers (as in critic_rows)
     f32x16 top[RT][2];
-    fwd_net<NT, RT>(a.critic, act, stage, xin, red, a.masks_c, n_rt, nullptr, 0u, row0, B, rt0, top);
+    uint32_t top_bits[RT * 2];
+    WoCols wo;
+    fwd_net<NT, RT>(a.critic, act, stage, xin, red, a.masks_c, n_rt, nullptr, 0u, row0, B, rt0, top,
+                    -64, &l0_c, top_bits, &wo);
     if (tid < TM && a.q && row0 + tid < B) a.q[row0 + tid] = out_y<RT>(a.critic, red, tid, 0);
     bwd_net<NT, RT>(a.critic, act, stage, dys, xin, a.masks_c, n_rt, nullptr, nullptr, nullptr, 0u, row0,
-                    B, rt0);
+                    B, rt0, -64, top_bits, &wo);
     if (tid < 2 * TM) {
         const int rloc = tid % TM, j = tid / TM;
         const int64_t r = row0 + rloc;
