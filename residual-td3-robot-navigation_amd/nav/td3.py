@@ -9,7 +9,6 @@ device ring, or taken from an injected index tensor (parity tests, the N=1 drop-
 import contextlib
 import ctypes as C
 import math
-import os
 
 import torch
 
@@ -50,7 +49,8 @@ class _Adam:
 
 class TD3:
     def __init__(self, cfg=None, device="cuda", seed=K.RANDOM_SEED, actor=None, critic1=None,
-                 critic2=None, grad_hook=None):
+                 critic2=None, grad_hook=None, row_backward=True, fuse_soft_update=True,
+                 wgrad_splits=None):
         self.cfg = cfg or K.TD3Config()
         c = self.cfg
         nc = c.net
@@ -81,12 +81,15 @@ class TD3:
                 raise ValueError("grad_hook must carry an int world_size >= 1: it SUM-all-reduces "
                                  "the gradient bucket and Adam divides by world_size")
             self.grad_div = float(ws)
-        # train_critic's row backward inside the critic_rows launch (NAV_CRITIC_ROW_BWD=0: its
-        # own launch; tuning / A/B only)
-        self.row_backward = os.environ.get("NAV_CRITIC_ROW_BWD", "1") != "0"
-        # a policy epoch's soft updates inside the actor's reduce + Adam launch
-        # (NAV_FUSE_SOFT_UPDATE=0: their own launch; A/B only)
-        self.fuse_soft_update = os.environ.get("NAV_FUSE_SOFT_UPDATE", "1") != "0"
+        # train_critic's row backward inside the critic_rows launch (False: its own launch; the
+        # results are bit-identical, A/B only)
+        self.row_backward = bool(row_backward)
+        # a policy epoch's soft updates inside the actor's reduce + Adam launch (False: their own
+        # launch; A/B only)
+        self.fuse_soft_update = bool(fuse_soft_update)
+        # row splits of the weight-gradient launches, (critic twins, actor); None = as many as
+        # fill the chip (nav_mlp_wgrad_splits; tuning only)
+        self.wgrad_splits = wgrad_splits
         # the twin online critics in separate workgroups: -1 = the library's choice by batch size
         # (1 / 0 force either form; the results are bit-identical)
         self.split_twins = -1
@@ -123,13 +126,11 @@ class TD3:
         self.eslab1, self.eslab2 = f(self.nblk, ec), f(self.nblk, ec)
         self.eslab_a = f(self.nblk, L.nav_mlp_edge_count(2, 2, hp, nh))
         # row splits of the weight-gradient launch (partial slabs): critic twins and actor
-        # separately, as many as fill the chip (NAV_WGRAD_SPLITS="critic,actor" overrides;
-        # tuning only)
+        # separately, as many as fill the chip (wgrad_splits overrides; tuning only)
         sc = L.nav_mlp_wgrad_splits(2, self.critic_network_1.d_out, hp, nh, B)
         sa = L.nav_mlp_wgrad_splits(1, self.actor_network.d_out, hp, nh, B)
-        env = os.environ.get("NAV_WGRAD_SPLITS")
-        if env:
-            sc, sa = (max(1, min(int(v), max(1, B // 32))) for v in env.split(","))
+        if self.wgrad_splits:
+            sc, sa = (max(1, min(int(v), max(1, B // 32))) for v in self.wgrad_splits)
         self.splits_c, self.splits_a = sc, sa
         hc = max(4, L.nav_mlp_hidden_count(hp, nh))
         self.hslab, self.hslab2 = f(max(sc, sa), hc), f(sc, hc)

@@ -10,7 +10,6 @@ on batches sampled from the device replay ring. The reference's schedule (100 ep
 here is updates_per_step * batch / n_envs sampled transitions per collected transition.
 """
 import ctypes as C
-import os
 
 import numpy as np
 import torch
@@ -27,7 +26,7 @@ from .vec_env import ReplayRing, VecEnv
 class VecTrainer:
     def __init__(self, n_envs=65536, hidden=256, n_hidden=2, batch=32768, updates_per_step=2,
                  replay_capacity=None, seed=K.RANDOM_SEED, envs_per_group=1024, demos=True,
-                 device="cuda", field=None, grad_hook=None):
+                 device="cuda", field=None, grad_hook=None, fuse_tick=True):
         self.n = int(n_envs)
         self.device = torch.device(device)
         self.seed = int(seed)
@@ -55,9 +54,9 @@ class VecTrainer:
         self.action = torch.zeros(self.n, 2, dtype=torch.float64, device=self.device)
         self.steps = 0
         self.updates_per_step = int(updates_per_step)
-        # act + tick fused into one launch (NAV_FUSE_TICK=0: the two launches; A/B and the
-        # fused-vs-unfused parity test)
-        self.fuse_tick = os.environ.get("NAV_FUSE_TICK", "1") != "0"
+        # act + tick fused into one launch (False: the two launches; A/B and the fused-vs-unfused
+        # parity test)
+        self.fuse_tick = bool(fuse_tick)
 
     # robot.py:541-569 for every env
     def act(self, training=True, stream=None):

@@ -4,7 +4,6 @@
 gfx950 kernels of libnavenv.so through the C-ABI. One env = one lane; n envs advance per launch.
 """
 import ctypes as C
-import os
 
 import torch
 
@@ -97,7 +96,7 @@ class ReplayRing:
 
 class VecEnv:
     def __init__(self, n, field, seed=K.RANDOM_SEED, envs_per_group=1, demo_flag=True,
-                 device="cuda", init=True, **param_overrides):
+                 device="cuda", init=True, fuse_demo=True, **param_overrides):
         require_gpu()
         self.n = int(n)
         self.device = torch.device(device)
@@ -130,9 +129,9 @@ class VecEnv:
         self.demo_xy = None
         self.demo_off = None
         self.demo_index = None
-        # demo reward fused into the tick launch (nav_agent_step_indexed); NAV_FUSE_DEMO=0 keeps
-        # the two launches (A/B and the fused-vs-unfused parity test)
-        self.fuse_demo = os.environ.get("NAV_FUSE_DEMO", "1") != "0"
+        # demo reward fused into the tick launch (nav_agent_step_indexed); False keeps the two
+        # launches (A/B and the fused-vs-unfused parity test)
+        self.fuse_demo = bool(fuse_demo)
         if init:
             self.init(demo_flag)
 

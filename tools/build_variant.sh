@@ -2,7 +2,7 @@
 # Build an A/B variant of libnavenv.so with extra -D flags on one translation unit (tuning only):
 #   tools/build_variant.sh NAME learner|env|mlpN "-DFOO=1 ..."  (mlpN: the row kernels of hidden
 #   width 32*N; mlp8 = 256; mlp0 = the row kernels' C-ABI object)
-# -> abl/libnavenv_NAME.so (load it with NAV_LIB=abl/libnavenv_NAME.so)
+# -> abl/libnavenv_NAME.so (bind it with python tools/withlib.py abl/libnavenv_NAME.so SCRIPT ...)
 set -eu
 cd "$(dirname "$0")/.."
 name=$1; unit=$2; flags=$3

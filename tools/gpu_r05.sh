@@ -1,17 +1,19 @@
 #!/bin/bash
-# One gpurun call of round 4 (run from the repo root through gpurun): the named steps in order,
+# One gpurun call of round 5 (run from the repo root through gpurun): the named steps in order,
 # each under its own time limit; a fault / abort / timeout (exit status other than 0 or 1) ends
 # the call there. Output under gpurun_out/TAG/.
 #   tests     GPU test suite
 #   mlptests  the MLP / learner GPU tests only
 #   smoke     __graft_entry__.smoke()
-#   wgrad     tools/wgrad_bench.py on this tree and on abl/head (the previous HEAD, if present)
-#   ab        interleaved same-box bench A/B: this tree vs abl/head, 3 rounds
+#   wgrad     tools/wgrad_bench.py on this tree's library
 #   bench     the default bench line
 #   prof      rocprofv3 kernel trace + stats of a short bench
 #   pmc       FETCH_SIZE / WRITE_SIZE / SQ passes of a short bench (separate runs)
 #   vab       interleaved bench A/B (3 rounds, kernel times included): this tree's library vs
-#             each abl/libnavenv_$v.so named in $VARS
+#             each abl/libnavenv_$v.so named in $VARS (bound through tools/withlib.py; `prev` =
+#             the previous HEAD's library, tools/build_prev.sh)
+#   clock     held shader clock of the row kernels (tools/clock_probe.py on abl/libnavenv_clock.so)
+#   shape     tools/probe/mfma_shape_probe (build/mfma_shape_probe): 32x32x16 vs 16x16x32 split GEMM
 #   phase     critic_rows phase trace (abl/libnavenv_$v.so for each $v in $PVARS, default
 #             trace) at batch 32768 (two workgroups per CU) and 16448 (one), and act_tick's
 #   wpmc      SQ counters and timing of tools/wgrad_bench.py for this tree's library and each
@@ -41,12 +43,7 @@ for step in "$@"; do
     tests) run gputest 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     mlptests) run mlptest 300 python -u -m pytest tests/test_gpu_mlp.py tests/test_gpu_fullsize.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    wgrad) run wgrad_new 200 python tools/wgrad_bench.py
-           if [ -d abl/head ]; then (cd abl/head && run wgrad_old 200 python tools/wgrad_bench.py); fi ;;
-    ab) for r in 1 2 3; do
-          run ab_new_$r 200 python bench.py $SHORT --steps 60 --warmup 5 --no-timed-events
-          (cd abl/head && run ab_old_$r 200 python bench.py $SHORT --steps 60 --warmup 5 --no-timed-events)
-        done ;;
+    wgrad) run wgrad 200 python tools/wgrad_bench.py ;;
     bench) run bench 500 python bench.py ;;
     prof) run prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace" -o run -- python bench.py $SHORT ;;
     pmc) run pmc_fetch 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/fetch" -o run -- python bench.py $PMCB &&
@@ -54,26 +51,25 @@ for step in "$@"; do
          run pmc_sq 150 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$O/sq" -o run -- python bench.py $PMCB ;;
     wpmc) for v in "" $WVARS; do
             tag=${v:-base}
-            if [ -n "$v" ]; then export NAV_LIB=$ROOT/abl/libnavenv_$v.so; else unset NAV_LIB; fi
-            run wpmc_$tag 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$O/wpmc_$tag" -o run -- python tools/wgrad_bench.py --reps 5
-            run wvar_$tag 120 python tools/wgrad_bench.py
-          done
-          unset NAV_LIB ;;
+            W=(); [ -n "$v" ] && W=(tools/withlib.py "$ROOT/abl/libnavenv_$v.so")
+            run wpmc_$tag 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$O/wpmc_$tag" -o run -- python "${W[@]}" tools/wgrad_bench.py --reps 5
+            run wvar_$tag 120 python "${W[@]}" tools/wgrad_bench.py
+          done ;;
     vab) for r in 1 2 3; do
            for v in "" $VARS; do
              tag=${v:-base}
-             if [ -n "$v" ]; then export NAV_LIB=$ROOT/abl/libnavenv_$v.so; else unset NAV_LIB; fi
-             run vab_${tag}_$r 200 python bench.py $SHORT --steps 60 --warmup 5
+             W=(); [ -n "$v" ] && W=(tools/withlib.py "$ROOT/abl/libnavenv_$v.so")
+             run vab_${tag}_$r 200 python "${W[@]}" bench.py $SHORT --steps 60 --warmup 5
            done
-         done
-         unset NAV_LIB ;;
+         done ;;
     phase) for v in ${PVARS:-trace}; do
-             export NAV_LIB=$ROOT/abl/libnavenv_$v.so
-             run phase_${v}_32768 200 python tools/phase_trace.py --batch 32768
-             run phase_${v}_16448 200 python tools/phase_trace.py --batch 16448
-             run phase_${v}_tick 200 python tools/phase_trace.py --tick
-           done
-           unset NAV_LIB ;;
+             W=(tools/withlib.py "$ROOT/abl/libnavenv_$v.so")
+             run phase_${v}_32768 200 python "${W[@]}" tools/phase_trace.py --batch 32768
+             run phase_${v}_16448 200 python "${W[@]}" tools/phase_trace.py --batch 16448
+             run phase_${v}_tick 200 python "${W[@]}" tools/phase_trace.py --tick
+           done ;;
+    clock) run clock 200 python tools/withlib.py "$ROOT/abl/libnavenv_clock.so" tools/clock_probe.py --seconds 3 ;;
+    shape) run shape 200 ./build/mfma_shape_probe 512 2.5 0 && run shape_dz 200 ./build/mfma_shape_probe 512 2.5 1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -1,11 +1,11 @@
 """Phase timing of k_td3_critic_rows at the bench shape (tuning probe, not a test).
 
 Needs a library built with -DNAV_PHASE_TRACE (tools/build_variant.sh trace mlp8 -DNAV_PHASE_TRACE)
-loaded through NAV_LIB. Runs the bench trainer for a few steps, then reads the s_memtime marks of
+bound through tools/withlib.py. Runs the bench trainer for a few steps, then reads the s_memtime marks of
 4 traced workgroups (blocks 0, 1, 200, 511) x 4 waves and prints each phase's duration in
 cycles of that counter, per wave, plus the per-phase mean over the 16 traced waves.
 
-NAV_LIB=abl/libnavenv_trace.so python tools/phase_trace.py [--batch B]
+python tools/withlib.py abl/libnavenv_trace.so tools/phase_trace.py [--batch B]
 (--batch 16448: 257 workgroups of 64 rows, so the traced ones run alone on their CU)
 """
 import ctypes as C
@@ -58,14 +58,14 @@ def main():
                     help="a -DNAV_TRACE_WIDE build: 64 blocks (0, 8, 16, ...), per block its start "
                          "and end relative to the earliest traced start, plus the phase means")
     args = ap.parse_args()
-    from nav._lib import LIB_PATH
+    from nav._lib import lib_path
     from nav.trainer import VecTrainer
     tr = VecTrainer(n_envs=65536, hidden=256, n_hidden=2, batch=args.batch, updates_per_step=2,
                     envs_per_group=1024)
     for _ in range(4):
         tr.step()
     torch.cuda.synchronize()
-    raw = C.CDLL(LIB_PATH)
+    raw = C.CDLL(lib_path())
     nt = 64 if args.wide else 4
     buf = (C.c_ulonglong * (nt * 4 * 64))()
     rc = raw.nav_phase_trace_read(buf, nt * 4 * 64)
