@@ -36,11 +36,23 @@ from nav import prof  # noqa: E402
 EVENT_SAMPLE = 8             # timed region: event pairs around 1 launch in 8 of the dominant kernel
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP64_VALU_PEAK_TFS = 78.6    # MI355X spec FP64 vector
-BF16_MFMA_PEAK_TFS = 2516.6  # MI355X_MICROARCH.md: 1024 FLOP/clk/SIMD x 1024 SIMDs x 2.4 GHz (dense)
-# bf16 MFMA partial products per hidden x hidden layer of each row kernel: one entry per network
-# pass (forwards + row backwards). A pass with both operands split three ways (hi + mid + lo)
-# runs 6 products; these are the bf16 FLOPs the matrix cores execute for the f32 GEMM
-HIDDEN_PRODUCTS = {"critic_rows": [6] * 7, "actor_rows": [6] * 4, "act": [6], "act_tick": [6]}
+F16_MFMA_PEAK_TFS = 2516.6  # MI355X_MICROARCH.md: 1024 FLOP/clk/SIMD x 1024 SIMDs x 2.4 GHz
+#                             (dense fp16 = bf16 rate)
+# The row kernels' hidden x hidden f32 GEMMs run on the fp16 matrix cores as 3 products of a
+# scaled two-plane split (lo.hi + hi.lo + hi.hi; rounds 3-4: 6 products of a three-plane bf16
+# split): the MFMA FLOPs per f32 product, and the network passes (forwards + row backwards) per
+# row block of each row kernel
+PRODUCTS_PER_PASS = 3
+ROOFLINE_VERSION = "r05: fp16 two-plane split, 3 products per f32 product (r03-r04: bf16 6)"
+
+
+def hidden_passes(region, rows):
+    """Hidden x hidden GEMM passes per row block: critic_rows 7 (target actor, 2 target critics,
+    2 online forwards, 2 row backwards), or 10 at batches <= 2048 where the twins split into two
+    workgroups that each repeat the 3 target passes; actor_rows 4; the acting forward 1."""
+    if region == "critic_rows":
+        return 10 if rows <= 2048 else 7
+    return {"actor_rows": 4, "act": 1, "act_tick": 1}.get(region, 0)
 # HBM bytes per launch from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this same
 # command (tools/pmc_traffic.py, gfx950 correction applied); bench regions -> kernel names
 PMC_TRAFFIC = os.path.join(HERE, "profiles", "pmc_traffic.json")
@@ -374,24 +386,25 @@ def main():
                     "frac": round(tf / FP64_VALU_PEAK_TFS, 4), "traffic": traffic,
                     "traffic_source": traffic_src, "avg_us": round(d["avg_us"], 2)}
         else:
-            # the matrix-core view: the bf16 FLOPs the kernel's hidden x hidden GEMMs execute
-            # (each f32 product as bf16 partial products of the exact split) against the bf16
-            # dense peak; the f32-equivalent rate of all its FLOPs is a separate key
+            # the matrix-core view: the MFMA FLOPs the kernel's hidden x hidden GEMMs execute
+            # (each f32 product as 3 fp16 products of the scaled two-plane split) against the
+            # fp16 dense peak; the f32-equivalent rate of all its FLOPs is a separate key
             hp = (args.hidden + 31) // 32 * 32
             rows = args.envs if dominant in ("act", "act_tick") else rank_batch
             layer = (args.layers - 1) * 2.0 * rows * hp * hp
-            prods = HIDDEN_PRODUCTS.get(dominant, [])
-            hidden = len(prods) * layer
-            bf16_flop = sum(prods) * layer
-            bf16 = bf16_flop / (d["avg_us"] * 1e-6) / 1e12
-            roof = {"bound": "mfma", "kernel": dominant, "achieved": round(bf16, 1),
-                    "peak": BF16_MFMA_PEAK_TFS, "unit": "TFLOP/s",
-                    "frac": round(bf16 / BF16_MFMA_PEAK_TFS, 4),
-                    "peak_note": "bf16 dense MFMA peak: the hidden x hidden f32 GEMMs run on the "
-                                 "bf16 matrix cores as partial products of an exact 3-way bf16 "
-                                 "split (f32 accuracy); achieved = those bf16 FLOPs per launch / "
-                                 "the launch's event-timed duration",
-                    "bf16_flop_per_launch": bf16_flop,
+            hidden = hidden_passes(dominant, rows) * layer
+            mfma_flop = PRODUCTS_PER_PASS * hidden
+            tfs = mfma_flop / (d["avg_us"] * 1e-6) / 1e12
+            roof = {"bound": "mfma", "kernel": dominant, "achieved": round(tfs, 1),
+                    "peak": F16_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                    "frac": round(tfs / F16_MFMA_PEAK_TFS, 4),
+                    "version": ROOFLINE_VERSION,
+                    "peak_note": "fp16 dense MFMA peak: the hidden x hidden f32 GEMMs run on the "
+                                 "fp16 matrix cores as 3 products of a power-of-two-scaled "
+                                 "two-plane fp16 split (f32 accuracy, pinned vs fp64); achieved "
+                                 "= those MFMA FLOPs per launch / the launch's event-timed "
+                                 "duration",
+                    "mfma_flop_per_launch": mfma_flop,
                     "hidden_gemm_f32_flop_per_launch": hidden,
                     "f32_equiv": {"flop_per_launch": d["work_per_launch"],
                                   "achieved_TFs": round(ach / 1e12, 2),

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define NAV_ABI_VERSION 9
+#define NAV_ABI_VERSION 10
 #define NAV_EINVAL (-100000)
 
 #define NAV_WORLD_CELLS 100 /* field = float32 [100][100][2] (speed, angle), x-major: cell cx*100+cy
@@ -80,10 +80,10 @@ typedef struct nav_step_out {
     float* block_stats;   /* nullable: [ceil(n/64)][8], row k = envs [64k, 64k+64): sum of the
                              reward pushed to the replay rows, n_done, n_goal, n_stuck, n_ended,
                              0, 0, 0 (one wave's shuffle tree per row: deterministic). The sum
-                             includes the demo term wherever the demo pass runs in the same
-                             launch (nav_agent_step_indexed, nav_act_tick); after nav_agent_step
-                             with demo_pending it lacks the flagged envs' demo term, which
-                             nav_demo_reward(_indexed) adds to their rows later                 */
+                             is of the final pushed rewards in every launch form: the demo pass
+                             of nav_agent_step_indexed / nav_act_tick runs in the same launch;
+                             after nav_agent_step with demo_pending, nav_demo_reward(_indexed)
+                             given this pointer rewrites the rows of flagged envs             */
 } nav_step_out;
 
 /* Replay ring (device): rows [capacity][8] float32 (robot.py:58-124 ReplayBuffer). */
@@ -95,10 +95,14 @@ typedef struct nav_replay {
 /* ReLU MLP (robot.py:128-206) in the device layout: one flat fp32 buffer per network,
  * hidden width padded to a multiple of 32 with zeros (exact: relu(0)=0, zero rows/cols add 0):
  *   W0 [hp][d_in], b0 [hp], {Wl [hp][hp], bl [hp]} x (n_hidden-1), Wo [d_out][hp], bo [d_out]
- * plus `packed` = per hidden->hidden layer the split bf16 MFMA B-operand images of the forward
- * (B[k][n] = W[n][k]) then of the backward (B[k][n] = W[k][n]) product: each W entry as three
- * bf16 hi + mid + lo == W exactly, laid out [plane 3][hp/16][2][hp][8] (entry (p, k/16, (k/8)&1,
- * n, k&7)), 1.5 hp^2 floats per image; kept current by nav_adam / nav_polyak / nav_mlp_pack. */
+ * plus `packed` = per hidden->hidden layer the fp16 MFMA B-operand images of the forward
+ * (B[k][n] = W[n][k]) then of the backward (B[k][n] = W[k][n]) product: per column n an exponent
+ * e_n (B's column max |B| 2^e_n in [2^13, 2^14)) and each entry as two fp16 planes hi =
+ * fp16(B 2^e_n), lo = fp16(B 2^e_n - hi) (22 significant bits), laid out [plane 2][hp/16][2][hp][8]
+ * (entry (p, k/16, (k/8)&1, n, k&7)) followed by int32 e[hp]: hp^2 + hp floats per image; rebuilt
+ * after every writer by nav_adam(_multi) / nav_polyak(_multi) / nav_grad_reduce_adam(_polyak) /
+ * nav_mlp_pack (one extra launch on the same stream). ABI 10: the image format (ABI 9: three
+ * bf16 planes, 1.5 hp^2 floats). */
 typedef struct nav_mlp {
     int32_t d_in;       /* 2 actor (robot.py:145), 4 critic (robot.py:185) */
     int32_t d_out;      /* 2 actor, 1 critic */
@@ -171,12 +175,15 @@ int nav_check_if_stuck(const nav_params* p, const nav_env_soa* env, const double
 /* robot.py:741-762 demo-proximity term for envs flagged by nav_agent_step:
  * r = (goal_term + demo_factor * -min_j ||s' - d_j||) - stuck_penalty*stuck, written to the
  * replay row. demo_xy [m][2] f64 per group: group g = env / envs_per_group uses
- * demo_xy[demo_off[g] .. demo_off[g+1]) (demo_off NULL = one shared set of m points). */
+ * demo_xy[demo_off[g] .. demo_off[g+1]) (demo_off NULL = one shared set of m points).
+ * block_stats (nullable, nav_step_out's [ceil(n/64)][8] of the nav_agent_step this pass
+ * completes): the reward column of every 64-env row holding a flagged env is summed again from
+ * the final pushed rewards, so it equals the one-launch forms' column bit for bit. */
 int nav_demo_reward(const nav_params* p, int64_t n, const double* next_state,
                     const double* goal_term, const uint8_t* flags, const double* demo_xy,
                     const int64_t* demo_off, int64_t m, int32_t envs_per_group,
                     const nav_replay* replay, int64_t replay_base, double* reward_out,
-                    void* stream);
+                    float* block_stats, void* stream);
 /* Exact bucketed nearest-demo index (robot.py:753 made sublinear, result bit-identical to the
  * brute force), built in two levels.
  * Level 1, the 100 x 100 dynamics cells over all points of each group: for each (group, cell) the
@@ -207,13 +214,13 @@ int nav_demo_index_subfill(const double* demo_xy, const int64_t* demo_off, int32
                            const double* sub_bound, const int64_t* sub_start, int32_t* sub_cand,
                            void* stream);
 /* nav_demo_reward through the level-2 index (same result, a few instead of 11 355 points per
- * env). */
+ * env; block_stats as there). */
 int nav_demo_reward_indexed(const nav_params* p, int64_t n, const double* next_state,
                             const double* goal_term, const uint8_t* flags, const double* demo_xy,
                             const int64_t* demo_off, int32_t envs_per_group,
                             const int64_t* cell_start, const int32_t* cand,
                             const nav_replay* replay, int64_t replay_base, double* reward_out,
-                            void* stream);
+                            float* block_stats, void* stream);
 /* nav_agent_step + nav_demo_reward_indexed in one launch (same results bit for bit): flagged envs
  * get their demo-proximity reward through the index before the replay row is written, so the row
  * is stored once with the final reward. reward_out (nullable) [n] receives the reward of the

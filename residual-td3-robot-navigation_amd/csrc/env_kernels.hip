@@ -902,6 +902,23 @@ __global__ __launch_bounds__(kBlock) void k_demo_reward_idx(nav_params p, int64_
     if (reward_out) reward_out[e] = r;
 }
 
+// block_stats' reward column after a separate demo pass (nav_demo_reward(_indexed) with
+// block_stats): the row of every 64 envs that hold a flagged env is summed again from the pushed
+// rewards (the replay rows, now final) — the same wave tree over the same floats as the tick
+// that runs the demo pass in its own launch, so every launch form reports the pushed reward.
+__global__ __launch_bounds__(kBlock) void k_restat_reward(int64_t n, const uint8_t* __restrict__ flags,
+                                                          const float* __restrict__ rows,
+                                                          int64_t cap, int64_t base,
+                                                          float* __restrict__ block_stats) {
+    const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const bool live = e < n;
+    const bool flagged = live && (flags[e] & F_DEMO);
+    if (!__any(flagged)) return;  // wave-uniform
+    const float r = live ? rows[((base + e) % cap) * NAV_ROW + 4] : 0.f;
+    const float v = wave_sum(r);
+    if ((threadIdx.x & 63) == 0) block_stats[(e >> 6) * 8] = v;
+}
+
 // One training tick per env (see navenv.h nav_agent_step). DEMO: the demo-proximity reward of
 // flagged envs through the index in the same launch (nav_agent_step_indexed): the block's demo
 // pass walks all its flagged envs' candidate lists together. One statistics row per wave.
@@ -1270,7 +1287,7 @@ int nav_replay_push(const nav_replay* replay, int64_t base, int64_t n, const dou
 int nav_demo_reward(const nav_params* p, int64_t n, const double* next_state,
                     const double* goal_term, const uint8_t* flags, const double* demo_xy,
                     const int64_t* demo_off, int64_t m, int32_t epg, const nav_replay* replay,
-                    int64_t replay_base, double* reward_out, void* stream) {
+                    int64_t replay_base, double* reward_out, float* block_stats, void* stream) {
     if (!p || n < 0 || !replay || !replay->rows || replay->capacity <= 0 || replay_base < 0)
         return NAV_EINVAL;
     if (n && (!next_state || !goal_term || !flags)) return NAV_EINVAL;
@@ -1282,16 +1299,21 @@ int nav_demo_reward(const nav_params* p, int64_t n, const double* next_state,
                            *p, reinterpret_cast<const double2*>(next_state), goal_term, flags,
                            demo_xy, demo_off, m, epg > 0 ? epg : 1, replay->rows,
                            replay->capacity, replay_base % replay->capacity, reward_out);
-        NAV_CHECK_LAUNCH();
-        return 0;
+    } else {
+        hipLaunchKernelGGL(k_demo_reward, dim3((unsigned)((n + kDemoEnvs - 1) / kDemoEnvs)),
+                           dim3(kDemoBlock), 0, S(stream), *p, n,
+                           reinterpret_cast<const double2*>(next_state), goal_term, flags, demo_xy,
+                           demo_off, m, epg > 0 ? epg : 1,
+                           replay->rows, replay->capacity, replay_base % replay->capacity,
+                           reward_out);
     }
-    hipLaunchKernelGGL(k_demo_reward, dim3((unsigned)((n + kDemoEnvs - 1) / kDemoEnvs)),
-                       dim3(kDemoBlock), 0, S(stream), *p, n,
-                       reinterpret_cast<const double2*>(next_state), goal_term, flags, demo_xy,
-                       demo_off, m, epg > 0 ? epg : 1,
-                       replay->rows, replay->capacity, replay_base % replay->capacity,
-                       reward_out);
     NAV_CHECK_LAUNCH();
+    if (block_stats) {
+        hipLaunchKernelGGL(k_restat_reward, dim3(blocks_for(n)), dim3(kBlock), 0, S(stream), n,
+                           flags, replay->rows, replay->capacity, replay_base % replay->capacity,
+                           block_stats);
+        NAV_CHECK_LAUNCH();
+    }
     return 0;
 }
 
@@ -1383,7 +1405,7 @@ int nav_demo_reward_indexed(const nav_params* p, int64_t n, const double* next_s
                             const int64_t* demo_off, int32_t envs_per_group,
                             const int64_t* cell_start, const int32_t* cand,
                             const nav_replay* replay, int64_t replay_base, double* reward_out,
-                            void* stream) {
+                            float* block_stats, void* stream) {
     if (!p || n < 0 || !replay || !replay->rows || replay->capacity <= 0 || replay_base < 0 ||
         (demo_off && envs_per_group <= 0))
         return NAV_EINVAL;
@@ -1397,6 +1419,12 @@ int nav_demo_reward_indexed(const nav_params* p, int64_t n, const double* next_s
                        replay->rows, replay->capacity, replay_base % replay->capacity,
                        reward_out);
     NAV_CHECK_LAUNCH();
+    if (block_stats) {
+        hipLaunchKernelGGL(k_restat_reward, dim3(blocks_for(n)), dim3(kBlock), 0, S(stream), n,
+                           flags, replay->rows, replay->capacity, replay_base % replay->capacity,
+                           block_stats);
+        NAV_CHECK_LAUNCH();
+    }
     return 0;
 }
 

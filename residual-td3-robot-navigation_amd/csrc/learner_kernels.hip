@@ -200,6 +200,42 @@ NAV_DEV void wgrad_rows(const WgradArgs& a, int y, int L, int n0, int k0, int64_
     }
 }
 
+// Wave-uniform max |dy_d| (d < d_out) and max |x_i| (i < d_in) over the wave's rows [r_lo, r_hi):
+// the bounds behind the fp16 operand scales of the weight-gradient products (a bound within a
+// few binades of the true max costs nothing: the lo plane's absolute step stays 2^-24 of the
+// scaled bound).
+NAV_DEV void row_maxima(const WgradArgs& a, int y, int64_t r_lo, int64_t r_hi, float (&G)[2],
+                        float (&X)[4]) {
+    const int lane = threadIdx.x & 63, d_in = a.net[y].d_in, d_out = a.net[y].d_out;
+    float g0 = 0.f, g1 = 0.f, x0 = 0.f, x1 = 0.f, x2 = 0.f, x3 = 0.f;
+    for (int64_t r = r_lo + lane; r < r_hi; r += 64) {
+        const float* g = a.dy[y] + r * a.ld_dy;
+        const float* x = a.in + r * a.ld_in + a.in_col;
+        g0 = fmaxf(g0, fabsf(g[0]));
+        if (d_out > 1) g1 = fmaxf(g1, fabsf(g[1]));
+        x0 = fmaxf(x0, fabsf(x[0]));
+        if (d_in > 1) x1 = fmaxf(x1, fabsf(x[1]));
+        if (d_in > 2) x2 = fmaxf(x2, fabsf(x[2]));
+        if (d_in > 3) x3 = fmaxf(x3, fabsf(x[3]));
+    }
+    // wave-uniform: scalar registers
+    auto su = [](float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(wave_max_abs(v)))); };
+    G[0] = su(g0);
+    G[1] = su(g1);
+    X[0] = su(x0);
+    X[1] = su(x1);
+    X[2] = su(x2);
+    X[3] = su(x3);
+}
+
+// Bound on |h_0[r][c]| = relu(b0[c] + sum_i x_ri W0[c][i]) for the column c of this lane from the
+// lane half's constants (inputs h and 2 + h; the bias on h = 0): sum_i X_i |W0[c][i]| + |b0[c]|.
+NAV_DEV float h0_bound(const float (&X)[4], float wa, float wb, float bias) {
+    const int h = (threadIdx.x & 63) >> 5;
+    const float part = (h ? X[1] : X[0]) * fabsf(wa) + (h ? X[3] : X[2]) * fabsf(wb) + fabsf(bias);
+    return part + __shfl_xor(part, 32, 64);
+}
+
 // The MFMA-operand path for a full 64 x 64 tile of a 2-hidden-layer network with d_out = 2 (the
 // actor; d_out = 1 takes the factored path below).
 // The operands are produced by MFMAs too: per 32-row tile, dz = dy . Wo (K = d_out <= 2, one
@@ -235,6 +271,28 @@ NAV_DEV void wgrad_rows_mfma(const WgradArgs& a, int y, int n0, int k0, int64_t 
             w0b[i][0] = h < d_in ? W0[c * d_in + h] : 0.f;
             w0b[i][1] = 2 + h < d_in ? W0[c * d_in + 2 + h] : 0.f;
             bob[i] = h == 0 ? bb[c] : 0.f;
+        }
+    }
+    if (r_lo >= r_hi) return;
+    // fp16 operand scales (mlp_common.h), folded into the operand MFMAs' constants (a power of two
+    // commutes with every rounding of the f32 chains): P column tile i by 2^ep[i] from the bound
+    // sum_d max|g_d| |Wo[d][n]| (max over the tile's 32 n), Q column k by 2^eq[j] from h0_bound
+    int ep[2], eq[2];
+    {
+        float G[2], X[4];
+        row_maxima(a, y, r_lo, r_hi, G, X);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            float b = G[h] * fabsf(wob[i]);
+            b += __shfl_xor(b, 32, 64);
+#pragma unroll
+            for (int m = 1; m < 32; m <<= 1) b = fmaxf(b, __shfl_xor(b, m, 64));
+            ep[i] = pow2_exp(b);
+            wob[i] = ldexpf(wob[i], ep[i]);
+            eq[i] = pow2_exp(h0_bound(X, w0b[i][0], w0b[i][1], bob[i]));
+            w0b[i][0] = ldexpf(w0b[i][0], eq[i]);
+            w0b[i][1] = ldexpf(w0b[i][1], eq[i]);
+            bob[i] = ldexpf(bob[i], eq[i]);
         }
     }
     const float one = h == 0 ? 1.f : 0.f;
@@ -310,9 +368,8 @@ NAV_DEV void wgrad_rows_mfma(const WgradArgs& a, int y, int n0, int k0, int64_t 
             Q[1][e] = __int_as_float(max(__float_as_int(Q[1][e]), 0));
         }
     };
-    if (r_lo >= r_hi) return;
     // per 32-row tile: the operand MFMAs, their ReLU epilogue, then the tile's two 16-deep k steps
-    // of the bf16 product (the partner wave on the SIMD keeps the matrix pipe busy while this one
+    // of the fp16 product (the partner wave on the SIMD keeps the matrix pipe busy while this one
     // waits for its operand MFMAs; double-buffering the operand tiles would not fit the 256
     // registers of two waves per SIMD next to the split fragments). The raw loads run two tiles
     // ahead.
@@ -326,26 +383,37 @@ NAV_DEV void wgrad_rows_mfma(const WgradArgs& a, int y, int n0, int k0, int64_t 
         issue(rt, cur, P, Q);
         finish(cur, P, Q);
         // registers 8s .. 8s+7 of the C-layout operands are k step s (rows 16s + 8(j>>2) + 4h +
-        // (j&3), the same for P and Q), each split three ways (mlp_common.h) right before its six
-        // partial products
+        // (j&3), the same for P and Q), each (already scaled) split into two fp16 planes right
+        // before its three products
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
-            Split3 sp[2], sq[2];
+            Split2 sp[2], sq[2];
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                sp[i] = split8(make_float4(P[i][8 * s2], P[i][8 * s2 + 1], P[i][8 * s2 + 2], P[i][8 * s2 + 3]),
-                               make_float4(P[i][8 * s2 + 4], P[i][8 * s2 + 5], P[i][8 * s2 + 6], P[i][8 * s2 + 7]));
-                sq[i] = split8(make_float4(Q[i][8 * s2], Q[i][8 * s2 + 1], Q[i][8 * s2 + 2], Q[i][8 * s2 + 3]),
-                               make_float4(Q[i][8 * s2 + 4], Q[i][8 * s2 + 5], Q[i][8 * s2 + 6], Q[i][8 * s2 + 7]));
+                float vp[8], vq[8];
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    vp[t] = P[i][8 * s2 + t];
+                    vq[t] = Q[i][8 * s2 + t];
+                }
+                sp[i] = split2_8(vp);
+                sq[i] = split2_8(vq);
             }
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
-                for (int j = 0; j < 2; ++j) acc[i][j] = mfma_x6s(sp[i], sq[j], acc[i][j]);
+                for (int j = 0; j < 2; ++j) acc[i][j] = mfma_x3s(sp[i], sq[j], acc[i][j]);
         }
         cur = nxt;
         nxt = nn;
     }
+    // unscale: tile (i, j) by 2^-(ep[i] + eq[j]) (eq per lane column), exact
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = ldexpf(acc[i][j][e], -(ep[i] + eq[j]));
 }
 
 // ---- the factored form for 2-hidden-layer networks (the bench shape) ----
@@ -353,12 +421,14 @@ NAV_DEV void wgrad_rows_mfma(const WgradArgs& a, int y, int n0, int k0, int64_t 
 //   dz_1[r][n] = e[r][n] sum_d g_d[r] Wo[d][n]        (robot.py:355-363 autograd, d < d_out)
 //   dW_1[n][k] = sum_r dz_1[r][n] h_0[r][k] = sum_d Wo[d][n] S_d[n][k],
 //   S_d[n][k]  = sum_r e[r][n] Q_d[r][k],   Q_d[r][k] = g_d[r] h_0[r][k].
-// The A operand of S_d is the ReLU bit itself, exact in bf16 (as 2.0, the 0.5 goes into Wo; 8
-// bits of a mask word become an A fragment by one 16-B read of a 256-entry LDS table), and
-// only the B operand Q_d is split — three bf16 planes, exactly, so the product carries f32
-// accuracy with 3 MFMAs per 16-deep k step and 32 x 32 tile instead of the 6 of a product with
-// both operands split, and nothing per element on the n side. That frees a wave to own NI = 4
-// column tiles of n (128 x 64) at D = 1 — the twin critics — for 128 accumulator registers.
+// The A operand of S_d is the ReLU bit itself, exact in fp16 (as 2.0, the 0.5 goes into Wo; 8
+// bits of a mask word become an A fragment by one 16-B read of a 256-entry LDS table — fp16 2.0
+// and bf16 2.0 share the bit pattern 0x4000), and only the B operand Q_d is split: scaled by a
+// power of two (h_0 per column k into [2^6, 2^7) through the layer-0 constants, g_d per wave into
+// [2^7, 2^8) from the wave's max |g_d|) and cut into two fp16 planes, so the product carries f32
+// accuracy with 2 MFMAs per 16-deep k step and 32 x 32 tile (the three-plane bf16 form: 3), and
+// nothing per element on the n side. That frees a wave to own NI = 4 column tiles of n
+// (128 x 64) at D = 1 — the twin critics — for 128 accumulator registers.
 
 
 template <int NI, int D>
@@ -394,6 +464,29 @@ NAV_DEV void wgrad_rows_fact(const WgradArgs& a, int y, int n0, int k0, int64_t 
             bob[j] = h == 0 ? bb[c] : 0.f;
         }
     }
+    // the fp16 scales of Q_d = relu(h_0) g_d: h_0 column half j by 2^eh[j] (folded into the
+    // layer-0 constants: a power of two commutes with the fma chain's roundings), g_d by 2^eg[d]
+    int eh[2], eg[D];
+    float sg[D];
+    {
+        float G[2], X[4];
+        row_maxima(a, y, r_lo, r_hi, G, X);
+        // per 32-column half (wave-uniform, scalar registers: the 128-accumulator program has no
+        // vector register to spare)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            eh[j] = __builtin_amdgcn_readfirstlane(
+                pow2_exp_to(wave_max_abs(h0_bound(X, w0b[j][0], w0b[j][1], bob[j])), 7));
+            w0b[j][0] = ldexpf(w0b[j][0], eh[j]);
+            w0b[j][1] = ldexpf(w0b[j][1], eh[j]);
+            bob[j] = ldexpf(bob[j], eh[j]);
+        }
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            eg[d] = pow2_exp_to(G[d], 8);
+            sg[d] = ldexpf(1.f, eg[d]);
+        }
+    }
     const float one = h == 0 ? 1.f : 0.f;
     const bool x23 = d_in > 2;
     const size_t mstride = (size_t)NTm * 64;
@@ -417,8 +510,8 @@ NAV_DEV void wgrad_rows_fact(const WgradArgs& a, int y, int n0, int k0, int64_t 
 #pragma unroll
         for (int i = 0; i < NI; ++i) v.m[i] = m[i * 64];
     };
-    // one 32-row tile: h_0 by the f32 MFMAs, Q_d = relu(h_0) g_d split per k step, 3 MFMAs per
-    // (i, j, d) and step. gs[s2][d][t]: g_d of the row of register e = 8 s2 + t
+    // one 32-row tile: h_0 by the f32 MFMAs, Q_d = relu(h_0) g_d split per k step, 2 MFMAs per
+    // (i, j, d) and step. gs[s2][d][t]: g_d (scaled) of the row of register e = 8 s2 + t
     auto tile = [&](const Raw& cur, const float (&gs)[2][D][8]) {
         const float x0 = h < d_in ? cur.x0 : 0.f, x1 = 2 + h < d_in ? cur.x1 : 0.f;
         // one 32-column half j of the k side at a time (16 registers of h_0 live)
@@ -438,8 +531,7 @@ NAV_DEV void wgrad_rows_fact(const WgradArgs& a, int y, int n0, int k0, int64_t 
 #pragma unroll
                     for (int t = 0; t < 8; ++t)
                         q[t] = __int_as_float(max(__float_as_int(Z[8 * s2 + t]), 0)) * gs[s2][d][t];
-                    const Split3 sq = split8(make_float4(q[0], q[1], q[2], q[3]),
-                                             make_float4(q[4], q[5], q[6], q[7]));
+                    const Split2 sq = split2_8(q);
 #pragma unroll
                     for (int i = 0; i < NI; ++i) {
                         // the fragment of byte s2 of the mask word, read from the table right
@@ -447,10 +539,9 @@ NAV_DEV void wgrad_rows_fact(const WgradArgs& a, int y, int n0, int k0, int64_t 
                         // all NI x 2 fragments live across the passes over j)
                         uint32_t ta = (s2 == 0 ? cur.m[i] << 4 : cur.m[i] >> 4) & 0xFF0u;
                         asm volatile("" : "+v"(ta));
-                        const bf16x8 pi = *reinterpret_cast<const bf16x8*>(tab + ta);
-                        acc[d][i][j] = mfma16(pi, sq.l, acc[d][i][j]);
-                        acc[d][i][j] = mfma16(pi, sq.m, acc[d][i][j]);
-                        acc[d][i][j] = mfma16(pi, sq.h, acc[d][i][j]);
+                        const f16x8 pi = *reinterpret_cast<const f16x8*>(tab + ta);
+                        acc[d][i][j] = mfma_h(pi, sq.l, acc[d][i][j]);
+                        acc[d][i][j] = mfma_h(pi, sq.h, acc[d][i][j]);
                     }
                 }
         }
@@ -484,6 +575,12 @@ NAV_DEV void wgrad_rows_fact(const WgradArgs& a, int y, int n0, int k0, int64_t 
                         for (int d = 0; d < D; ++d) gs[s2][d][4 * qq + t] = g[t * ld_dy + d];
                 }
             }
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+            for (int d = 0; d < D; ++d)
+#pragma unroll
+                for (int t = 0; t < 8; ++t) gs[s2][d][t] *= sg[d];
     };
     if (r_lo < r_full) {
         // d_out = 2 loads its 32 g values at the tile (prefetched they do not fit the registers)
@@ -518,7 +615,7 @@ NAV_DEV void wgrad_rows_fact(const WgradArgs& a, int y, int n0, int k0, int64_t 
         for (int e = 0; e < 16; ++e) {
             const int64_t r = r_full + acc_row(e, h);
 #pragma unroll
-            for (int d = 0; d < D; ++d) gs[e >> 3][d][e & 7] = r < r_hi ? dyp[r * ld_dy + d] : 0.f;
+            for (int d = 0; d < D; ++d) gs[e >> 3][d][e & 7] = r < r_hi ? dyp[r * ld_dy + d] * sg[d] : 0.f;
         }
         tile(cur, gs);
     }
@@ -542,11 +639,11 @@ NAV_DEV void wgrad_rows_fact(const WgradArgs& a, int y, int n0, int k0, int64_t 
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
                     const float w0 = (t == 0 ? wv[0].x : t == 1 ? wv[0].y : t == 2 ? wv[0].z : wv[0].w) * 0.5f;
-                    float v = w0 * acc[0][i][j][e];
+                    float v = w0 * ldexpf(acc[0][i][j][e], -(eh[j] + eg[0]));
                     if (D > 1) {
                         const float w1 = (t == 0 ? wv[D - 1].x : t == 1 ? wv[D - 1].y
                                           : t == 2 ? wv[D - 1].z : wv[D - 1].w) * 0.5f;
-                        v = fmaf(w1, acc[D - 1][i][j][e], v);
+                        v = fmaf(w1, ldexpf(acc[D - 1][i][j][e], -(eh[j] + eg[D - 1])), v);
                     }
                     out[i][j][e] = v;
                 }
@@ -623,8 +720,8 @@ NAV_DEV void wave_rows(const WgradArgs& a, int split, int wv, int64_t& r_lo, int
 
 template <int NI, int D>
 NAV_DEV void wgrad_tile_fact(const WgradArgs& a, const TileJob& t, float* smem) {
-    // the bits -> A fragment table at LDS offset 0: entry b, dword d holds bf16 2.0 in its low
-    // half when bit 2d of b is set and in its high half when bit 2d + 1 is
+    // the bits -> A fragment table at LDS offset 0: entry b, dword d holds fp16 2.0 (0x4000) in its
+    // low half when bit 2d of b is set and in its high half when bit 2d + 1 is
     uint4* tab = reinterpret_cast<uint4*>(smem);
     if (threadIdx.x < 256) {
         const uint32_t b = threadIdx.x;
@@ -689,35 +786,87 @@ struct PackInfo {
     float* packed;
 };
 
-NAV_DEV void repack(const PackInfo& pk, int64_t i, float4 v) {
-    // i = flat float index of v.x (multiple of 4): W[n][k .. k+3] of a hidden x hidden layer ->
-    // the three bf16 planes of the forward image (B[k][n], 4 consecutive j: one 8-B store per
-    // plane) and of the backward image (B[n][k + c], 4 columns)
-    for (int L = 1; L < pk.n_hidden; ++L) {
-        const int hp = pk.hp;
-        const int64_t off = pk.w_off[L], sz = (int64_t)hp * hp;
-        if (i >= off && i < off + sz) {
-            const int64_t e = i - off;
-            const int n = (int)(e / hp), k = (int)(e % hp);
-            const int64_t img = split_image_floats(hp);
-            __bf16* Wf = reinterpret_cast<__bf16*>(pk.packed + (int64_t)(L - 1) * 2 * img);
-            __bf16* Wb = reinterpret_cast<__bf16*>(pk.packed + (int64_t)(L - 1) * 2 * img + img);
-            const float x[4] = {v.x, v.y, v.z, v.w};
-            __bf16 sp[3][4];
-#pragma unroll
-            for (int c = 0; c < 4; ++c) split1(x[c], sp[0][c], sp[1][c], sp[2][c]);
-#pragma unroll
-            for (int p = 0; p < 3; ++p) {
-                typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-                bf16x4 q4;
-                q4[0] = sp[p][0]; q4[1] = sp[p][1]; q4[2] = sp[p][2]; q4[3] = sp[p][3];
-                *reinterpret_cast<bf16x4*>(Wf + split_entry(hp, p, k, n)) = q4;
-#pragma unroll
-                for (int c = 0; c < 4; ++c) Wb[split_entry(hp, p, n, k + c)] = sp[p][c];
+// The fp16 B images (mlp_common.h) of every hidden x hidden weight of up to 8 networks, rebuilt
+// from the f32 parameters after each writer (Adam, Polyak, pack). One workgroup per (network,
+// hidden layer, image, 64-column group): thread (c = t & 63, kq = t >> 6) takes column n = 64 g + c
+// and the kq-th quarter of its k range; the column's max |B| meets in LDS, every thread then
+// writes its quarter's entries (two 16-B planes per 8 k) and the kq = 0 thread the exponent e_n.
+// The forward image's column n is W_L's row n (B[k][n] = W_L[n][k], float4 reads along the row),
+// the backward image's is W_L's column n (B[k][n] = W_L[k][n], reads coalesced across lanes).
+struct PackJob {
+    const float* p;
+    PackInfo pk;
+};
+struct PackArgs {
+    PackJob j[8];
+    int n, per_net, cg;
+};
+
+template <int WHICH>
+NAV_DEV void pack_column(const float* W, int hp, int n, int k0, int kn, float* img, float* cmax) {
+    const int c = threadIdx.x & 63, kq = threadIdx.x >> 6;
+    float m = 0.f;
+    if (n < hp) {
+        for (int k = k0; k < k0 + kn; k += 4) {
+            float4 v;
+            if (WHICH == 0) {
+                v = *reinterpret_cast<const float4*>(W + (int64_t)n * hp + k);
+            } else {
+                v = make_float4(W[(int64_t)k * hp + n], W[(int64_t)(k + 1) * hp + n],
+                                W[(int64_t)(k + 2) * hp + n], W[(int64_t)(k + 3) * hp + n]);
             }
-            return;
+            m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
         }
     }
+    cmax[kq * 64 + c] = m;
+    __syncthreads();
+    if (n >= hp) return;
+    m = fmaxf(fmaxf(cmax[c], cmax[64 + c]), fmaxf(cmax[128 + c], cmax[192 + c]));
+    const int e = pow2_exp(m);
+    const float sc = ldexpf(1.f, e);
+    _Float16* h16 = reinterpret_cast<_Float16*>(img);
+    for (int k = k0; k < k0 + kn; k += 8) {
+        float v[8];
+        if (WHICH == 0) {
+            const float4 a = *reinterpret_cast<const float4*>(W + (int64_t)n * hp + k);
+            const float4 b = *reinterpret_cast<const float4*>(W + (int64_t)n * hp + k + 4);
+            v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+            v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = W[(int64_t)(k + j) * hp + n];
+        }
+        float xs[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xs[j] = v[j] * sc;
+        const Split2 sp = split2_8(xs);
+        const f16x8 ph = sp.h, pl = sp.l;
+        *reinterpret_cast<f16x8*>(h16 + split_entry(hp, 0, k, n)) = ph;
+        *reinterpret_cast<f16x8*>(h16 + split_entry(hp, 1, k, n)) = pl;
+    }
+    if (kq == 0) reinterpret_cast<int*>(img + (int64_t)hp * hp)[n] = e;
+}
+
+__global__ __launch_bounds__(kBlock) void k_pack_img(PackArgs a) {
+    __shared__ float cmax[4 * 64];
+    int b = blockIdx.x;
+    const int jn = b / a.per_net;
+    b -= jn * a.per_net;
+    const PackJob& J = a.j[jn];
+    const int hp = J.pk.hp;
+    const int g = b % a.cg;
+    b /= a.cg;
+    const int which = b & 1, L = (b >> 1) + 1;
+    if (L >= J.pk.n_hidden) return;  // workgroup-uniform
+    const float* W = J.p + J.pk.w_off[L];
+    float* img = J.pk.packed + (int64_t)(L - 1) * 2 * split_image_floats(hp) +
+                 which * split_image_floats(hp);
+    const int kn = hp / 4, k0 = (threadIdx.x >> 6) * kn;  // hp / 4: a multiple of 8
+    const int n = g * 64 + (threadIdx.x & 63);
+    if (which == 0)
+        pack_column<0>(W, hp, n, k0, kn, img, cmax);
+    else
+        pack_column<1>(W, hp, n, k0, kn, img, cmax);
 }
 
 NAV_DEV float adam1(float& p, float g, float& m, float& v, float b1w, float b2, float omb2,
@@ -743,7 +892,6 @@ struct PolyPair {
     float4* t;
     const float4* s;
     int64_t n4;
-    PackInfo pk;
 };
 struct PolyArgs {
     PolyPair q[4];
@@ -761,10 +909,8 @@ struct RedNet {
     float4* m;
     float4* v;
     float step_size, bc2s;
-    PackInfo pk;
     int nbh, nbe;
     float4* tgt;   // nullable: this net's target, soft-updated from the new parameters
-    PackInfo tpk;
 };
 
 struct RedArgs {
@@ -778,8 +924,8 @@ struct RedArgs {
     int red_blocks;
 };
 
-// Adam on the float4 of parameters at flat4 with its finished gradient g, the packed images and
-// the net's own target (when soft-updated in the launch)
+// Adam on the float4 of parameters at flat4 with its finished gradient g and the net's own
+// target (when soft-updated in the launch); the packed images follow in k_pack_img
 NAV_DEV void adam_out(const RedArgs& a, const RedNet& rn, int64_t flat4, float4 g) {
     float4 pp = rn.p[flat4], mm = rn.m[flat4], vv = rn.v[flat4];
     adam1(pp.x, g.x, mm.x, vv.x, a.b1w, a.b2, a.omb2, a.eps, rn.step_size, rn.bc2s);
@@ -789,7 +935,6 @@ NAV_DEV void adam_out(const RedArgs& a, const RedNet& rn, int64_t flat4, float4 
     rn.p[flat4] = pp;
     rn.m[flat4] = mm;
     rn.v[flat4] = vv;
-    if (rn.pk.packed) repack(rn.pk, flat4 * 4, pp);
     if (rn.tgt) {  // robot.py:309 on the parameter just stepped (k_polyak's expression)
         float4 t = rn.tgt[flat4];
         t.x = t.x * a.poly.omt + pp.x * a.poly.tau;
@@ -797,7 +942,6 @@ NAV_DEV void adam_out(const RedArgs& a, const RedNet& rn, int64_t flat4, float4 
         t.z = t.z * a.poly.omt + pp.z * a.poly.tau;
         t.w = t.w * a.poly.omt + pp.w * a.poly.tau;
         rn.tgt[flat4] = t;
-        if (rn.tpk.packed) repack(rn.tpk, flat4 * 4, t);
     }
 }
 
@@ -821,7 +965,6 @@ NAV_DEV void polyak_elem(const PolyArgs& a, int64_t i) {
     t.z = t.z * a.omt + s.z * a.tau;
     t.w = t.w * a.omt + s.w * a.tau;
     q.t[j] = t;
-    if (q.pk.packed) repack(q.pk, j * 4, t);
 }
 
 template <bool ADAM>
@@ -906,8 +1049,7 @@ __global__ __launch_bounds__(kBlock) void k_grad_reduce(RedArgs a) {
 __global__ __launch_bounds__(kBlock) void k_adam(float4* __restrict__ p,
                                                  const float4* __restrict__ g, float4* m,
                                                  float4* v, int64_t n4, float b1w, float b2,
-                                                 float omb2, float eps, float ss, float bc2s,
-                                                 PackInfo pk) {
+                                                 float omb2, float eps, float ss, float bc2s) {
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n4;
          i += (int64_t)gridDim.x * kBlock) {
         float4 pp = p[i], gg = g[i], mm = m[i], vv = v[i];
@@ -916,7 +1058,6 @@ __global__ __launch_bounds__(kBlock) void k_adam(float4* __restrict__ p,
         adam1(pp.z, gg.z, mm.z, vv.z, b1w, b2, omb2, eps, ss, bc2s);
         adam1(pp.w, gg.w, mm.w, vv.w, b1w, b2, omb2, eps, ss, bc2s);
         p[i] = pp; m[i] = mm; v[i] = vv;
-        if (pk.packed) repack(pk, i * 4, pp);
     }
 }
 
@@ -930,7 +1071,6 @@ struct AdamNet {
     float4* v;
     int64_t n4;
     float step_size, bc2s;
-    PackInfo pk;
 };
 struct AdamArgs {
     AdamNet q[2];
@@ -952,13 +1092,12 @@ __global__ __launch_bounds__(kBlock) void k_adam_multi(AdamArgs a) {
         adam1(pp.z, gg.z, mm.z, vv.z, a.b1w, a.b2, a.omb2, a.eps, q.step_size, q.bc2s);
         adam1(pp.w, gg.w, mm.w, vv.w, a.b1w, a.b2, a.omb2, a.eps, q.step_size, q.bc2s);
         q.p[j] = pp; q.m[j] = mm; q.v[j] = vv;
-        if (q.pk.packed) repack(q.pk, j * 4, pp);
     }
 }
 
 __global__ __launch_bounds__(kBlock) void k_polyak(float4* __restrict__ t,
                                                    const float4* __restrict__ s, int64_t n4,
-                                                   float omt, float tau, PackInfo pk) {
+                                                   float omt, float tau) {
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n4;
          i += (int64_t)gridDim.x * kBlock) {
         float4 a = t[i];
@@ -969,7 +1108,6 @@ __global__ __launch_bounds__(kBlock) void k_polyak(float4* __restrict__ t,
         a.z = a.z * omt + b.z * tau;
         a.w = a.w * omt + b.w * tau;
         t[i] = a;
-        if (pk.packed) repack(pk, i * 4, a);
     }
 }
 
@@ -977,13 +1115,6 @@ __global__ __launch_bounds__(kBlock) void k_polyak_multi(PolyArgs a) {
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < a.total4;
          i += (int64_t)gridDim.x * kBlock)
         polyak_elem(a, i);
-}
-
-__global__ __launch_bounds__(kBlock) void k_pack(const float4* __restrict__ p, int64_t n4,
-                                                 PackInfo pk) {
-    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n4;
-         i += (int64_t)gridDim.x * kBlock)
-        repack(pk, i * 4, p[i]);
 }
 
 // ---------------- TD3 glue ----------------
@@ -1034,6 +1165,35 @@ PackInfo pack_info(const MlpDev& d, float* packed) {
     pk.packed = d.n_hidden > 1 ? packed : nullptr;
     return pk;
 }
+
+// The networks whose packed images a launch changed; launch() rebuilds them (k_pack_img) on the
+// same stream right after the writer.
+struct PackSet {
+    PackArgs a{};
+    bool add(const nav_mlp* net) {
+        MlpDev d;
+        if (!net || !make_dev(net, &d)) return false;
+        if (d.n_hidden < 2) return true;
+        if (a.n >= 8) return false;
+        a.j[a.n].p = net->params;
+        a.j[a.n].pk = pack_info(d, net->packed);
+        ++a.n;
+        return true;
+    }
+    int launch(hipStream_t st) {
+        if (a.n == 0) return 0;
+        int hp = 0, nh = 0;
+        for (int i = 0; i < a.n; ++i) {
+            hp = a.j[i].pk.hp > hp ? a.j[i].pk.hp : hp;
+            nh = a.j[i].pk.n_hidden > nh ? a.j[i].pk.n_hidden : nh;
+        }
+        a.cg = (hp + 63) / 64;
+        a.per_net = (nh - 1) * 2 * a.cg;
+        hipLaunchKernelGGL(k_pack_img, dim3((unsigned)(a.n * a.per_net)), dim3(kBlock), 0, st, a);
+        NAV_CHECK_LAUNCH();
+        return 0;
+    }
+};
 
 bool red_net(const nav_mlp* net, const float* hs, int splits, const float* es, float* grad,
              RedNet* rn) {
@@ -1177,6 +1337,7 @@ int nav_adam_multi(const nav_mlp* nets, int32_t n_nets, const float* const* grad
                    float* const* m, float* const* v, float beta1, float beta2, float eps,
                    const float* step_size, const float* bc2_sqrt, float grad_div, void* stream) {
     AdamArgs a{};
+    PackSet ps;
     if (!nets || n_nets < 1 || n_nets > 2 || !grads || !m || !v || !step_size || !bc2_sqrt ||
         !(grad_div > 0.f))
         return NAV_EINVAL;
@@ -1191,7 +1352,7 @@ int nav_adam_multi(const nav_mlp* nets, int32_t n_nets, const float* const* grad
         q.n4 = d.count / 4;
         q.step_size = step_size[i];
         q.bc2s = bc2_sqrt[i];
-        q.pk = pack_info(d, nets[i].packed);
+        if (!ps.add(&nets[i])) return NAV_EINVAL;
         a.total4 += q.n4;
     }
     a.n = n_nets;
@@ -1203,7 +1364,7 @@ int nav_adam_multi(const nav_mlp* nets, int32_t n_nets, const float* const* grad
     hipLaunchKernelGGL(k_adam_multi, dim3(grid_stride_blocks(a.total4)), dim3(kBlock), 0,
                        S(stream), a);
     NAV_CHECK_LAUNCH();
-    return 0;
+    return ps.launch(S(stream));
 }
 
 // RedArgs of the reduce (+ Adam when m is non-NULL, + the soft updates): *blocks = the reduce
@@ -1213,7 +1374,7 @@ static int red_args(const nav_mlp* nets, int32_t n_nets, const float* const* hid
                     float* const* grads, float* const* m, float* const* v, float beta1,
                     float beta2, float eps, const float* step_size, const float* bc2_sqrt,
                     const nav_mlp* net_targets, const nav_mlp* targets, const nav_mlp* sources,
-                    int32_t n_pairs, float tau, RedArgs& a, int* blocks_out) {
+                    int32_t n_pairs, float tau, RedArgs& a, int* blocks_out, PackSet* ps) {
     const bool adam = m != nullptr;
     if (!nets || n_nets < 1 || n_nets > 2 || !hidden_slabs || !edge_slabs || edge_blocks < 1 ||
         splits < 0 || (adam && (!v || !step_size || !bc2_sqrt)) || n_pairs < 0 || n_pairs > 4 ||
@@ -1234,7 +1395,7 @@ static int red_args(const nav_mlp* nets, int32_t n_nets, const float* const* hid
             rn.v = reinterpret_cast<float4*>(v[i]);
             rn.step_size = step_size[i];
             rn.bc2s = bc2_sqrt[i];
-            rn.pk = pack_info(rn.net, nets[i].packed);
+            if (ps && !ps->add(&nets[i])) return NAV_EINVAL;
         }
         if (net_targets) {
             MlpDev dt;
@@ -1242,7 +1403,7 @@ static int red_args(const nav_mlp* nets, int32_t n_nets, const float* const* hid
                 dt.hp != rn.net.hp || dt.n_hidden != rn.net.n_hidden)
                 return NAV_EINVAL;
             rn.tgt = reinterpret_cast<float4*>(net_targets[i].params);
-            rn.tpk = pack_info(dt, net_targets[i].packed);
+            if (ps && !ps->add(&net_targets[i])) return NAV_EINVAL;
         }
         blocks += rn.nbh + rn.nbe;
     }
@@ -1254,7 +1415,7 @@ static int red_args(const nav_mlp* nets, int32_t n_nets, const float* const* hid
         a.poly.q[i].t = reinterpret_cast<float4*>(targets[i].params);
         a.poly.q[i].s = reinterpret_cast<const float4*>(sources[i].params);
         a.poly.q[i].n4 = dt.count / 4;
-        a.poly.q[i].pk = pack_info(dt, targets[i].packed);
+        if (ps && !ps->add(&targets[i])) return NAV_EINVAL;
         a.poly.total4 += a.poly.q[i].n4;
     }
     a.poly.n = n_pairs;
@@ -1280,16 +1441,17 @@ static int grad_reduce_adam_impl(const nav_mlp* nets, int32_t n_nets, const floa
                           const nav_mlp* net_targets, const nav_mlp* targets,
                           const nav_mlp* sources, int32_t n_pairs, float tau, void* stream) {
     RedArgs a{};
+    PackSet ps;
     int blocks = 0;
     if (!m) return NAV_EINVAL;
     const int rc = red_args(nets, n_nets, hidden_slabs, splits, edge_slabs, edge_blocks, grads, m,
                             v, beta1, beta2, eps, step_size, bc2_sqrt, net_targets, targets,
-                            sources, n_pairs, tau, a, &blocks);
+                            sources, n_pairs, tau, a, &blocks, &ps);
     if (rc) return rc;
     hipLaunchKernelGGL(k_grad_reduce<true>, dim3((unsigned)blocks), dim3(kBlock), 0, S(stream),
                        a);
     NAV_CHECK_LAUNCH();
-    return 0;
+    return ps.launch(S(stream));
 }
 
 int nav_grad_reduce_adam(const nav_mlp* nets, int32_t n_nets, const float* const* hidden_slabs,
@@ -1319,6 +1481,7 @@ int nav_grad_reduce_adam_polyak(const nav_mlp* nets, int32_t n_nets,
 int nav_polyak_multi(const nav_mlp* targets, const nav_mlp* sources, int32_t n, float tau,
                      void* stream) {
     PolyArgs a{};
+    PackSet ps;
     if (!targets || !sources || n < 1 || n > 4) return NAV_EINVAL;
     for (int i = 0; i < n; ++i) {
         MlpDev dt, ds;
@@ -1328,7 +1491,7 @@ int nav_polyak_multi(const nav_mlp* targets, const nav_mlp* sources, int32_t n, 
         a.q[i].t = reinterpret_cast<float4*>(targets[i].params);
         a.q[i].s = reinterpret_cast<const float4*>(sources[i].params);
         a.q[i].n4 = dt.count / 4;
-        a.q[i].pk = pack_info(dt, targets[i].packed);
+        if (!ps.add(&targets[i])) return NAV_EINVAL;
         a.total4 += a.q[i].n4;
     }
     a.n = n;
@@ -1337,7 +1500,7 @@ int nav_polyak_multi(const nav_mlp* targets, const nav_mlp* sources, int32_t n, 
     hipLaunchKernelGGL(k_polyak_multi, dim3(grid_stride_blocks(a.total4)), dim3(kBlock), 0,
                        S(stream), a);
     NAV_CHECK_LAUNCH();
-    return 0;
+    return ps.launch(S(stream));
 }
 
 int nav_adam(const nav_mlp* net, const float* grad, float* m, float* v, float beta1, float beta2,
@@ -1349,9 +1512,11 @@ int nav_adam(const nav_mlp* net, const float* grad, float* m, float* v, float be
                        reinterpret_cast<float4*>(net->params),
                        reinterpret_cast<const float4*>(grad), reinterpret_cast<float4*>(m),
                        reinterpret_cast<float4*>(v), n4, 1.0f - beta1, beta2, 1.0f - beta2, eps,
-                       step_size, bc2_sqrt, pack_info(d, net->packed));
+                       step_size, bc2_sqrt);
     NAV_CHECK_LAUNCH();
-    return 0;
+    PackSet ps;
+    ps.add(net);
+    return ps.launch(S(stream));
 }
 
 int nav_polyak(const nav_mlp* target, const nav_mlp* source, float tau, void* stream) {
@@ -1362,22 +1527,21 @@ int nav_polyak(const nav_mlp* target, const nav_mlp* source, float tau, void* st
     const int64_t n4 = dt.count / 4;
     hipLaunchKernelGGL(k_polyak, dim3(grid_stride_blocks(n4)), dim3(kBlock), 0, S(stream),
                        reinterpret_cast<float4*>(target->params),
-                       reinterpret_cast<const float4*>(source->params), n4, 1.0f - tau, tau,
-                       pack_info(dt, target->packed));
+                       reinterpret_cast<const float4*>(source->params), n4, 1.0f - tau, tau);
     NAV_CHECK_LAUNCH();
-    return 0;
+    PackSet ps;
+    ps.add(target);
+    return ps.launch(S(stream));
 }
 
 int nav_mlp_pack(const nav_mlp* net, void* stream) {
     MlpDev d;
     if (!make_dev(net, &d)) return NAV_EINVAL;
     if (d.n_hidden < 2) return 0;
-    const int64_t n4 = d.count / 4;
-    hipLaunchKernelGGL(k_pack, dim3(grid_stride_blocks(n4)), dim3(kBlock), 0, S(stream),
-                       reinterpret_cast<const float4*>(net->params), n4,
-                       pack_info(d, net->packed));
-    NAV_CHECK_LAUNCH();
-    return 0;
+    if (!net->packed) return NAV_EINVAL;
+    PackSet ps;
+    ps.add(net);
+    return ps.launch(S(stream));
 }
 
 int nav_replay_sample(const nav_replay* replay, int64_t size, int64_t B, const int64_t* idx,

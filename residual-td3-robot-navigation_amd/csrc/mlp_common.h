@@ -154,13 +154,98 @@ NAV_DEV f32x16 mfma_x6s(const Split3& a, const Split3& b, f32x16 c) {
     return mfma16(a.h, b.h, c);
 }
 
-// Split B-operand image of one hp x hp matrix B[k][n] (k = the product's K): entry
-// (plane p, k step q = k / 16, lane half h = (k / 8) & 1, column n) holds the 8 bf16 of plane p
-// of B[16q + 8h + j][n], j = 0..7 — one 16-B load per lane per plane and k step, 32 lanes of a
-// half-wave on 512 consecutive bytes. [3][hp/16][2][hp] x 8 bf16 = 1.5 hp^2 floats.
-__host__ __device__ constexpr int64_t split_image_floats(int hp) { return (int64_t)3 * hp * hp / 2; }
+// Entry (plane p, k step q = k / 16, lane half h = (k / 8) & 1, column n) of a 16-bit B-operand
+// image of one hp x hp matrix B[k][n] (k = the product's K): the 8 values of plane p of
+// B[16q + 8h + j][n], j = 0..7 — one 16-B load per lane per plane and k step, 32 lanes of a
+// half-wave on 512 consecutive bytes.
 __host__ __device__ inline int64_t split_entry(int hp, int p, int k, int n) {
     return ((((int64_t)p * (hp / 16) + (k >> 4)) * 2 + ((k >> 3) & 1)) * hp + n) * 8 + (k & 7);
+}
+
+// ---- fp32 GEMMs on the fp16 matrix cores (the row kernels' hidden x hidden products) ----
+// Both f32 operands carry a power-of-two scale and are split EXACTLY-to-22-bits into two fp16
+// planes: x 2^e = hi + lo + r, hi = fp16(x 2^e), lo = fp16(x 2^e - hi) (the remainder exact in
+// f32), |r| <= 2^-22 |x 2^e| (11 + 11 significant bits). sum_k a_k b_k is formed from the three
+// products lo.hi + hi.lo + hi.hi on v_mfma_f32_32x32x16_f16 (fp16 x fp16 is exact in the f32
+// accumulator); the dropped lo.lo is below 2^-22 |a||b|. The scales keep both planes out of fp16
+// overflow and the lo plane's absolute precision (2^-24 in scaled units, the fp16 subnormal step)
+// at 2^-37 of the operand's max: A (the LDS rows) per workgroup and GEMM, from the block's
+// max |a| that the producing epilogue publishes (publish_amax); B per column n, from the
+// column's max |b|, stored with the image. The accumulators are unscaled by ldexp(acc, -(ea +
+// e_n)), exact. Half the MFMAs of the three-plane bf16 split (six products) at a smaller error
+// (probe tools/probe/mfma_shape_probe.hip: 6.6e-7 vs 7.9e-7 relative to fp64 on uniform rows,
+// 2.7e-7 vs 3.9e-7 on dz-like rows spanning 1e-9 .. 6e-5; 99 vs 156 us per 8-layer launch).
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+
+NAV_DEV f32x16 mfma_h(f16x8 a, f16x8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+struct Split2 {
+    f16x8 h, l;
+};
+
+// acc += a . b over one 16-deep k step, the three products smallest first
+NAV_DEV f32x16 mfma_x3(const Split2& a, const f16x8 (&b)[2], f32x16 c) {
+    c = mfma_h(a.l, b[0], c);
+    c = mfma_h(a.h, b[1], c);
+    return mfma_h(a.h, b[0], c);
+}
+
+// the same with both operands split in registers: a.lo b.hi + a.hi b.lo + a.hi b.hi
+NAV_DEV f32x16 mfma_x3s(const Split2& a, const Split2& b, f32x16 c) {
+    c = mfma_h(a.l, b.h, c);
+    c = mfma_h(a.h, b.l, c);
+    return mfma_h(a.h, b.h, c);
+}
+
+// max |v| over the wave (every lane gets it)
+NAV_DEV float wave_max_abs(float v) {
+    v = fabsf(v);
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) v = fmaxf(v, __shfl_xor(v, m, 64));
+    return v;
+}
+
+// The hi plane of a split is converted ONCE and lo is formed from those very bits: without the
+// barrier the compiler may form the stored hi with v_cvt_pk_f16_f32 and rematerialise the hi
+// that lo subtracts with v_cvt_f16_f32, and the two round an fp16 tie differently (hi + lo then
+// misses x by one fp16 ulp of hi: tools/probe/cvt_probe.hip, a 7.8e-4 error at a tie).
+template <typename T>
+NAV_DEV void pin_value(T& v) {
+    asm volatile("" : "+v"(v));
+}
+
+// 8 scaled f32 values -> the two fp16 fragments
+NAV_DEV Split2 split2_8(const float (&v)[8]) {
+    Split2 s;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s.h[j] = (_Float16)v[j];
+    pin_value(s.h);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s.l[j] = (_Float16)(v[j] - (float)s.h[j]);
+    return s;
+}
+
+// Exponent e with max_abs 2^e in [2^(top-1), 2^top) (0 for max_abs 0 or not finite), clamped so
+// that 2^e and 2^-e are normal floats.
+__host__ __device__ inline int pow2_exp_to(float max_abs, int top) {
+    if (!(max_abs > 0.f) || !(max_abs < 3.0e38f)) return 0;
+    int E;
+    (void)frexpf(max_abs, &E);  // max_abs = m 2^E, m in [0.5, 1)
+    int e = top - E;
+    return e > 126 ? 126 : e < -126 ? -126 : e;
+}
+// an operand's scale: its max |x| 2^e in [2^13, 2^14), so products of two scaled operands and
+// their K-sums stay far inside f32 and both fp16 planes inside fp16's range
+__host__ __device__ inline int pow2_exp(float max_abs) { return pow2_exp_to(max_abs, 14); }
+
+// The fp16 B image of one hp x hp matrix: planes [2][hp/16][2][hp] x 8 fp16 (split_entry), then
+// the per-column exponents e_n (int32[hp]): hp^2 + hp floats.
+__host__ __device__ constexpr int64_t split_image_floats(int hp) { return (int64_t)hp * hp + hp; }
+NAV_DEV const int* image_exps(const float* image, int hp) {
+    return reinterpret_cast<const int*>(image + (int64_t)hp * hp);
 }
 
 NAV_DEV int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
@@ -221,6 +306,26 @@ __device__ unsigned long long g_phase_trace[kTraced][kBlock / 64][64];
     do {                  \
     } while (0)
 #define NAV_TICK_MK -64
+#endif
+
+// Held-clock probe (variant builds with -DNAV_CLOCK_STAMP only; tools/clock_probe.py): thread 0 of
+// each of the first kClockBlocks workgroups stamps s_memtime (shader clock) and s_memrealtime
+// (100 MHz) at the kernel's start and end; kernel ids: 0 critic_rows, 1 actor_rows, 2 the tick
+// launch. The stamps go only to this buffer (MI355X_MICROARCH.md 'DVFS give-back' 6).
+#ifdef NAV_CLOCK_STAMP
+constexpr int kClockBlocks = 1024;
+__device__ unsigned long long g_clock_stamp[3][kClockBlocks][4];
+#define NAV_CLOCK(kid, at)                                                                     \
+    do {                                                                                       \
+        if (threadIdx.x == 0 && blockIdx.y == 0 && blockIdx.x < kClockBlocks) {                \
+            g_clock_stamp[kid][blockIdx.x][2 * (at)] = __builtin_amdgcn_s_memtime();           \
+            g_clock_stamp[kid][blockIdx.x][2 * (at) + 1] = __builtin_amdgcn_s_memrealtime();   \
+        }                                                                                      \
+    } while (0)
+#else
+#define NAV_CLOCK(kid, at) \
+    do {                   \
+    } while (0)
 #endif
 
 // Mask image row-tile count: independent of the workgroup height, so any RT reads what any RT

@@ -29,25 +29,44 @@ struct WaveCols {
     NAV_DEV WaveCols(int wv) : t0(wv), t1(wv + 4), has0(NT >= 4 || wv < NT), has1(NT >= 8 || wv + 4 < NT) {}
 };
 
-// acc[rt][j] = A[TM rows][hp] (LDS f32, row stride S_) x B[hp][tile t_j] on the bf16 matrix
-// cores at f32 accuracy (mlp_common.h: three-way exact bf16 split, six partial products). Per
-// 16-deep k step the workgroup splits the step's TM x 16 A values ONCE, four per thread, into an
-// LDS stage of three bf16 planes (split_stage), and every wave reads its 16-B fragments from there
-// (before: each of the 4 waves split every A value it read — the split was ~15 % of the GEMM;
-// probe r03v: -10 %). Two barriers per step: stage written, stage read. B is the layer's split
-// image (split_entry layout) in global memory, L2-resident, its three planes loaded PF steps
-// ahead. Lane (h, l32) holds A[row l32][16q + 8h + j] and B[16q + 8h + j][col l32], j = 0..7 (the
-// 32x32x16 operand maps). Every wave runs the split and the barriers; waves without a column
-// tile (NT < 4) skip only the MFMAs.
+// Per-(32-row tile, wave) max |value| slots of the block (float[RT][kWaves], just past gemm_cols'
+// split stage): the epilogue that writes a GEMM's A rows into LDS publishes its values' max per
+// row tile here, and gemm_cols reads them (after the epilogue's barrier) for the A operand's
+// power-of-two scale of each 32-row tile. Per row tile, not per workgroup: 32- and 64-row blocks
+// then scale every row identically, so the forward stays bit-identical across block heights.
+template <int TM>
+NAV_DEV float* amax_slots(_Float16* stage);
+
+template <int RT>
+NAV_DEV void publish_amax(float* slots, const float (&m)[RT]) {
+    if (!slots) return;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+        const float v = wave_max_abs(m[rt]);
+        if ((threadIdx.x & 63) == 0) slots[rt * kWaves + (threadIdx.x >> 6)] = v;
+    }
+}
+
+// acc[rt][j] = A[TM rows][hp] (LDS f32, row stride S_) x B[hp][tile t_j] on the fp16 matrix
+// cores at f32 accuracy (mlp_common.h: power-of-two scales, two-plane fp16 split, three
+// products). Per 16-deep k step the workgroup scales and splits the step's TM x 16 A values ONCE,
+// four per thread, into an LDS stage of two fp16 planes (split_stage), and every wave reads its
+// 16-B fragments from there (before: each of the 4 waves split every A value it read — the split
+// was ~15 % of the GEMM; probe r03v: -10 %). Two barriers per step: stage written, stage read. B is
+// the layer's image (split_entry layout, per-column exponents after the planes) in global
+// memory, L2-resident, its two planes loaded PF steps ahead. Lane (h, l32) holds A[row
+// l32][16q + 8h + j] and B[16q + 8h + j][col l32], j = 0..7 (the 32x32x16 operand maps). Every wave
+// runs the split and the barriers; waves without a column tile (NT < 4) skip only the MFMAs. The
+// result is unscaled before it is returned: the callers see acc = A . B in f32.
 template <int NT, int RT>
-NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const bf16x8* __restrict__ Bs,
-                       __bf16* stage, f32x16 (&acc)[RT][2]) {
+NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const float* __restrict__ img,
+                       _Float16* stage, f32x16 (&acc)[RT][2]) {
     constexpr int hp = NT * 32;
     constexpr int nq = hp / 16;
     constexpr int TM = RT * 32;
     constexpr size_t PL = (size_t)nq * 2 * hp;  // 16-B entries per plane
     constexpr size_t STEP = 2 * (size_t)hp;     // entries per k step
-    constexpr int PP = TM * 16;                 // bf16 per stage plane
+    constexpr int PP = TM * 16;                 // fp16 per stage plane
     const int tid = threadIdx.x, lane = tid & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
     const WaveCols<NT> wc(wv);
 #pragma unroll
@@ -60,22 +79,33 @@ NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const bf16x8* __rest
     // is unconditional; its second-tile MFMAs are skipped by a scalar branch (a wave without any
     // tile reads tile 0's and issues none).
     const int t0 = wc.has0 ? wc.t0 : 0, t1 = wc.has1 ? wc.t1 : t0;
+    // the scales: A's per 32-row tile from the producing epilogue's published maxima, B's per
+    // column (in flight under the whole product)
+    const float* slots = amax_slots<TM>(stage);
+    int ea[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+        const float* sl = slots + rt * kWaves;
+        ea[rt] = pow2_exp(fmaxf(fmaxf(sl[0], sl[1]), fmaxf(sl[2], sl[3])));
+    }
+    const int* ex = image_exps(img, hp);
+    const int eb0 = ex[t0 * 32 + l32], eb1 = ex[t1 * 32 + l32];
     // B entries as the uniform image base + a 32-bit per-lane byte offset (SGPR base + VGPR
     // offset addressing: one 32-bit add per load instead of a 64-bit address pair)
-    const char* Bb = reinterpret_cast<const char*>(Bs);
+    const char* Bb = reinterpret_cast<const char*>(img);
     const uint32_t o0 = (uint32_t)(h * hp + t0 * 32 + l32) * 16u;
     const uint32_t o1 = (uint32_t)(h * hp + t1 * 32 + l32) * 16u;
     auto ldB = [&](uint32_t o, int p, int q) {
-        return *reinterpret_cast<const bf16x8*>(Bb + (o + (uint32_t)((p * PL + q * STEP) * 16)));
+        return *reinterpret_cast<const f16x8*>(Bb + (o + (uint32_t)((p * PL + q * STEP) * 16)));
     };
     // B planes PF steps ahead: one step for 64-row blocks (the register budget of the big row
-    // kernels), two for 32-row blocks, whose step (12 MFMAs per wave) is shorter than an L2 hit
+    // kernels), two for 32-row blocks, whose step (6 MFMAs per wave) is shorter than an L2 hit
     constexpr int PF = RT == 1 ? 2 : 1;
-    bf16x8 bq0[PF + 1][3], bq1[PF + 1][3];
+    f16x8 bq0[PF + 1][2], bq1[PF + 1][2];
 #pragma unroll
     for (int d = 0; d < PF; ++d)
 #pragma unroll
-        for (int p = 0; p < 3; ++p) {
+        for (int p = 0; p < 2; ++p) {
             const int qd = d < nq ? d : nq - 1;
             bq0[d][p] = ldB(o0, p, qd);
             bq1[d][p] = ldB(o1, p, qd);
@@ -87,32 +117,29 @@ NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const bf16x8* __rest
     const bool sp = TM * 4 >= kBlock || tid < TM * 4;
     const int sr = tid >> 2, sk = (tid & 3) * 4;
     const float* src = A + sr * S_ + sk;
-    __bf16* dst = stage + sr * 16 + ((((sk >> 3) ^ (sr >> 3)) & 1) << 3) + (sk & 7);
-    const __bf16* frag = stage + l32 * 16 + (((h ^ (l32 >> 3)) & 1) << 3);
+    _Float16* dst = stage + sr * 16 + ((((sk >> 3) ^ (sr >> 3)) & 1) << 3) + (sk & 7);
+    const _Float16* frag = stage + l32 * 16 + (((h ^ (l32 >> 3)) & 1) << 3);
     float4 x = sp ? *reinterpret_cast<const float4*>(src) : make_float4(0.f, 0.f, 0.f, 0.f);
-    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-    // split of step q's share (x) into the stage, the next x from the LDS rows, B planes ahead
-    // 32-row blocks (small batches: latency-bound, one wave per SIMD) double-buffer the stage and
-    // pass one barrier per step: step q + 1's stores go to the buffer step q - 1 was read from,
-    // which every wave finished reading (and consumed in its MFMAs) before step q's barrier
+    const float sa = ldexpf(1.f, RT == 1 ? ea[0] : ea[(sr >> 5) < RT ? (sr >> 5) : RT - 1]);
+    // scale + split of step q's share (x) into the stage, the next x from the LDS rows, B planes
+    // ahead. 32-row blocks (small batches: latency-bound, one wave per SIMD) double-buffer the
+    // stage and pass one barrier per step: step q + 1's stores go to the buffer step q - 1 was
+    // read from, which every wave finished reading (and consumed in its MFMAs) before step q's
+    // barrier
     constexpr bool DB = RT == 1 && kStageDb1;
-    constexpr int SB = 3 * PP;  // bf16 per stage buffer
+    constexpr int SB = 2 * PP;  // fp16 per stage buffer
     auto produce = [&](int q) {
         if (sp) {
-            __bf16* const dq = dst + (DB ? (q & 1) * SB : 0);
-            const float v[4] = {x.x, x.y, x.z, x.w};
-            bf16x4 ph, pm, pl;
+            _Float16* const dq = dst + (DB ? (q & 1) * SB : 0);
+            const float v[4] = {x.x * sa, x.y * sa, x.z * sa, x.w * sa};
+            f16x4 ph, pl;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                __bf16 hh, mm, ll;
-                split1(v[j], hh, mm, ll);
-                ph[j] = hh;
-                pm[j] = mm;
-                pl[j] = ll;
-            }
-            *reinterpret_cast<bf16x4*>(dq) = ph;
-            *reinterpret_cast<bf16x4*>(dq + PP) = pm;
-            *reinterpret_cast<bf16x4*>(dq + 2 * PP) = pl;
+            for (int j = 0; j < 4; ++j) ph[j] = (_Float16)v[j];
+            pin_value(ph);  // lo from the stored hi's bits (mlp_common.h)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) pl[j] = (_Float16)(v[j] - (float)ph[j]);
+            *reinterpret_cast<f16x4*>(dq) = ph;
+            *reinterpret_cast<f16x4*>(dq + PP) = pl;
             if (q + 1 < nq) x = *reinterpret_cast<const float4*>(src + 16 * (q + 1));
         }
         // production of step q runs during step q - 1's MFMAs: the B planes loaded here are
@@ -120,65 +147,74 @@ NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const bf16x8* __rest
         const int qb = q - 1 + PF;
         if (q >= 1 && qb < nq) {
 #pragma unroll
-            for (int p = 0; p < 3; ++p) {
+            for (int p = 0; p < 2; ++p) {
                 bq0[qb % (PF + 1)][p] = ldB(o0, p, qb);
                 bq1[qb % (PF + 1)][p] = ldB(o1, p, qb);
             }
         }
     };
-    Split3 sa[RT];
+    Split2 sa2[RT];
     // two barriers per step (one buffer): the stage is written, then read (the next step may
     // overwrite it); one barrier with the double buffer
     auto consume = [&](int q) {
         __syncthreads();
-        const __bf16* fq = frag + (DB ? (q & 1) * SB : 0);
+        const _Float16* fq = frag + (DB ? (q & 1) * SB : 0);
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) {
-            const __bf16* f = fq + rt * 32 * 16;
-            sa[rt].h = *reinterpret_cast<const bf16x8*>(f);
-            sa[rt].m = *reinterpret_cast<const bf16x8*>(f + PP);
-            sa[rt].l = *reinterpret_cast<const bf16x8*>(f + 2 * PP);
+            const _Float16* f = fq + rt * 32 * 16;
+            sa2[rt].h = *reinterpret_cast<const f16x8*>(f);
+            sa2[rt].l = *reinterpret_cast<const f16x8*>(f + PP);
         }
         if (!DB) __syncthreads();
     };
     produce(0);
     consume(0);
-    // Two workgroups share a CU at the bench shapes (blocks b and b + #CUs, dispatched together),
+    // Two workgroups share a CU at the bench shapes (blocks b and b + kCUs, dispatched together),
     // and at equal priority the SIMD arbiter issues the older wave first: the second workgroup's
     // GEMMs lag and it ends its last ~50 k cycles alone at the lone-workgroup MFMA rate (critic_rows:
-    // 247 k vs 297 k cycles). The upper half of the grid raises its wave priority inside its GEMMs,
-    // which balances the pair (270 k / 267 k; critic_rows 161.6 -> 153.5 us, profiles/r04y, r04z).
-    const bool favored = blockIdx.x >= (gridDim.x >> 1);
+    // 247 k vs 297 k cycles). The younger partner of each pair (odd multiples of kCUs) raises its
+    // wave priority inside its GEMMs, which balances the pair (270 k / 267 k; critic_rows 161.6 ->
+    // 153.5 us, profiles/r04y, r04z). At a 512-block grid this is the grid's upper half.
+    const bool favored = (blockIdx.x / kCUs) & 1;
     if (favored) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int q = 0; q < nq; ++q) {
         // step q + 1's production comes first in program order, so the scheduler can place it
         // between step q's MFMAs (its stage stores follow step q's second barrier)
         if (q + 1 < nq) produce(q + 1);
-        Split3 cur[RT];
+        Split2 cur[RT];
 #pragma unroll
-        for (int rt = 0; rt < RT; ++rt) cur[rt] = sa[rt];
+        for (int rt = 0; rt < RT; ++rt) cur[rt] = sa2[rt];
         if (wc.has0) {  // wave-uniform
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt) {
-                acc[rt][0] = mfma_x6(cur[rt], bq0[q % (PF + 1)], acc[rt][0]);
+                acc[rt][0] = mfma_x3(cur[rt], bq0[q % (PF + 1)], acc[rt][0]);
                 if (NT >= 8 || wc.has1)
-                    acc[rt][1] = mfma_x6(cur[rt], bq1[q % (PF + 1)], acc[rt][1]);
+                    acc[rt][1] = mfma_x3(cur[rt], bq1[q % (PF + 1)], acc[rt][1]);
             }
         }
         if (q + 1 < nq) consume(q + 1);
     }
     if (favored) __builtin_amdgcn_s_setprio(0);
+    // unscale: acc 2^-(ea[rt] + e_n), exact (v_ldexp_f32)
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+        const int u0 = -(ea[rt] + eb0), u1 = -(ea[rt] + eb1);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            acc[rt][0][i] = ldexpf(acc[rt][0][i], u0);
+            acc[rt][1][i] = ldexpf(acc[rt][1][i], u1);
+        }
+    }
 }
 
-// the split B images of hidden layer L (1 .. n_hidden-1): forward (B[k][n] = W_L[n][k]) and
+// the fp16 B images of hidden layer L (1 .. n_hidden-1): forward (B[k][n] = W_L[n][k]) and
 // backward (B[k][n] = W_L[k][n])
-NAV_DEV const bf16x8* img_fwd(const MlpDev& net, int L) {
-    return reinterpret_cast<const bf16x8*>(net.packed + (int64_t)(L - 1) * 2 * split_image_floats(net.hp));
+NAV_DEV const float* img_fwd(const MlpDev& net, int L) {
+    return net.packed + (int64_t)(L - 1) * 2 * split_image_floats(net.hp);
 }
-NAV_DEV const bf16x8* img_bwd(const MlpDev& net, int L) {
-    return reinterpret_cast<const bf16x8*>(net.packed + (int64_t)(L - 1) * 2 * split_image_floats(net.hp) +
-                                           split_image_floats(net.hp));
+NAV_DEV const float* img_bwd(const MlpDev& net, int L) {
+    return net.packed + (int64_t)(L - 1) * 2 * split_image_floats(net.hp) + split_image_floats(net.hp);
 }
 
 enum { IN_F32 = 0, IN_BASELINE = 1 };
@@ -232,9 +268,17 @@ struct FwdArgs {
 // Output-layer partial sums: [d_out <= 2][4 waves][TM rows] (red_floats per block).
 __host__ __device__ constexpr int red_floats(int tm) { return 2 * kWaves * tm; }
 
-// bytes of gemm_cols' split stage for TM rows: [3 planes][TM][16] bf16
+// bytes of gemm_cols' split stage for TM rows: [2 planes][TM][16] fp16 (two buffers for 32-row
+// blocks), then the kWaves amax slots
+__host__ __device__ constexpr size_t stage_halves(int tm) {
+    return (size_t)(tm == 32 && kStageDb1 ? 2 : 1) * 2 * tm * 16;
+}
 __host__ __device__ constexpr size_t stage_bytes(int tm) {
-    return (size_t)(tm == 32 && kStageDb1 ? 2 : 1) * 3 * tm * 16 * 2;
+    return stage_halves(tm) * 2 + 4 * kWaves * (tm / 32);
+}
+template <int TM>
+NAV_DEV float* amax_slots(_Float16* stage) {
+    return reinterpret_cast<float*>(stage + stage_halves(TM));
 }
 
 // rows [tm][hp+4] + input/dy staging [tm][4] + output-layer partial sums, then the split stage
@@ -245,11 +289,14 @@ inline size_t lds_bytes(int hp, int tm) { return lds_floats(hp, tm) * 4 + stage_
 
 
 // Store a layer's C-layout result into the LDS rows (the next layer's A operand) and its ReLU
-// mask bits. Global copies of the rows are written afterwards by copy_rows (coalesced).
+// mask bits; with slots, publish the rows' max |value| for the next GEMM's A scale. Global copies
+// of the rows are written afterwards by copy_rows (coalesced).
 template <int NT, int RT>
-NAV_DEV void store_layer(f32x16 (&acc)[RT][2], float* act, int S_, uint16_t* mask, int64_t rt0) {
+NAV_DEV void store_layer(f32x16 (&acc)[RT][2], float* act, int S_, uint16_t* mask, int64_t rt0,
+                         float* slots = nullptr) {
     const int lane = threadIdx.x & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
     const WaveCols<NT> wc(wv);
+    float m[RT] = {};
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
         if (!(j == 0 ? wc.has0 : wc.has1)) continue;
@@ -263,10 +310,12 @@ NAV_DEV void store_layer(f32x16 (&acc)[RT][2], float* act, int S_, uint16_t* mas
                 const float v = acc[rt][j][i];
                 col[(rt * 32 + (i & 3) + 8 * (i >> 2)) * S_] = v;
                 bits |= (v > 0.f ? 1u : 0u) << i;
+                m[rt] = fmaxf(m[rt], v);  // post-ReLU: v >= 0
             }
             if (mask) mask[mask_idx(rt0 + rt, NT, t, lane)] = (uint16_t)bits;
         }
     }
+    publish_amax(slots, m);
 }
 
 // 128 LDS rows -> global [M][hp] rows row0.., float4 per lane (1 KiB per wave instruction).
@@ -546,7 +595,7 @@ NAV_DEV L0Pre load_l0(const MlpDev& net) {
 // for its global copy — and the output layer's per-wave partials land in `red` (ready for out_y
 // after the trailing barrier).
 template <int NT, int RT>
-NAV_DEV void fwd_net(const MlpDev& net, float* act, __bf16* stage, const float* xin, float* red,
+NAV_DEV void fwd_net(const MlpDev& net, float* act, _Float16* stage, const float* xin, float* red,
                      uint16_t* masks, int64_t n_rt, float* act_save, uint32_t save_mask,
                      int64_t row0, int64_t M, int64_t rt0, f32x16 (&top)[RT][2], int mk = -64,
                      const L0Pre* pre = nullptr, uint32_t* top_bits = nullptr,
@@ -567,6 +616,7 @@ NAV_DEV void fwd_net(const MlpDev& net, float* act, __bf16* stage, const float* 
     {
         const L0Pre l0 = pre ? *pre : load_l0<NT>(net);
         const f32x16 zero = {};
+        float m0[RT] = {};
         const float one = h == 0 ? 1.f : 0.f;
         // A operands: row l32 of each row tile, inputs h and 2 + h
         float xa[RT], xb[RT];
@@ -594,10 +644,12 @@ NAV_DEV void fwd_net(const MlpDev& net, float* act, __bf16* stage, const float* 
                     const float r = fmaxf(v[i], 0.f);
                     col[(rt * 32 + (i & 3) + 8 * (i >> 2)) * SS] = r;
                     bits |= (r > 0.f ? 1u : 0u) << i;
+                    m0[rt] = fmaxf(m0[rt], r);
                 }
                 if (masks) masks[mask_idx(rt0 + rt, NT, t, lane)] = (uint16_t)bits;
             }
         }
+        if (nh >= 2) publish_amax(amax_slots<RT * 32>(stage), m0);  // layer 1's A scale
     }
     NAV_MARK(mk + 1);
     __syncthreads();
@@ -626,7 +678,7 @@ NAV_DEV void fwd_net(const MlpDev& net, float* act, __bf16* stage, const float* 
         f32x16 acc[RT][2];
         hidden_layer(L, acc);
         __syncthreads();  // every wave has finished reading the layer's input rows
-        store_layer<NT, RT>(acc, act, SS, mask_of(L), rt0);
+        store_layer<NT, RT>(acc, act, SS, mask_of(L), rt0, amax_slots<RT * 32>(stage));
         __syncthreads();
         if (act_save && ((save_mask >> L) & 1u))
             copy_rows<NT, RT>(act, SS, act_save + (int64_t)L * M * hp, row0, M);
@@ -694,10 +746,11 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
     const int64_t n_rt = mask_rowtiles(M);
     float* act = smem;
     float* xin = smem + TM * SS;  // [TM][4]
-    __bf16* stage = reinterpret_cast<__bf16*>(smem + lds_floats(hp, TM));
+    _Float16* stage = reinterpret_cast<_Float16*>(smem + lds_floats(hp, TM));
     const int d_in = net.d_in, d_out = net.d_out;
     // layer 0's per-lane weights and bias: issued first, in flight under the input rows' loads
     const L0Pre l0 = load_l0<NT>(net);
+    if constexpr (OUT_MODE == OUT_TICK) NAV_CLOCK(2, 0);
 
     // ---- input rows -> xin
     if (tid < TM) {
@@ -800,6 +853,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
         if (tid < TM && a.sout.block_stats && row0 + (tid & ~63) < M)
             wave_stats(st, a.sout.block_stats, r);
         NAV_TRACE_MARK(NAV_TICK_MK + 9);
+        NAV_CLOCK(2, 1);
         return;
     }
     if (r >= M || j >= d_out) return;
@@ -950,12 +1004,14 @@ NAV_DEV void mask_regs(f32x16 (&acc)[RT][2], const uint32_t (&mbits)[RT][2]) {
     }
 }
 
-// Masks the layer's dz registers in place (ReLU derivative bits) and stores them to the LDS rows.
+// Masks the layer's dz registers in place (ReLU derivative bits) and stores them to the LDS rows;
+// with slots, publishes their max |value| for the next GEMM's A scale.
 template <int NT, int RT>
 NAV_DEV void mask_and_store(f32x16 (&acc)[RT][2], const uint32_t (&mbits)[RT][2], float* act,
-                            int S_) {
+                            int S_, float* slots = nullptr) {
     const int lane = threadIdx.x & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
     const WaveCols<NT> wc(wv);
+    float m[RT] = {};
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
         if (!(j == 0 ? wc.has0 : wc.has1)) {
@@ -974,9 +1030,11 @@ NAV_DEV void mask_and_store(f32x16 (&acc)[RT][2], const uint32_t (&mbits)[RT][2]
             for (int i = 0; i < 16; ++i) {
                 acc[rt][j][i] = (bits >> i) & 1u ? acc[rt][j][i] : 0.f;
                 col[(rt * 32 + (i & 3) + 8 * (i >> 2)) * S_] = acc[rt][j][i];
+                m[rt] = fmaxf(m[rt], fabsf(acc[rt][j][i]));
             }
         }
     }
+    publish_amax(slots, m);
 }
 
 // One network's row backward over the block's TM rows: dy rows in dys [TM][4] (LDS, ready), the
@@ -984,7 +1042,7 @@ NAV_DEV void mask_and_store(f32x16 (&acc)[RT][2], const uint32_t (&mbits)[RT][2]
 // partials (every bias, dW0 from the input rows xin [TM][4], and dWo / dbo when h_top [M][hp] is
 // given); dz_L rows to dz for save_mask bits.
 template <int NT, int RT>
-NAV_DEV void bwd_net(const MlpDev& net, float* act, __bf16* stage, const float* dys, const float* xin,
+NAV_DEV void bwd_net(const MlpDev& net, float* act, _Float16* stage, const float* dys, const float* xin,
                      const uint16_t* masks, int64_t n_rt, float* es, const float* h_top,
                      float* dz, uint32_t save_mask, int64_t row0, int64_t M, int64_t rt0,
                      int mk = -64, const uint32_t* top_bits = nullptr,
@@ -1061,7 +1119,7 @@ NAV_DEV void bwd_net(const MlpDev& net, float* act, __bf16* stage, const float* 
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt) z[rt][j] = mfma(ga[rt], wb, zero);
         }
-        mask_and_store<NT, RT>(z, mb, act, SS);
+        mask_and_store<NT, RT>(z, mb, act, SS, nh > 1 ? amax_slots<TM>(stage) : nullptr);
         if (es && nh > 1) edge_regs<NT, RT>(net, z, xin, nh - 1, es);
     }
     NAV_MARK(mk + 1);
@@ -1090,7 +1148,7 @@ NAV_DEV void bwd_net(const MlpDev& net, float* act, __bf16* stage, const float* 
         // layer 0's rows only when a reader follows (the caller's dx, the save copy); its edge
         // partials come from the registers
         if (L > 1 || dz0_rows || (save_mask & 1u))
-            mask_and_store<NT, RT>(acc, mbits, act, SS);
+            mask_and_store<NT, RT>(acc, mbits, act, SS, L > 1 ? amax_slots<TM>(stage) : nullptr);
         else
             mask_regs<NT, RT>(acc, mbits);
         if (es) edge_regs<NT, RT>(net, acc, xin, L - 1, es);
@@ -1125,7 +1183,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_bwd(BwdArgs a) {
     const int64_t rt0 = (int64_t)blockIdx.x * RT;
     const int64_t n_rt = mask_rowtiles(M);
     float* act = smem;
-    __bf16* stage = reinterpret_cast<__bf16*>(smem + lds_floats(hp, TM));
+    _Float16* stage = reinterpret_cast<_Float16*>(smem + lds_floats(hp, TM));
     float* dys = smem + TM * SS;  // [TM][4] dy rows
     float* xin = dys + TM * 4;    // [TM][4] forward input rows (dW0), inside the red scratch
     const int d_in = net.d_in, d_out = net.d_out;
@@ -1220,8 +1278,9 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
     float* brow = red + red_floats(TM);  // [TM][8] the sampled replay rows
     float* qv = brow + TM * 8;     // [TM] q1'
     float* dys = qv + TM;          // [TM][4] dL/dq rows of the row backward
-    __bf16* stage = reinterpret_cast<__bf16*>(dys + TM * 4);  // gemm_cols' split stage
+    _Float16* stage = reinterpret_cast<_Float16*>(dys + TM * 4);  // gemm_cols' split stage
     NAV_MARK(0);
+    NAV_CLOCK(0, 0);
     const L0Pre l0_at = load_l0<NT>(a.actor_t);  // in flight under the sampling
     // the sampled replay row of thread tid < TM: its gather is issued first, so it is in flight
     // while the smoothing noise below is formed
@@ -1323,6 +1382,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
         }
         NAV_MARK(35 + 14 * q);
     }
+    NAV_CLOCK(0, 1);
 }
 
 struct ActorRowsArgs {
@@ -1362,8 +1422,9 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_actor_rows(ActorRowsArgs a) {
     float* red = xin + TM * 4;       // [2][PARTS][TM]
     float* dys = red + red_floats(TM);  // [TM][4] critic dy
     float* dys2 = dys + TM * 4;      // [TM][4] actor dy = dL/da
-    __bf16* stage = reinterpret_cast<__bf16*>(dys2 + TM * 4);  // gemm_cols' split stage
+    _Float16* stage = reinterpret_cast<_Float16*>(dys2 + TM * 4);  // gemm_cols' split stage
     const L0Pre l0_a = load_l0<NT>(a.actor);  // in flight under the sampling
+    NAV_CLOCK(1, 0);
     if (tid < TM) {
         const int64_t b = row0 + tid;
         float4 lo = make_float4(0.f, 0.f, 0.f, 0.f), hi = lo;
@@ -1422,6 +1483,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_actor_rows(ActorRowsArgs a) {
     }
     bwd_net<NT, RT>(a.actor, act, stage, dys2, xin, a.masks_a, n_rt, es, nullptr, a.dz, a.dz_save_mask,
                     row0, B, rt0, -64, nullptr, nullptr, false);
+    NAV_CLOCK(1, 1);
 }
 
 
@@ -1546,6 +1608,15 @@ extern "C" int nav_phase_trace_read(unsigned long long* host, int n) {
     const size_t bytes = sizeof(g_phase_trace);
     if (!host || (size_t)n * sizeof(unsigned long long) < bytes) return NAV_EINVAL;
     const hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(g_phase_trace), bytes);
+    return e == hipSuccess ? 0 : -(int)e;
+}
+#endif
+
+#if defined(NAV_CLOCK_STAMP) && NAV_MLP_PART == 8
+extern "C" int nav_clock_stamp_read(unsigned long long* host, int n) {
+    const size_t bytes = sizeof(g_clock_stamp);
+    if (!host || (size_t)n * sizeof(unsigned long long) < bytes) return NAV_EINVAL;
+    const hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(g_clock_stamp), bytes);
     return e == hipSuccess ? 0 : -(int)e;
 }
 #endif

@@ -12,6 +12,9 @@
 namespace nav {
 
 constexpr int kBlock = 256;
+// MI355X: 256 CUs (8 XCDs x 32). A grid's first 2 x kCUs workgroups are dispatched as co-resident
+// pairs (b, b + kCUs) on one CU (profiles/r04x wide phase trace).
+constexpr int kCUs = 256;
 
 // Philox4x32-10 (Salmon et al. 2011); key (k0,k1), counter (c0..c3).
 NAV_DEV uint4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,

@@ -10,10 +10,10 @@ import os
 import torch  # noqa: F401  (must be loaded first: provides the HIP runtime)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# NAV_LIB: load another build of the same ABI instead (A/B timing of kernel variants only)
-LIB_PATH = os.environ.get("NAV_LIB") or os.path.join(HERE, "libnavenv.so")
+LIB_PATH = os.path.join(HERE, "libnavenv.so")
+_lib_path = LIB_PATH
 NAV_EINVAL = -100000
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 _dp = C.POINTER(C.c_double)
 _vp = C.c_void_p
@@ -69,7 +69,7 @@ SIGNATURES = [
     ("nav_agent_step", C.c_int, [_P(NavParams), _P(NavEnvSoa), _vp, _vp, _P(NavReplay),
                                  C.c_int64, _P(NavStepOut), C.c_int32, _vp]),
     ("nav_demo_reward", C.c_int, [_P(NavParams), C.c_int64, _vp, _vp, _vp, _vp, _vp, C.c_int64,
-                                  C.c_int32, _P(NavReplay), C.c_int64, _vp, _vp]),
+                                  C.c_int32, _P(NavReplay), C.c_int64, _vp, _vp, _vp]),
     ("nav_transition", C.c_int, [_P(NavParams), _P(NavEnvSoa), _vp, _vp, _vp, _P(NavReplay),
                                  C.c_int64, _P(NavStepOut), C.c_int32, _vp]),
     ("nav_check_if_stuck", C.c_int, [_P(NavParams), _P(NavEnvSoa), _vp, _vp, _vp]),
@@ -92,7 +92,7 @@ SIGNATURES = [
     ("nav_demo_index_subfill", C.c_int, [_vp, _vp, C.c_int32, _vp, _vp, _vp, _vp, _vp, _vp]),
     ("nav_demo_reward_indexed", C.c_int, [_P(NavParams), C.c_int64, _vp, _vp, _vp, _vp, _vp,
                                           C.c_int32, _vp, _vp, _P(NavReplay), C.c_int64, _vp,
-                                          _vp]),
+                                          _vp, _vp]),
     ("nav_agent_step_indexed", C.c_int, [_P(NavParams), _P(NavEnvSoa), _vp, _vp, _P(NavReplay),
                                          C.c_int64, _P(NavStepOut), _vp, _vp, C.c_int32, _vp,
                                          _vp, _vp, _vp]),
@@ -188,7 +188,7 @@ class _Checked:
 
 
 class _Lib:
-    def __init__(self, path=LIB_PATH):
+    def __init__(self, path):
         if not os.path.exists(path):
             raise NavError(f"{path} is missing: build it with `make -C "
                            f"residual-td3-robot-navigation_amd` (or __graft_entry__.build())")
@@ -209,8 +209,24 @@ _lib = None
 def lib():
     global _lib
     if _lib is None:
-        _lib = _Lib()
+        _lib = _Lib(_lib_path)
     return _lib
+
+
+def lib_path():
+    """The library this process binds (libnavenv.so next to this file unless a tuning tool chose
+    another build through use_library)."""
+    return _lib_path
+
+
+def use_library(path):
+    """Bind another build of the same ABI instead of the in-tree libnavenv.so. For the A/B timing
+    tools only (tools/withlib.py); must run before the first call into the library."""
+    global _lib_path
+    path = os.path.abspath(path)
+    if _lib is not None and path != _lib_path:
+        raise NavError(f"libnavenv is already loaded from {_lib_path}")
+    _lib_path = path
 
 
 def require_gpu():

@@ -129,6 +129,7 @@ class TD3(_GpuTD3):
         c.batch_size, c.gamma, c.tau = B, self.gamma, self.tau
         c.policy_noise, c.noise_clip = self.policy_noise, self.noise_clip
         c.policy_update_delay, c.num_epochs = self.policy_update_delay, self.num_epochs
+        c.max_action = self.max_action  # robot.py:339's clamp
         L = len(replay_buffer)
         n_idx = self.num_epochs + (self.num_epochs + self.policy_update_delay - 1) // \
             self.policy_update_delay
@@ -309,7 +310,7 @@ class Robot:
         if has_demo:
             lib().nav_demo_reward(C.byref(self._p), 1, ptr(self._ns_out), ptr(self._gterm),
                                   ptr(self._flags), ptr(self._demo), None, self._demo.shape[0],
-                                  1, C.byref(rd), base, None, s)
+                                  1, C.byref(rd), base, None, None, s)
         self.memory.advance(1)
         meta = int(self._meta.item())
         self.goal_reached = bool(meta & 1)

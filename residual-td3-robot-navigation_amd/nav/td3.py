@@ -6,7 +6,6 @@ provides the stream. Sampling: robot.py:98-115 draws `batch_size` rows without r
 <=10 000-row buffer; here rows are drawn with replacement by Philox (NAV_TAG_SAMPLE) from the
 device ring, or taken from an injected index tensor (parity tests, the N=1 drop-in).
 """
-import contextlib
 import ctypes as C
 import math
 
@@ -160,11 +159,7 @@ class TD3:
                           (4 if adam else 1) * x.count) for x, e in zip(nets, eslabs))
 
     def _hook_and_adam(self, nets, opts, grads, s, stream, soft_update):
-        bucket = self.grad_c if len(nets) == 2 else grads[0]
-        # the collective runs on torch's current stream: make it the launch stream, so it
-        # starts after the reduce and Adam starts after it
-        with torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext():
-            self.grad_hook(bucket)
+        self._hook(self.grad_c if len(nets) == 2 else grads[0], stream)
         self._adam(nets, opts, grads, s, self.grad_div)
         if soft_update:
             self.soft_update_all(stream)
@@ -223,7 +218,7 @@ class TD3:
     # ---- the per-epoch launches with their constant arguments built once (the small-batch
     # learner of config 1 is bound by the host's issue of ~450 launches per td3_update)
     def _fast(self):
-        return prof._active is None and self.grad_hook is None and self.row_backward
+        return prof._active is None and self.row_backward
 
     def _static_key(self):
         c = self.cfg
@@ -273,6 +268,19 @@ class TD3:
         st["poly"] = (descs(self.target_actor),
                       descs(self.target_critic_network_1, self.target_critic_network_2),
                       descs(c1, c2), 2, c.tau)
+        # shared policy (grad_hook): reduce into the flat bucket, the hook's collective, then the
+        # multi-net Adam on bucket / world_size and (policy epoch) the three soft updates
+        st["redm_c"] = (descs(c1, c2), 2, parr(self.hslab, self.hslab2), self.splits_c,
+                        parr(self.eslab1, self.eslab2), self.nblk, parr(self.grad_c1, self.grad_c2))
+        st["adam_c"] = (descs(c1, c2), 2, parr(self.grad_c1, self.grad_c2),
+                        parr(*[o.m for o in oc]), parr(*[o.v for o in oc]), oc[0].b1, oc[0].b2,
+                        oc[0].eps)
+        st["redm_a"] = (descs(a), 1, parr(self.hslab), self.splits_a, parr(self.eslab_a),
+                        self.nblk, parr(self.grad_a))
+        st["adam_a"] = (descs(a), 1, parr(self.grad_a), parr(oa.m), parr(oa.v), oa.b1, oa.b2,
+                        oa.eps)
+        st["poly3"] = (descs(self.target_actor, self.target_critic_network_1,
+                             self.target_critic_network_2), descs(a, c1, c2), 3, c.tau)
         st["wgrad"] = c1.n_hidden > 1
         self._st, self._st_key = st, key
         return st
@@ -283,7 +291,16 @@ class TD3:
             self._rd = (replay, (d, C.byref(d)))
         return self._rd[1][1]
 
-    def _critic_epoch_fast(self, replay, idx, eps, s):
+    def _hook(self, bucket, stream):
+        # the collective runs on torch's current stream: make it the launch stream, so it starts
+        # after the reduce and Adam starts after it
+        if stream is None:
+            self.grad_hook(bucket)
+        else:
+            with torch.cuda.stream(stream):
+                self.grad_hook(bucket)
+
+    def _critic_epoch_fast(self, replay, idx, eps, s, stream):
         c = self.cfg
         B = c.batch_size
         self._workspace(B)
@@ -296,10 +313,15 @@ class TD3:
         if st["wgrad"]:
             L.nav_mlp_wgrad(*st["wg_c"], s)
         o1, o2 = self.critic_optimizer_1.advance(), self.critic_optimizer_2.advance()
-        L.nav_grad_reduce_adam(*st["red_c"], (C.c_float * 2)(o1[0], o2[0]),
-                               (C.c_float * 2)(o1[1], o2[1]), s)
+        ss, bc = (C.c_float * 2)(o1[0], o2[0]), (C.c_float * 2)(o1[1], o2[1])
+        if self.grad_hook is None:
+            L.nav_grad_reduce_adam(*st["red_c"], ss, bc, s)
+            return
+        L.nav_grad_reduce_multi(*st["redm_c"], s)
+        self._hook(self.grad_c, stream)
+        L.nav_adam_multi(*st["adam_c"], ss, bc, self.grad_div, s)
 
-    def _actor_epoch_fast(self, replay, idx, s, soft_update):
+    def _actor_epoch_fast(self, replay, idx, s, stream, soft_update):
         c = self.cfg
         B = c.batch_size
         self._workspace(B)
@@ -311,7 +333,13 @@ class TD3:
             L.nav_mlp_wgrad(*st["wg_a"], s)
         o = self.actor_optimizer.advance()
         ss, bc = (C.c_float * 1)(o[0]), (C.c_float * 1)(o[1])
-        if soft_update:
+        if self.grad_hook is not None:
+            L.nav_grad_reduce_multi(*st["redm_a"], s)
+            self._hook(self.grad_a, stream)
+            L.nav_adam_multi(*st["adam_a"], ss, bc, self.grad_div, s)
+            if soft_update:
+                L.nav_polyak_multi(*st["poly3"], s)
+        elif soft_update:
             L.nav_grad_reduce_adam_polyak(*st["red_a"], ss, bc, *st["poly"], s)
         else:
             L.nav_grad_reduce_adam(*st["red_a"], ss, bc, s)
@@ -353,7 +381,7 @@ class TD3:
     def train_critic(self, replay, idx=None, eps=None, stream=None):
         s = stream_handle(stream)
         if self._fast():
-            return self._critic_epoch_fast(replay, idx, eps, s)
+            return self._critic_epoch_fast(replay, idx, eps, s, stream)
         self._critic_rows(replay, idx, eps, s)
         c1, c2 = self.critic_network_1, self.critic_network_2
         B = self.cfg.batch_size
@@ -417,7 +445,7 @@ class TD3:
         follow it on a policy epoch ride in the actor's reduce + Adam launch."""
         s = stream_handle(stream)
         if self._fast():
-            return self._actor_epoch_fast(replay, idx, s, soft_update)
+            return self._actor_epoch_fast(replay, idx, s, stream, soft_update)
         self._actor_rows(replay, idx, s)
         self._grads_and_step([self.actor_network], [self.actor_optimizer], self.cfg.batch_size,
                              *self._actor_wgrad_args(), [self.eslab_a], [self.grad_a],

@@ -210,14 +210,14 @@ class VecEnv:
                         C.byref(self.p), self.n, ptr(self.next_state), ptr(self.goal_term),
                         ptr(self.flags), ptr(self.demo_xy), ptr(self.demo_off),
                         self.envs_per_group, ptr(ix.cell_start), ptr(ix.cand), C.byref(rd), base,
-                        ptr(reward_out), s)
+                        ptr(reward_out), ptr(self.block_stats), s)
             else:
                 with prof.region("demo_reward", prof.demo_flops(self.n, m_per)):
                     lib().nav_demo_reward(C.byref(self.p), self.n, ptr(self.next_state),
                                           ptr(self.goal_term), ptr(self.flags),
                                           ptr(self.demo_xy), ptr(self.demo_off), m,
                                           self.envs_per_group, C.byref(rd), base,
-                                          ptr(reward_out), s)
+                                          ptr(reward_out), ptr(self.block_stats), s)
         replay.advance(self.n)
         return base
 

@@ -355,7 +355,8 @@ def test_demo_index_bit_exact_vs_brute_force(nav, orc):
     """The two-level demo index returns the brute-force minimum bit for bit (same f64 values),
     through the tick's block-cooperative demo pass (nav_agent_step_indexed) and the per-env
     indexed pass (nav_demo_reward_indexed), on states at dynamics-cell and index-cell corners, on
-    demo points, and packed around the demo path (the longest candidate lists)."""
+    demo points, and packed around the demo path (the longest candidate lists). The block_stats
+    reward column is the pushed (final) reward's sum in all three launch forms, bit for bit."""
     from nav.vec_env import ReplayRing, VecEnv
     t = golden("trace.npz")
     demo = t["demo_set"]
@@ -384,10 +385,14 @@ def test_demo_index_bit_exact_vs_brute_force(nav, orc):
         rep = ReplayRing(n, DEV)
         r = torch.zeros(n, dtype=torch.float64, device=DEV)
         env.agent_step(torch.zeros(n, 2, dtype=torch.float64, device=DEV), rep, reward_out=r)
-        rewards.append((r.cpu().numpy(), env.flags.cpu().numpy(), rep.rows.cpu().numpy()))
+        rewards.append((r.cpu().numpy(), env.flags.cpu().numpy(), rep.rows.cpu().numpy(),
+                        env.block_stats.cpu().numpy()))
         if mode != "brute":
             assert env.demo_index.mean_candidates < 200
-    (ri, fi, wi), (rp, fp, wp), (rb, fb, wb) = rewards
+    (ri, fi, wi, si), (rp, fp, wp, sp), (rb, fb, wb, sb) = rewards
+    assert np.array_equal(si, sb) and np.array_equal(sp, sb)
+    pushed = wb[:, 4].astype(np.float64).reshape(-1, 64).sum(1)
+    assert np.allclose(sb[:, 0], pushed, rtol=1e-5, atol=1e-3)
     assert np.array_equal(fi, fb) and np.array_equal(fp, fb)
     m = (fi & 16) != 0
     assert m.sum() > n // 2

@@ -1,9 +1,11 @@
 """GPU parity of the MFMA MLP kernels and the TD3 learner.
 
-Numerics: the hidden x hidden GEMMs run on the bf16 matrix cores with both fp32 operands split
-exactly into three bf16 planes (hi + mid + lo == x) and the six partial products of weight >= 2^-16
-accumulated in fp32 — fp32 accuracy, pinned here against an fp64 reference (max |err| / scale <=
-2e-6; a 2-plane split measures 6-8e-6 and fails it). The thin layers are fp32 fma chains. Against a
+Numerics: the row kernels' hidden x hidden GEMMs run on the fp16 matrix cores with both fp32
+operands scaled by powers of two and split into two fp16 planes (x 2^e = hi + lo to 22 bits) and
+the three products lo.hi + hi.lo + hi.hi accumulated in fp32; the weight-gradient kernels on the
+bf16 matrix cores with an exact three-plane bf16 split — fp32 accuracy either way, pinned here
+against an fp64 reference (max |err| / scale <= 2e-6; a two-plane bf16 split, a 16-bit-mantissa
+GEMM, measures 6-8e-6 and fails it). The thin layers are fp32 fma chains. Against a
 torch fp32 reference of the same op the outputs and gradients agree to rtol 1e-4 / 1e-3 with an atol
 scaled by the operand magnitudes (stated per test)."""
 import ctypes as C
@@ -676,7 +678,7 @@ def test_acting_forward_residual_bitwise(nav, hidden, nh, M):
     assert torch.equal(res, out)
 
 
-# ---- fp32 accuracy of the split-bf16 GEMMs (the property behind the bench's "fp32" dtype) ----
+# ---- fp32 accuracy of the split GEMMs (the property behind the bench's "fp32" dtype) ----
 def _f64_forward(layers, x):
     """fp64 forward of the same f32 weights; returns the output and every hidden pre-activation."""
     h, zs = x.double(), []
@@ -696,9 +698,10 @@ def _f64_forward(layers, x):
 def test_split_gemm_f32_accuracy_vs_fp64(nav, d_in, d_out, hidden, nh, M):
     """nav_mlp_forward and the row backward (nav_mlp_backward: dz rows and dx) against an fp64
     reference of the same f32 weights and inputs: max |err| / max |ref| <= 2e-6 for every output,
-    saved activation, dz row and dx. fp32 itself sits at ~1e-7 here; the kernels' three-plane
-    split measures 3-4e-7 in emulation, a two-plane split (a 16-bit-mantissa GEMM, narrower than
-    fp32) 6-8e-6 — the rtol 1e-4 tests above pass either, this one only the first. The row
+    saved activation, dz row and dx. fp32 itself sits at ~1e-7 here; the three-plane bf16 split
+    measured 3-4e-7, the scaled two-plane fp16 split (22 significant bits) 3-7e-7 in the probe, a
+    two-plane bf16 split (a 16-bit-mantissa GEMM, narrower than fp32) 6-8e-6 — the rtol 1e-4 tests
+    above pass all three, this one not the last. The row
     backward's reference uses the kernel's own ReLU bits (a kink within rounding of 0 may take the
     other branch in fp64; the bits are checked against the fp64 signs outside that band). Weight
     gradients (cross-row sums) are held to 1e-5 of their scale."""
@@ -823,40 +826,59 @@ def test_weight_grads_2layer_edge_cases(nav, d_in, d_out, hidden, M, splits, dy_
     assert (got[hidden:, :] == 0).all() and (got[:, hidden:] == 0).all()
 
 
-def _split_planes(packed, off, hp):
-    """The three bf16 planes of one split image (split_entry layout [3][hp/16][2][hp][8]) as
-    fp32 [3][K][N]."""
-    n = 3 * hp * hp // 2
-    raw = packed[off:off + n].contiguous().view(torch.int16).to(torch.int32) & 0xFFFF
-    f = (raw << 16).view(torch.float32)
-    return f.view(3, hp // 16, 2, hp, 8).permute(0, 1, 2, 4, 3).reshape(3, hp, hp)
+def _fp16_image(packed, off, hp):
+    """One fp16 B image (split_entry layout [2][hp/16][2][hp][8], then int32 exponents [hp]) as
+    its two planes in fp32 [2][K][N] and the per-column exponents."""
+    n = hp * hp
+    raw = packed[off:off + n].contiguous().view(torch.float16).float()
+    P = raw.view(2, hp // 16, 2, hp, 8).permute(0, 1, 2, 4, 3).reshape(2, hp, hp)
+    e = packed[off + n:off + n + hp].contiguous().view(torch.int32)
+    return P, e
+
+
+def _pow2_exp(m):
+    """mlp_common.h pow2_exp: e with m 2^e in [2^13, 2^14), clamped to +-126; 0 for 0 / inf."""
+    import math
+    if not (m > 0) or not math.isfinite(m) or m >= 3.0e38:
+        return 0
+    _, E = math.frexp(m)
+    return max(-126, min(126, 14 - E))
 
 
 def _assert_images_exact(net, tag):
     """Every hidden x hidden weight: the forward image (B[k][n] = W[n][k]) and the backward image
-    (B[k][n] = W[k][n]) hold hi = bf16_rne(W), mid = bf16_rne(W - hi), lo = W - hi - mid, and
-    hi + mid + lo == W bit for bit (the sum in fp64 is exact)."""
+    (B[k][n] = W[k][n]) hold, per column n with e_n = pow2_exp(max_k |B[k][n]|), hi =
+    fp16_rne(B 2^e_n) and lo = fp16_rne(B 2^e_n - hi) bit for bit, and (hi + lo) 2^-e_n equals B
+    within 2^-22 of the column's max (11 + 11 significant bits)."""
     hp, nh = net.hp, net.n_hidden
     pk = net.packed.detach().cpu()
     flat = net.params.detach().cpu()
-    img = 3 * hp * hp // 2
+    img = hp * hp + hp
     for L in range(1, nh):
         w_off = net.offsets[L][0]
         W = flat[w_off:w_off + hp * hp].view(hp, hp)
-        for which, off, Wk in (("fwd", (L - 1) * 2 * img, W.t()), ("bwd", (L - 1) * 2 * img + img, W)):
-            P = _split_planes(pk, off, hp)
-            assert torch.equal(P.double().sum(0), Wk.double()), (tag, L, which)
-            hi = Wk.bfloat16().float()
+        for which, off, Bk in (("fwd", (L - 1) * 2 * img, W.t()), ("bwd", (L - 1) * 2 * img + img, W)):
+            P, e = _fp16_image(pk, off, hp)
+            cmax = Bk.abs().max(0).values
+            want = torch.tensor([_pow2_exp(float(m)) for m in cmax], dtype=torch.int32)
+            assert torch.equal(e, want), (tag, L, which)
+            sc = torch.pow(2.0, want.double())
+            x = (Bk.double() * sc).float()  # exact: a power of two
+            hi = x.half().float()
             assert torch.equal(P[0], hi), (tag, L, which)
-            mid = (Wk - hi).bfloat16().float()
-            assert torch.equal(P[1], mid), (tag, L, which)
+            lo = (x - hi).half().float()
+            assert torch.equal(P[1], lo), (tag, L, which)
+            rec = (P[0].double() + P[1].double()) / sc
+            tol = 2.0 ** -22 * cmax.double() + 1e-45
+            assert ((rec - Bk.double()).abs() <= tol).all(), (tag, L, which)
 
 
 @pytest.mark.parametrize("hidden,nh", [(256, 2), (200, 3), (96, 4)])
 def test_packed_images_exact_after_pack_adam_polyak(nav, hidden, nh):
-    """The split B-operand images that the hidden GEMMs read are exact decompositions of the
-    weights after every writer: nav_mlp_pack, nav_adam, nav_polyak, and the product path's fused
-    reduce + Adam + soft updates (nav_grad_reduce_adam_polyak), targets included."""
+    """The fp16 B-operand images that the hidden GEMMs read follow the weights after every writer
+    (the exact two-plane decomposition of _assert_images_exact): nav_mlp_pack, nav_adam,
+    nav_polyak, and the product path's fused reduce + Adam + soft updates
+    (nav_grad_reduce_adam_polyak), targets included."""
     from nav._lib import descs, lib, parr, ptr, stream_handle
     L = lib()
     s = stream_handle()

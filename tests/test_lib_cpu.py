@@ -67,7 +67,7 @@ def test_gfx950_code_object_present(navlib):
 def test_abi_and_layout(navlib):
     from nav.mlp import layer_offsets
     from nav._lib import NavMlp
-    assert navlib.nav_abi_version() == 9
+    assert navlib.nav_abi_version() == 10
     assert navlib.nav_demo_index_res() in (1, 2, 4, 8)
     # the CPU port's index (cpu_baseline) is built at the same resolution
     from oracle import oracle as O
@@ -77,7 +77,7 @@ def test_abi_and_layout(navlib):
         hp = (hidden + 31) // 32 * 32
         offs, count = layer_offsets(d_in, d_out, hp, nh)
         assert navlib.nav_mlp_param_count(d_in, d_out, hp, nh) == count
-        assert navlib.nav_mlp_packed_count(hp, nh) == (nh - 1) * 2 * 3 * hp * hp // 2
+        assert navlib.nav_mlp_packed_count(hp, nh) == (nh - 1) * 2 * (hp * hp + hp)
         d = NavMlp(d_in, d_out, hidden, hp, nh, 16, 16)
         for l, (w, b, _, _) in enumerate(offs):
             wo, bo = C.c_int64(), C.c_int64()

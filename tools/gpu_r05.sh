@@ -6,6 +6,8 @@
 #   mlptests  the MLP / learner GPU tests only
 #   smoke     __graft_entry__.smoke()
 #   wgrad     tools/wgrad_bench.py on this tree's library
+#   abprev    interleaved same-box bench A/B (3 rounds): this tree vs abl/prev (a copy of the
+#             previous round's tree with its own built library; removed before the round ends)
 #   bench     the default bench line
 #   prof      rocprofv3 kernel trace + stats of a short bench
 #   pmc       FETCH_SIZE / WRITE_SIZE / SQ passes of a short bench (separate runs)
@@ -13,6 +15,7 @@
 #             each abl/libnavenv_$v.so named in $VARS (bound through tools/withlib.py; `prev` =
 #             the previous HEAD's library, tools/build_prev.sh)
 #   clock     held shader clock of the row kernels (tools/clock_probe.py on abl/libnavenv_clock.so)
+#   sphost    tools/shared_policy_host.py: config 5's learner host cost at rank batch 4 096
 #   shape     tools/probe/mfma_shape_probe (build/mfma_shape_probe): 32x32x16 vs 16x16x32 split GEMM
 #   phase     critic_rows phase trace (abl/libnavenv_$v.so for each $v in $PVARS, default
 #             trace) at batch 32768 (two workgroups per CU) and 16448 (one), and act_tick's
@@ -41,9 +44,15 @@ run() {
 for step in "$@"; do
   case "$step" in
     tests) run gputest 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
+    alltests) run gputest_all 600 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread ;;
+    dbgw) run dbg_wgrad 200 python tools/dbg_wgrad.py ;;
     mlptests) run mlptest 300 python -u -m pytest tests/test_gpu_mlp.py tests/test_gpu_fullsize.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     wgrad) run wgrad 200 python tools/wgrad_bench.py ;;
+    abprev) for r in 1 2 3; do
+          run ab_new_$r 200 python bench.py $SHORT --steps 100 --warmup 10 --no-timed-events
+          (cd abl/prev && run ab_old_$r 200 python bench.py $SHORT --steps 100 --warmup 10 --no-timed-events)
+        done ;;
     bench) run bench 500 python bench.py ;;
     prof) run prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace" -o run -- python bench.py $SHORT ;;
     pmc) run pmc_fetch 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/fetch" -o run -- python bench.py $PMCB &&
@@ -69,6 +78,7 @@ for step in "$@"; do
              run phase_${v}_tick 200 python "${W[@]}" tools/phase_trace.py --tick
            done ;;
     clock) run clock 200 python tools/withlib.py "$ROOT/abl/libnavenv_clock.so" tools/clock_probe.py --seconds 3 ;;
+    sphost) run sphost 300 python tools/shared_policy_host.py ;;
     shape) run shape 200 ./build/mfma_shape_probe 512 2.5 0 && run shape_dz 200 ./build/mfma_shape_probe 512 2.5 1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
