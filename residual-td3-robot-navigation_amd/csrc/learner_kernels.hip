@@ -788,11 +788,12 @@ struct PackInfo {
 
 // The fp16 B images (mlp_common.h) of every hidden x hidden weight of up to 8 networks, rebuilt
 // from the f32 parameters after each writer (Adam, Polyak, pack). One workgroup per (network,
-// hidden layer, image, 64-column group): thread (c = t & 63, kq = t >> 6) takes column n = 64 g + c
-// and the kq-th quarter of its k range; the column's max |B| meets in LDS, every thread then
-// writes its quarter's entries (two 16-B planes per 8 k) and the kq = 0 thread the exponent e_n.
-// The forward image's column n is W_L's row n (B[k][n] = W_L[n][k], float4 reads along the row),
-// the backward image's is W_L's column n (B[k][n] = W_L[k][n], reads coalesced across lanes).
+// hidden layer, image, 16-column group): thread (c = t & 15, kq = t >> 4) holds the 16 values
+// B[16 kq .. 16 kq + 15][16 g + c] in registers; the column's max |B| meets in LDS, then every
+// thread writes its two 8-k entries of both planes and the kq = 0 thread the exponent e_n. The
+// forward image's column n is W_L's row n (B[k][n] = W_L[n][k]: float4 reads along the row), the
+// backward image's is W_L's column n (B[k][n] = W_L[k][n]: 16 lanes on 64 consecutive bytes).
+// hp / 16 <= 16 k chunks: one load round trip and no second pass over W.
 struct PackJob {
     const float* p;
     PackInfo pk;
@@ -802,53 +803,8 @@ struct PackArgs {
     int n, per_net, cg;
 };
 
-template <int WHICH>
-NAV_DEV void pack_column(const float* W, int hp, int n, int k0, int kn, float* img, float* cmax) {
-    const int c = threadIdx.x & 63, kq = threadIdx.x >> 6;
-    float m = 0.f;
-    if (n < hp) {
-        for (int k = k0; k < k0 + kn; k += 4) {
-            float4 v;
-            if (WHICH == 0) {
-                v = *reinterpret_cast<const float4*>(W + (int64_t)n * hp + k);
-            } else {
-                v = make_float4(W[(int64_t)k * hp + n], W[(int64_t)(k + 1) * hp + n],
-                                W[(int64_t)(k + 2) * hp + n], W[(int64_t)(k + 3) * hp + n]);
-            }
-            m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-        }
-    }
-    cmax[kq * 64 + c] = m;
-    __syncthreads();
-    if (n >= hp) return;
-    m = fmaxf(fmaxf(cmax[c], cmax[64 + c]), fmaxf(cmax[128 + c], cmax[192 + c]));
-    const int e = pow2_exp(m);
-    const float sc = ldexpf(1.f, e);
-    _Float16* h16 = reinterpret_cast<_Float16*>(img);
-    for (int k = k0; k < k0 + kn; k += 8) {
-        float v[8];
-        if (WHICH == 0) {
-            const float4 a = *reinterpret_cast<const float4*>(W + (int64_t)n * hp + k);
-            const float4 b = *reinterpret_cast<const float4*>(W + (int64_t)n * hp + k + 4);
-            v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-            v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-        } else {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = W[(int64_t)(k + j) * hp + n];
-        }
-        float xs[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) xs[j] = v[j] * sc;
-        const Split2 sp = split2_8(xs);
-        const f16x8 ph = sp.h, pl = sp.l;
-        *reinterpret_cast<f16x8*>(h16 + split_entry(hp, 0, k, n)) = ph;
-        *reinterpret_cast<f16x8*>(h16 + split_entry(hp, 1, k, n)) = pl;
-    }
-    if (kq == 0) reinterpret_cast<int*>(img + (int64_t)hp * hp)[n] = e;
-}
-
 __global__ __launch_bounds__(kBlock) void k_pack_img(PackArgs a) {
-    __shared__ float cmax[4 * 64];
+    __shared__ float cmax[16][16];
     int b = blockIdx.x;
     const int jn = b / a.per_net;
     b -= jn * a.per_net;
@@ -857,16 +813,49 @@ __global__ __launch_bounds__(kBlock) void k_pack_img(PackArgs a) {
     const int g = b % a.cg;
     b /= a.cg;
     const int which = b & 1, L = (b >> 1) + 1;
-    if (L >= J.pk.n_hidden) return;  // workgroup-uniform
+    if (L >= J.pk.n_hidden || g * 16 >= hp) return;  // workgroup-uniform
     const float* W = J.p + J.pk.w_off[L];
     float* img = J.pk.packed + (int64_t)(L - 1) * 2 * split_image_floats(hp) +
                  which * split_image_floats(hp);
-    const int kn = hp / 4, k0 = (threadIdx.x >> 6) * kn;  // hp / 4: a multiple of 8
-    const int n = g * 64 + (threadIdx.x & 63);
-    if (which == 0)
-        pack_column<0>(W, hp, n, k0, kn, img, cmax);
-    else
-        pack_column<1>(W, hp, n, k0, kn, img, cmax);
+    const int c = threadIdx.x & 15, kq = threadIdx.x >> 4;
+    const int n = g * 16 + c, k0 = 16 * kq;
+    const bool on = k0 < hp;  // hp is a multiple of 32 (and n < hp: whole 16-column groups)
+    float v[16];
+    float m = 0.f;
+    if (on) {
+        if (which == 0) {
+            const float4* r = reinterpret_cast<const float4*>(W + (int64_t)n * hp + k0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float4 u = r[q];
+                v[4 * q] = u.x; v[4 * q + 1] = u.y; v[4 * q + 2] = u.z; v[4 * q + 3] = u.w;
+            }
+        } else {
+#pragma unroll
+            for (int t = 0; t < 16; ++t) v[t] = W[(int64_t)(k0 + t) * hp + n];
+        }
+#pragma unroll
+        for (int t = 0; t < 16; ++t) m = fmaxf(m, fabsf(v[t]));
+    }
+    cmax[kq][c] = m;
+    __syncthreads();
+    if (!on) return;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) m = fmaxf(m, cmax[q][c]);
+    const int e = pow2_exp(m);
+    const float sc = ldexpf(1.f, e);
+    _Float16* h16 = reinterpret_cast<_Float16*>(img);
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+        float xs[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) xs[t] = v[8 * half + t] * sc;
+        const Split2 sp = split2_8(xs);
+        const int k = k0 + 8 * half;
+        *reinterpret_cast<f16x8*>(h16 + split_entry(hp, 0, k, n)) = sp.h;
+        *reinterpret_cast<f16x8*>(h16 + split_entry(hp, 1, k, n)) = sp.l;
+    }
+    if (kq == 0) reinterpret_cast<int*>(img + (int64_t)hp * hp)[n] = e;
 }
 
 NAV_DEV float adam1(float& p, float g, float& m, float& v, float b1w, float b2, float omb2,
@@ -1187,7 +1176,7 @@ struct PackSet {
             hp = a.j[i].pk.hp > hp ? a.j[i].pk.hp : hp;
             nh = a.j[i].pk.n_hidden > nh ? a.j[i].pk.n_hidden : nh;
         }
-        a.cg = (hp + 63) / 64;
+        a.cg = (hp + 15) / 16;
         a.per_net = (nh - 1) * 2 * a.cg;
         hipLaunchKernelGGL(k_pack_img, dim3((unsigned)(a.n * a.per_net)), dim3(kBlock), 0, st, a);
         NAV_CHECK_LAUNCH();
