@@ -438,6 +438,15 @@ int nav_grad_reduce_multi(const nav_mlp* nets, int32_t n_nets, const float* cons
 int nav_adam_multi(const nav_mlp* nets, int32_t n_nets, const float* const* grads,
                    float* const* m, float* const* v, float beta1, float beta2, float eps,
                    const float* step_size, const float* bc2_sqrt, float grad_div, void* stream);
+/* nav_adam_multi + a policy epoch's soft updates (robot.py:283-285) in the same launch: each net's
+ * own target net_targets[i] follows its stepped parameters, and the n_pairs (targets[i],
+ * sources[i]) pairs (sources not stepped by this call) run beside them — the shared-policy
+ * counterpart of nav_grad_reduce_adam_polyak; every written `packed` is rebuilt. */
+int nav_adam_polyak_multi(const nav_mlp* nets, int32_t n_nets, const float* const* grads,
+                          float* const* m, float* const* v, float beta1, float beta2, float eps,
+                          const float* step_size, const float* bc2_sqrt, float grad_div,
+                          const nav_mlp* net_targets, const nav_mlp* targets,
+                          const nav_mlp* sources, int32_t n_pairs, float tau, void* stream);
 /* torch.optim.Adam step (robot.py:236-239; torch 2.10 single-tensor semantics) on a flat buffer,
  * step_size = lr/(1-b1^t), bc2_sqrt = sqrt(1-b2^t) precomputed by the caller; refreshes `packed`
  * of `net` (net->params must equal params). */

@@ -1052,7 +1052,10 @@ __global__ __launch_bounds__(kBlock) void k_adam(float4* __restrict__ p,
 
 // torch.optim.Adam of up to 2 networks in one launch from flat gradients that a collective
 // produced (shared policy: the SUM all-reduce of the bucket); g / grad_div is the averaged
-// gradient (grad_div 1: the plain step, bit-identical to k_adam).
+// gradient (grad_div 1: the plain step, bit-identical to k_adam). With the soft updates (a
+// policy epoch, nav_adam_polyak_multi): each net's own target follows its stepped parameters
+// (k_polyak's expression, as in the fused reduce), and the extra (target, source) pairs run on
+// the blocks past the Adam blocks — the hook path's counterpart of nav_grad_reduce_adam_polyak.
 struct AdamNet {
     float4* p;
     const float4* g;
@@ -1060,17 +1063,26 @@ struct AdamNet {
     float4* v;
     int64_t n4;
     float step_size, bc2s;
+    float4* tgt;  // nullable: this net's target, soft-updated from the new parameters
 };
 struct AdamArgs {
     AdamNet q[2];
     int n;
     int64_t total4;
     float b1w, b2, omb2, eps, gdiv;
+    PolyArgs poly;
+    int adam_blocks;
 };
 
 __global__ __launch_bounds__(kBlock) void k_adam_multi(AdamArgs a) {
+    if ((int)blockIdx.x >= a.adam_blocks) {  // the extra soft-update pairs (block-uniform)
+        for (int64_t i = (int64_t)(blockIdx.x - a.adam_blocks) * kBlock + threadIdx.x;
+             i < a.poly.total4; i += (int64_t)(gridDim.x - a.adam_blocks) * kBlock)
+            polyak_elem(a.poly, i);
+        return;
+    }
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < a.total4;
-         i += (int64_t)gridDim.x * kBlock) {
+         i += (int64_t)a.adam_blocks * kBlock) {
         const bool second = a.n > 1 && i >= a.q[0].n4;
         const AdamNet& q = second ? a.q[1] : a.q[0];
         const int64_t j = second ? i - a.q[0].n4 : i;
@@ -1081,6 +1093,14 @@ __global__ __launch_bounds__(kBlock) void k_adam_multi(AdamArgs a) {
         adam1(pp.z, gg.z, mm.z, vv.z, a.b1w, a.b2, a.omb2, a.eps, q.step_size, q.bc2s);
         adam1(pp.w, gg.w, mm.w, vv.w, a.b1w, a.b2, a.omb2, a.eps, q.step_size, q.bc2s);
         q.p[j] = pp; q.m[j] = mm; q.v[j] = vv;
+        if (q.tgt) {  // robot.py:309 on the parameter just stepped
+            float4 t = q.tgt[j];
+            t.x = t.x * a.poly.omt + pp.x * a.poly.tau;
+            t.y = t.y * a.poly.omt + pp.y * a.poly.tau;
+            t.z = t.z * a.poly.omt + pp.z * a.poly.tau;
+            t.w = t.w * a.poly.omt + pp.w * a.poly.tau;
+            q.tgt[j] = t;
+        }
     }
 }
 
@@ -1322,13 +1342,15 @@ int nav_grad_reduce_multi(const nav_mlp* nets, int32_t n_nets, const float* cons
     return 0;
 }
 
-int nav_adam_multi(const nav_mlp* nets, int32_t n_nets, const float* const* grads,
-                   float* const* m, float* const* v, float beta1, float beta2, float eps,
-                   const float* step_size, const float* bc2_sqrt, float grad_div, void* stream) {
+static int adam_multi_impl(const nav_mlp* nets, int32_t n_nets, const float* const* grads,
+                           float* const* m, float* const* v, float beta1, float beta2, float eps,
+                           const float* step_size, const float* bc2_sqrt, float grad_div,
+                           const nav_mlp* net_targets, const nav_mlp* targets,
+                           const nav_mlp* sources, int32_t n_pairs, float tau, void* stream) {
     AdamArgs a{};
     PackSet ps;
     if (!nets || n_nets < 1 || n_nets > 2 || !grads || !m || !v || !step_size || !bc2_sqrt ||
-        !(grad_div > 0.f))
+        !(grad_div > 0.f) || n_pairs < 0 || n_pairs > 4 || (n_pairs && (!targets || !sources)))
         return NAV_EINVAL;
     for (int i = 0; i < n_nets; ++i) {
         MlpDev d;
@@ -1342,18 +1364,58 @@ int nav_adam_multi(const nav_mlp* nets, int32_t n_nets, const float* const* grad
         q.step_size = step_size[i];
         q.bc2s = bc2_sqrt[i];
         if (!ps.add(&nets[i])) return NAV_EINVAL;
+        if (net_targets) {
+            MlpDev dt;
+            if (!make_dev(&net_targets[i], &dt) || dt.count != d.count || dt.hp != d.hp ||
+                dt.n_hidden != d.n_hidden || !ps.add(&net_targets[i]))
+                return NAV_EINVAL;
+            q.tgt = reinterpret_cast<float4*>(net_targets[i].params);
+        }
         a.total4 += q.n4;
     }
+    for (int i = 0; i < n_pairs; ++i) {
+        MlpDev dt, ds;
+        if (!make_dev(&targets[i], &dt) || !make_dev(&sources[i], &ds) || dt.count != ds.count ||
+            dt.hp != ds.hp || dt.n_hidden != ds.n_hidden || !ps.add(&targets[i]))
+            return NAV_EINVAL;
+        a.poly.q[i].t = reinterpret_cast<float4*>(targets[i].params);
+        a.poly.q[i].s = reinterpret_cast<const float4*>(sources[i].params);
+        a.poly.q[i].n4 = dt.count / 4;
+        a.poly.total4 += a.poly.q[i].n4;
+    }
+    a.poly.n = n_pairs;
+    a.poly.omt = 1.0f - tau;
+    a.poly.tau = tau;
     a.n = n_nets;
     a.b1w = 1.0f - beta1;
     a.b2 = beta2;
     a.omb2 = 1.0f - beta2;
     a.eps = eps;
     a.gdiv = grad_div;
-    hipLaunchKernelGGL(k_adam_multi, dim3(grid_stride_blocks(a.total4)), dim3(kBlock), 0,
-                       S(stream), a);
+    a.adam_blocks = grid_stride_blocks(a.total4);
+    int blocks = a.adam_blocks;
+    if (n_pairs) blocks += (int)((a.poly.total4 + kBlock - 1) / kBlock < 256
+                                     ? (a.poly.total4 + kBlock - 1) / kBlock : 256);
+    hipLaunchKernelGGL(k_adam_multi, dim3((unsigned)blocks), dim3(kBlock), 0, S(stream), a);
     NAV_CHECK_LAUNCH();
     return ps.launch(S(stream));
+}
+
+int nav_adam_multi(const nav_mlp* nets, int32_t n_nets, const float* const* grads,
+                   float* const* m, float* const* v, float beta1, float beta2, float eps,
+                   const float* step_size, const float* bc2_sqrt, float grad_div, void* stream) {
+    return adam_multi_impl(nets, n_nets, grads, m, v, beta1, beta2, eps, step_size, bc2_sqrt,
+                           grad_div, nullptr, nullptr, nullptr, 0, 0.f, stream);
+}
+
+int nav_adam_polyak_multi(const nav_mlp* nets, int32_t n_nets, const float* const* grads,
+                          float* const* m, float* const* v, float beta1, float beta2, float eps,
+                          const float* step_size, const float* bc2_sqrt, float grad_div,
+                          const nav_mlp* net_targets, const nav_mlp* targets,
+                          const nav_mlp* sources, int32_t n_pairs, float tau, void* stream) {
+    if (!net_targets) return NAV_EINVAL;
+    return adam_multi_impl(nets, n_nets, grads, m, v, beta1, beta2, eps, step_size, bc2_sqrt,
+                           grad_div, net_targets, targets, sources, n_pairs, tau, stream);
 }
 
 // RedArgs of the reduce (+ Adam when m is non-NULL, + the soft updates): *blocks = the reduce

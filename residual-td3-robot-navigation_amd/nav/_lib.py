@@ -146,6 +146,10 @@ SIGNATURES = [
     ("nav_adam_multi", C.c_int, [_P(NavMlp), C.c_int32, _P(_vp), _P(_vp), _P(_vp), C.c_float,
                                  C.c_float, C.c_float, _P(C.c_float), _P(C.c_float), C.c_float,
                                  _vp]),
+    ("nav_adam_polyak_multi", C.c_int, [_P(NavMlp), C.c_int32, _P(_vp), _P(_vp), _P(_vp),
+                                        C.c_float, C.c_float, C.c_float, _P(C.c_float),
+                                        _P(C.c_float), C.c_float, _P(NavMlp), _P(NavMlp),
+                                        _P(NavMlp), C.c_int32, C.c_float, _vp]),
     ("nav_adam", C.c_int, [_P(NavMlp), _vp, _vp, _vp, C.c_float, C.c_float, C.c_float,
                            C.c_float, C.c_float, _vp]),
     ("nav_polyak", C.c_int, [_P(NavMlp), _P(NavMlp), C.c_float, _vp]),

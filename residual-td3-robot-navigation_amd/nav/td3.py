@@ -279,8 +279,7 @@ class TD3:
                         self.nblk, parr(self.grad_a))
         st["adam_a"] = (descs(a), 1, parr(self.grad_a), parr(oa.m), parr(oa.v), oa.b1, oa.b2,
                         oa.eps)
-        st["poly3"] = (descs(self.target_actor, self.target_critic_network_1,
-                             self.target_critic_network_2), descs(a, c1, c2), 3, c.tau)
+
         st["wgrad"] = c1.n_hidden > 1
         self._st, self._st_key = st, key
         return st
@@ -336,9 +335,10 @@ class TD3:
         if self.grad_hook is not None:
             L.nav_grad_reduce_multi(*st["redm_a"], s)
             self._hook(self.grad_a, stream)
-            L.nav_adam_multi(*st["adam_a"], ss, bc, self.grad_div, s)
-            if soft_update:
-                L.nav_polyak_multi(*st["poly3"], s)
+            if soft_update:  # the actor's step and the three soft updates in one launch
+                L.nav_adam_polyak_multi(*st["adam_a"], ss, bc, self.grad_div, *st["poly"], s)
+            else:
+                L.nav_adam_multi(*st["adam_a"], ss, bc, self.grad_div, s)
         elif soft_update:
             L.nav_grad_reduce_adam_polyak(*st["red_a"], ss, bc, *st["poly"], s)
         else:

@@ -351,6 +351,44 @@ def _rank_worker(rank, ws, port, hidden, nh, B, epochs, q):
         raise
 
 
+def test_adam_polyak_multi_bitwise_vs_adam_then_polyak():
+    """nav_adam_polyak_multi (the hook path's policy epoch: the actor's Adam step from the reduced
+    bucket and the three soft updates in one launch) equals nav_adam_multi followed by
+    nav_polyak_multi bit for bit: parameters, moments, every target and every packed image."""
+    import ctypes as C
+    from nav import _lib
+    from nav._lib import descs, lib, parr, stream_handle
+    from nav.mlp import DeviceMLP
+    from oracle.td3_oracle import make_mlp_params
+    _lib.require_gpu()
+    L = lib()
+    s = stream_handle()
+    res = []
+    for fused in (True, False):
+        mk = lambda di, do, seed: DeviceMLP(di, do, 256, 2, DEV).load(  # noqa: E731
+            make_mlp_params(seed, [di, 256, 256, do]))
+        a, ta = mk(2, 2, 11), mk(2, 2, 12)
+        c1, c2, t1, t2 = mk(4, 1, 13), mk(4, 1, 14), mk(4, 1, 15), mk(4, 1, 16)
+        g = torch.Generator().manual_seed(17)
+        grad = (torch.randn(a.count, generator=g) * 1e-2).to(DEV)
+        m = (torch.randn(a.count, generator=g) * 1e-3).to(DEV)
+        v = (torch.rand(a.count, generator=g) * 1e-4).to(DEV)
+        ss, bc = (C.c_float * 1)(1e-3), (C.c_float * 1)(0.7)
+        if fused:
+            assert L.nav_adam_polyak_multi(descs(a), 1, parr(grad), parr(m), parr(v), 0.9, 0.999,
+                                           1e-8, ss, bc, 8.0, descs(ta), descs(t1, t2),
+                                           descs(c1, c2), 2, 0.005, s) == 0
+        else:
+            assert L.nav_adam_multi(descs(a), 1, parr(grad), parr(m), parr(v), 0.9, 0.999, 1e-8,
+                                    ss, bc, 8.0, s) == 0
+            assert L.nav_polyak_multi(descs(ta, t1, t2), descs(a, c1, c2), 3, 0.005, s) == 0
+        torch.cuda.synchronize()
+        res.append([x.cpu() for x in (a.params, a.packed, m, v, ta.params, ta.packed, t1.params,
+                                       t1.packed, t2.params, t2.packed)])
+    for x, y in zip(*res):
+        assert torch.equal(x, y)
+
+
 def test_shared_policy_through_real_collective_two_processes():
     """BASELINE config 5's product path end to end with a real collective: two processes, each a
     TD3(grad_hook=nav.dist.GradAllReduce) on its half batch, all-reducing through
