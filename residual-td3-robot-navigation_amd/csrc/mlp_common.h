@@ -187,11 +187,31 @@ struct Split2 {
 };
 
 // acc += a . b over one 16-deep k step, the three products smallest first
+#ifndef NAV_MFMA16_TIMING
 NAV_DEV f32x16 mfma_x3(const Split2& a, const f16x8 (&b)[2], f32x16 c) {
     c = mfma_h(a.l, b[0], c);
     c = mfma_h(a.h, b[1], c);
     return mfma_h(a.h, b[0], c);
 }
+#else
+// Timing-only variant build (wrong results): the same MFMA cycles on v_mfma_f32_16x16x32_f16,
+// two per 32x32x16 product, to measure the shape's clock effect inside the real row kernels.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+NAV_DEV f32x16 mfma_x3(const Split2& a, const f16x8 (&b)[2], f32x16 c) {
+    f32x4 c0 = __builtin_shufflevector(c, c, 0, 1, 2, 3);
+    f32x4 c1 = __builtin_shufflevector(c, c, 4, 5, 6, 7);
+    c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a.l, b[0], c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[0], a.l, c1, 0, 0, 0);
+    c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a.h, b[1], c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[1], a.h, c1, 0, 0, 0);
+    c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a.h, b[0], c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[0], a.h, c1, 0, 0, 0);
+    const f32x8 t = __builtin_shufflevector(c0, c1, 0, 1, 2, 3, 4, 5, 6, 7);
+    const f32x8 u = __builtin_shufflevector(c, c, 8, 9, 10, 11, 12, 13, 14, 15);
+    return __builtin_shufflevector(t, u, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+}
+#endif
 
 // the same with both operands split in registers: a.lo b.hi + a.hi b.lo + a.hi b.hi
 NAV_DEV f32x16 mfma_x3s(const Split2& a, const Split2& b, f32x16 c) {

@@ -50,6 +50,11 @@ for step in "$@"; do
     mlptests) run mlptest 300 python -u -m pytest tests/test_gpu_mlp.py tests/test_gpu_fullsize.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     wgrad) run wgrad 200 python tools/wgrad_bench.py ;;
+    wgscan) run wg_32768 120 python tools/wgrad_bench.py &&
+            run wg_16384 120 python tools/wgrad_bench.py --batch 16384 &&
+            run wg_65536 120 python tools/wgrad_bench.py --batch 65536 &&
+            run wg_s8 120 python tools/wgrad_bench.py --splits 8,8 &&
+            run wg_s32 120 python tools/wgrad_bench.py --splits 32,32 ;;
     abprev) for r in 1 2 3; do
           run ab_new_$r 200 python bench.py $SHORT --steps 100 --warmup 10 --no-timed-events
           (cd abl/prev && run ab_old_$r 200 python bench.py $SHORT --steps 100 --warmup 10 --no-timed-events)

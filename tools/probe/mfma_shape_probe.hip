@@ -304,6 +304,329 @@ __device__ __forceinline__ void gemm32h(const float* A, const f16x8* Bs, _Float1
     if (favored) __builtin_amdgcn_s_setprio(0);
 }
 
+// ---- h32k32: the same products, the stage holding 32 k per round (two 16-deep MFMA steps per
+// barrier pair: half the barriers), chunk c of row r at c ^ ((r >> 2) & 3)
+__device__ __forceinline__ void gemm32h_k32(const float* A, const f16x8* Bs, _Float16* stage, float sa,
+                                            f32x16 (&acc)[2][2]) {
+    constexpr int PP = TM * 32;     // fp16 per plane
+    constexpr int NR = HP / 32;     // rounds
+    const int tid = threadIdx.x, lane = tid & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
+    for (int rt = 0; rt < 2; ++rt)
+        for (int j = 0; j < 2; ++j)
+            for (int i = 0; i < 16; ++i) acc[rt][j][i] = 0.f;
+    const char* Bb = reinterpret_cast<const char*>(Bs);
+    const uint32_t o0 = (uint32_t)(h * HP + wv * 32 + l32) * 16u;
+    const uint32_t o1 = (uint32_t)(h * HP + (wv + 4) * 32 + l32) * 16u;
+    auto ldB = [&](uint32_t o, int p, int q) {
+        return *reinterpret_cast<const f16x8*>(Bb + (o + (uint32_t)((p * PL2 + q * 2 * HP) * 16)));
+    };
+    f16x8 bq0[2][2][2], bq1[2][2][2];  // [round parity][sub-step][plane]
+    for (int u = 0; u < 2; ++u)
+        for (int p = 0; p < 2; ++p) {
+            bq0[0][u][p] = ldB(o0, p, u);
+            bq1[0][u][p] = ldB(o1, p, u);
+        }
+    const int sr = tid >> 2, ck = tid & 3;
+    const float* src = A + sr * SS + 8 * ck;
+    _Float16* dst = stage + sr * 32 + ((ck ^ ((sr >> 2) & 3)) << 3);
+    float4 x0 = *reinterpret_cast<const float4*>(src), x1 = *reinterpret_cast<const float4*>(src + 4);
+    auto produce = [&](int q) {
+        const float v[8] = {x0.x * sa, x0.y * sa, x0.z * sa, x0.w * sa, x1.x * sa, x1.y * sa, x1.z * sa, x1.w * sa};
+        f16x8 ph, pl;
+        for (int j = 0; j < 8; ++j) ph[j] = (_Float16)v[j];
+        asm volatile("" : "+v"(ph));
+        for (int j = 0; j < 8; ++j) pl[j] = (_Float16)(v[j] - (float)ph[j]);
+        *reinterpret_cast<f16x8*>(dst) = ph;
+        *reinterpret_cast<f16x8*>(dst + PP) = pl;
+        if (q + 1 < NR) {
+            x0 = *reinterpret_cast<const float4*>(src + 32 * (q + 1));
+            x1 = *reinterpret_cast<const float4*>(src + 32 * (q + 1) + 4);
+        }
+        if (q >= 1)
+            for (int u = 0; u < 2; ++u)
+                for (int p = 0; p < 2; ++p) {
+                    bq0[q & 1][u][p] = ldB(o0, p, 2 * q + u);
+                    bq1[q & 1][u][p] = ldB(o1, p, 2 * q + u);
+                }
+    };
+    f16x8 ah[2][2], al[2][2];  // [sub-step][row tile]
+    auto consume = [&]() {
+        __syncthreads();
+        for (int u = 0; u < 2; ++u)
+            for (int rt = 0; rt < 2; ++rt) {
+                const int r = rt * 32 + l32, c = 2 * u + h;
+                const _Float16* f = stage + r * 32 + ((c ^ ((r >> 2) & 3)) << 3);
+                ah[u][rt] = *reinterpret_cast<const f16x8*>(f);
+                al[u][rt] = *reinterpret_cast<const f16x8*>(f + PP);
+            }
+        __syncthreads();
+    };
+    produce(0);
+    consume();
+    const bool favored = blockIdx.x >= (gridDim.x >> 1);
+    if (favored) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int q = 0; q < NR; ++q) {
+        if (q + 1 < NR) produce(q + 1);
+        f16x8 ch[2][2], cl[2][2];
+        for (int u = 0; u < 2; ++u)
+            for (int rt = 0; rt < 2; ++rt) {
+                ch[u][rt] = ah[u][rt];
+                cl[u][rt] = al[u][rt];
+            }
+        for (int u = 0; u < 2; ++u)
+            for (int rt = 0; rt < 2; ++rt)
+                for (int j = 0; j < 2; ++j) {
+                    const f16x8* b = j == 0 ? bq0[q & 1][u] : bq1[q & 1][u];
+                    f32x16 c = acc[rt][j];
+                    c = mh32(cl[u][rt], b[0], c);
+                    c = mh32(ch[u][rt], b[1], c);
+                    acc[rt][j] = mh32(ch[u][rt], b[0], c);
+                }
+        if (q + 1 < NR) consume();
+    }
+    if (favored) __builtin_amdgcn_s_setprio(0);
+}
+
+// ---- h32db: the product's fp16 GEMM with a double-buffered stage and ONE barrier per step: after
+// step q's barrier a wave reads step q + 1's fragments (registers, in flight under step q's
+// MFMAs) and produces step q + 2 into the buffer step q was read from
+__device__ __forceinline__ void gemm32h_db(const float* A, const f16x8* Bs, _Float16* stage, float sa,
+                                           f32x16 (&acc)[2][2]) {
+    constexpr int PP = TM * 16, SB = 2 * PP;
+    const int tid = threadIdx.x, lane = tid & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
+    for (int rt = 0; rt < 2; ++rt)
+        for (int j = 0; j < 2; ++j)
+            for (int i = 0; i < 16; ++i) acc[rt][j][i] = 0.f;
+    const char* Bb = reinterpret_cast<const char*>(Bs);
+    const uint32_t o0 = (uint32_t)(h * HP + wv * 32 + l32) * 16u;
+    const uint32_t o1 = (uint32_t)(h * HP + (wv + 4) * 32 + l32) * 16u;
+    auto ldB = [&](uint32_t o, int p, int q) {
+        return *reinterpret_cast<const f16x8*>(Bb + (o + (uint32_t)((p * PL2 + q * 2 * HP) * 16)));
+    };
+    f16x8 bq0[2][2], bq1[2][2];
+    for (int p = 0; p < 2; ++p) {
+        bq0[0][p] = ldB(o0, p, 0);
+        bq1[0][p] = ldB(o1, p, 0);
+    }
+    const int sr = tid >> 2, sk = (tid & 3) * 4;
+    const float* src = A + sr * SS + sk;
+    _Float16* dst = stage + sr * 16 + ((((sk >> 3) ^ (sr >> 3)) & 1) << 3) + (sk & 7);
+    const _Float16* frag = stage + l32 * 16 + (((h ^ (l32 >> 3)) & 1) << 3);
+    float4 x = *reinterpret_cast<const float4*>(src);
+    auto produce = [&](int q) {  // step q into buffer q & 1; the next x; B of step q - 1 + 1
+        const float v[4] = {x.x * sa, x.y * sa, x.z * sa, x.w * sa};
+        f16x4 ph, pl;
+        for (int j = 0; j < 4; ++j) ph[j] = (_Float16)v[j];
+        asm volatile("" : "+v"(ph));
+        for (int j = 0; j < 4; ++j) pl[j] = (_Float16)(v[j] - (float)ph[j]);
+        _Float16* d = dst + (q & 1) * SB;
+        *reinterpret_cast<f16x4*>(d) = ph;
+        *reinterpret_cast<f16x4*>(d + PP) = pl;
+        if (q + 1 < NQ) x = *reinterpret_cast<const float4*>(src + 16 * (q + 1));
+    };
+    f16x8 ah[2][2], al[2][2];  // [step parity][row tile]
+    auto readf = [&](int q) {
+        const _Float16* fq = frag + (q & 1) * SB;
+        for (int rt = 0; rt < 2; ++rt) {
+            ah[q & 1][rt] = *reinterpret_cast<const f16x8*>(fq + rt * 32 * 16);
+            al[q & 1][rt] = *reinterpret_cast<const f16x8*>(fq + rt * 32 * 16 + PP);
+        }
+    };
+    produce(0);
+    produce(1);
+    __syncthreads();
+    readf(0);
+    const bool favored = blockIdx.x >= (gridDim.x >> 1);
+    if (favored) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        __syncthreads();
+        if (q + 1 < NQ) {
+            readf(q + 1);
+            for (int p = 0; p < 2; ++p) {
+                bq0[(q + 1) & 1][p] = ldB(o0, p, q + 1);
+                bq1[(q + 1) & 1][p] = ldB(o1, p, q + 1);
+            }
+        }
+        if (q + 2 < NQ) produce(q + 2);
+        for (int rt = 0; rt < 2; ++rt)
+            for (int j = 0; j < 2; ++j) {
+                const f16x8* b = j == 0 ? bq0[q & 1] : bq1[q & 1];
+                f32x16 c = acc[rt][j];
+                c = mh32(al[q & 1][rt], b[0], c);
+                c = mh32(ah[q & 1][rt], b[1], c);
+                acc[rt][j] = mh32(ah[q & 1][rt], b[0], c);
+            }
+    }
+    if (favored) __builtin_amdgcn_s_setprio(0);
+}
+
+__device__ __forceinline__ float wave_max(float v);
+__device__ __forceinline__ float pow2_scale(float amax);
+
+// ---- h32pre: the A operand kept in LDS as its two scaled fp16 planes [2][64][HP + 8] (written by the
+// previous layer's epilogue, 4 B per element like the f32 rows): no split stage, no barrier and
+// no split VALU inside the GEMM; every wave reads its fragments straight from the planes
+constexpr int PS2 = HP + 8;  // plane row stride (fp16)
+__device__ __forceinline__ void gemm32h_pre(const _Float16* P, const f16x8* Bs, f32x16 (&acc)[2][2]) {
+    constexpr int PPL = TM * PS2;
+    const int lane = threadIdx.x & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
+    for (int rt = 0; rt < 2; ++rt)
+        for (int j = 0; j < 2; ++j)
+            for (int i = 0; i < 16; ++i) acc[rt][j][i] = 0.f;
+    const char* Bb = reinterpret_cast<const char*>(Bs);
+    const uint32_t o0 = (uint32_t)(h * HP + wv * 32 + l32) * 16u;
+    const uint32_t o1 = (uint32_t)(h * HP + (wv + 4) * 32 + l32) * 16u;
+    auto ldB = [&](uint32_t o, int p, int q) {
+        return *reinterpret_cast<const f16x8*>(Bb + (o + (uint32_t)((p * PL2 + q * 2 * HP) * 16)));
+    };
+    f16x8 bq0[2][2], bq1[2][2];
+    for (int p = 0; p < 2; ++p) {
+        bq0[0][p] = ldB(o0, p, 0);
+        bq1[0][p] = ldB(o1, p, 0);
+    }
+    const _Float16* arow = P + l32 * PS2 + 8 * h;
+    f16x8 ah[2][2], al[2][2];
+    auto rdA = [&](int q) {
+        for (int rt = 0; rt < 2; ++rt) {
+            ah[q & 1][rt] = *reinterpret_cast<const f16x8*>(arow + rt * 32 * PS2 + 16 * q);
+            al[q & 1][rt] = *reinterpret_cast<const f16x8*>(arow + rt * 32 * PS2 + 16 * q + PPL);
+        }
+    };
+    rdA(0);
+    const bool favored = blockIdx.x >= (gridDim.x >> 1);
+    if (favored) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        if (q + 1 < NQ) {
+            rdA(q + 1);
+            for (int p = 0; p < 2; ++p) {
+                bq0[(q + 1) & 1][p] = ldB(o0, p, q + 1);
+                bq1[(q + 1) & 1][p] = ldB(o1, p, q + 1);
+            }
+        }
+        for (int rt = 0; rt < 2; ++rt)
+            for (int j = 0; j < 2; ++j) {
+                const f16x8* b = j == 0 ? bq0[q & 1] : bq1[q & 1];
+                f32x16 c = acc[rt][j];
+                c = mh32(al[q & 1][rt], b[0], c);
+                c = mh32(ah[q & 1][rt], b[1], c);
+                acc[rt][j] = mh32(ah[q & 1][rt], b[0], c);
+            }
+    }
+    if (favored) __builtin_amdgcn_s_setprio(0);
+}
+
+// epilogue of h32pre: relu(acc * unscale), the block max (wave maxima through LDS, a barrier),
+// then the scaled two-plane split stored into the planes (16-bit stores, C layout)
+__device__ __forceinline__ void store_planes_h(f32x16 (&acc)[2][2], _Float16* P, float* wmax,
+                                               const float* colinv, float& inv_next) {
+    constexpr int PPL = TM * PS2;
+    const int lane = threadIdx.x & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
+    float mm = 0.f;
+    for (int j = 0; j < 2; ++j) {
+        const float u = inv_next * colinv[(j == 0 ? wv : wv + 4) * 32 + l32];
+        for (int rt = 0; rt < 2; ++rt)
+            for (int i = 0; i < 16; ++i) {
+                acc[rt][j][i] = fmaxf(acc[rt][j][i] * u, 0.f);
+                mm = fmaxf(mm, acc[rt][j][i]);
+            }
+    }
+    mm = wave_max(mm);
+    if (lane == 0) wmax[wv] = mm;
+    __syncthreads();
+    const float amax = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
+    const float sa = pow2_scale(amax);
+    inv_next = 1.f / sa;
+    for (int j = 0; j < 2; ++j) {
+        _Float16* col = P + (j == 0 ? wv : wv + 4) * 32 + l32 + 4 * h * PS2;
+        for (int rt = 0; rt < 2; ++rt)
+            for (int i = 0; i < 16; ++i) {
+                const float v = acc[rt][j][i] * sa;
+                const _Float16 hh = (_Float16)v;
+                const int o = (rt * 32 + (i & 3) + 8 * (i >> 2)) * PS2;
+                col[o] = hh;
+                col[o + PPL] = (_Float16)(v - (float)hh);
+            }
+    }
+}
+
+// ---- h16: two fp16 planes, three products on v_mfma_f32_16x16x32_f16 (gemm16's tiling)
+__device__ __forceinline__ f32x4 mh16(f16x8 a, f16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ void gemm16h(const float* A, const f16x8* Bs, _Float16* stage, float sa,
+                                        f32x4 (&acc)[4][4]) {
+    constexpr int NS = HP / 32;
+    constexpr int PP = TM * 32;
+    const int tid = threadIdx.x, lane = tid & 63, wv = wave_id();
+    for (int rt = 0; rt < 4; ++rt)
+        for (int c = 0; c < 4; ++c)
+            for (int i = 0; i < 4; ++i) acc[rt][c][i] = 0.f;
+    const char* Bb = reinterpret_cast<const char*>(Bs);
+    const uint32_t ob = (uint32_t)(((lane >> 5) * 2 + ((lane >> 4) & 1)) * HP + wv * 64 + (lane & 15)) * 16u;
+    auto ldB = [&](int c, int p, int s) {
+        return *reinterpret_cast<const f16x8*>(Bb + (ob + (uint32_t)((p * PL2 + (size_t)s * 4 * HP + c * 16) * 16)));
+    };
+    f16x8 bq[2][4][2];
+    for (int c = 0; c < 4; ++c)
+        for (int p = 0; p < 2; ++p) bq[0][c][p] = ldB(c, p, 0);
+    const int sr = tid >> 2, ck = tid & 3;
+    const float* src = A + sr * SS + 8 * ck;
+    _Float16* dst = stage + sr * 32 + ((ck ^ ((sr >> 1) & 3)) << 3);
+    float4 x0 = *reinterpret_cast<const float4*>(src), x1 = *reinterpret_cast<const float4*>(src + 4);
+    auto produce = [&](int s) {
+        const float v[8] = {x0.x * sa, x0.y * sa, x0.z * sa, x0.w * sa, x1.x * sa, x1.y * sa, x1.z * sa, x1.w * sa};
+        f16x8 ph, pl;
+        for (int j = 0; j < 8; ++j) ph[j] = (_Float16)v[j];
+        asm volatile("" : "+v"(ph));
+        for (int j = 0; j < 8; ++j) pl[j] = (_Float16)(v[j] - (float)ph[j]);
+        *reinterpret_cast<f16x8*>(dst) = ph;
+        *reinterpret_cast<f16x8*>(dst + PP) = pl;
+        if (s + 1 < NS) {
+            x0 = *reinterpret_cast<const float4*>(src + 32 * (s + 1));
+            x1 = *reinterpret_cast<const float4*>(src + 32 * (s + 1) + 4);
+        }
+        if (s >= 1)
+            for (int c = 0; c < 4; ++c)
+                for (int p = 0; p < 2; ++p) bq[s & 1][c][p] = ldB(c, p, s);
+    };
+    f16x8 ah[4], al[4];
+    auto consume = [&]() {
+        __syncthreads();
+        for (int rt = 0; rt < 4; ++rt) {
+            const int r = rt * 16 + (lane & 15);
+            const _Float16* f = stage + r * 32 + (((lane >> 4) ^ ((r >> 1) & 3)) << 3);
+            ah[rt] = *reinterpret_cast<const f16x8*>(f);
+            al[rt] = *reinterpret_cast<const f16x8*>(f + PP);
+        }
+        __syncthreads();
+    };
+    produce(0);
+    consume();
+    const bool favored = blockIdx.x >= (gridDim.x >> 1);
+    if (favored) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        if (s + 1 < NS) produce(s + 1);
+        f16x8 ch[4], cl[4];
+        for (int rt = 0; rt < 4; ++rt) {
+            ch[rt] = ah[rt];
+            cl[rt] = al[rt];
+        }
+        for (int c = 0; c < 4; ++c)
+            for (int rt = 0; rt < 4; ++rt) {
+                f32x4 a4 = acc[rt][c];
+                a4 = mh16(cl[rt], bq[s & 1][c][0], a4);
+                a4 = mh16(ch[rt], bq[s & 1][c][1], a4);
+                acc[rt][c] = mh16(ch[rt], bq[s & 1][c][0], a4);
+            }
+        if (s + 1 < NS) consume();
+    }
+    if (favored) __builtin_amdgcn_s_setprio(0);
+}
+
 __device__ __forceinline__ float wave_max(float v) {
     for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m, 64));
     return v;
@@ -314,6 +637,128 @@ __device__ __forceinline__ float pow2_scale(float amax) {
     int e;
     frexpf(amax, &e);
     return ldexpf(1.f, 14 - e);
+}
+
+// ---- h32w8: 128 rows per workgroup, 8 waves (2 per SIMD, one workgroup per CU): wave w owns the
+// 64 rows (w >> 2) and the column tiles (w & 3), (w & 3) + 4 — the same wave tile, half the B
+// image reads per row (the B planes stream from L2 once per 128 rows instead of once per 64)
+constexpr int TM8 = 128;
+__device__ __forceinline__ void gemm32h_w8(const float* A, const f16x8* Bs, _Float16* stage, float sa,
+                                           f32x16 (&acc)[2][2]) {
+    constexpr int PP = TM8 * 16;
+    const int tid = threadIdx.x, lane = tid & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
+    const int ct = wv & 3, rh = wv >> 2;
+    for (int rt = 0; rt < 2; ++rt)
+        for (int j = 0; j < 2; ++j)
+            for (int i = 0; i < 16; ++i) acc[rt][j][i] = 0.f;
+    const char* Bb = reinterpret_cast<const char*>(Bs);
+    const uint32_t o0 = (uint32_t)(h * HP + ct * 32 + l32) * 16u;
+    const uint32_t o1 = (uint32_t)(h * HP + (ct + 4) * 32 + l32) * 16u;
+    auto ldB = [&](uint32_t o, int p, int q) {
+        return *reinterpret_cast<const f16x8*>(Bb + (o + (uint32_t)((p * PL2 + q * 2 * HP) * 16)));
+    };
+    f16x8 bq0[2][2], bq1[2][2];
+    for (int p = 0; p < 2; ++p) {
+        bq0[0][p] = ldB(o0, p, 0);
+        bq1[0][p] = ldB(o1, p, 0);
+    }
+    const int sr = tid >> 2, sk = (tid & 3) * 4;  // 512 threads: 128 rows x 4
+    const float* src = A + sr * SS + sk;
+    _Float16* dst = stage + sr * 16 + ((((sk >> 3) ^ (sr >> 3)) & 1) << 3) + (sk & 7);
+    const _Float16* frag = stage + (rh * 64 + l32) * 16 + (((h ^ (l32 >> 3)) & 1) << 3);
+    float4 x = *reinterpret_cast<const float4*>(src);
+    auto produce = [&](int q) {
+        const float v[4] = {x.x * sa, x.y * sa, x.z * sa, x.w * sa};
+        f16x4 ph, pl;
+        for (int j = 0; j < 4; ++j) ph[j] = (_Float16)v[j];
+        asm volatile("" : "+v"(ph));
+        for (int j = 0; j < 4; ++j) pl[j] = (_Float16)(v[j] - (float)ph[j]);
+        *reinterpret_cast<f16x4*>(dst) = ph;
+        *reinterpret_cast<f16x4*>(dst + PP) = pl;
+        if (q + 1 < NQ) x = *reinterpret_cast<const float4*>(src + 16 * (q + 1));
+        if (q >= 1)
+            for (int p = 0; p < 2; ++p) {
+                bq0[q & 1][p] = ldB(o0, p, q);
+                bq1[q & 1][p] = ldB(o1, p, q);
+            }
+    };
+    f16x8 ah[2], al[2];
+    auto consume = [&]() {
+        __syncthreads();
+        for (int rt = 0; rt < 2; ++rt) {
+            const _Float16* f = frag + rt * 32 * 16;
+            ah[rt] = *reinterpret_cast<const f16x8*>(f);
+            al[rt] = *reinterpret_cast<const f16x8*>(f + PP);
+        }
+        __syncthreads();
+    };
+    produce(0);
+    consume();
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        if (q + 1 < NQ) produce(q + 1);
+        const f16x8 ch[2] = {ah[0], ah[1]}, cl[2] = {al[0], al[1]};
+        for (int rt = 0; rt < 2; ++rt)
+            for (int j = 0; j < 2; ++j) {
+                const f16x8* b = j == 0 ? bq0[q & 1] : bq1[q & 1];
+                f32x16 c = acc[rt][j];
+                c = mh32(cl[rt], b[0], c);
+                c = mh32(ch[rt], b[1], c);
+                acc[rt][j] = mh32(ch[rt], b[0], c);
+            }
+        if (q + 1 < NQ) consume();
+    }
+}
+
+template <bool STAMP>
+__global__ __launch_bounds__(512, 1) void k_probe_w8(const float* rows, float* out, unsigned long long* stamps,
+                                                     const f16x8* Bh, const float* colinv) {
+    extern __shared__ __attribute__((aligned(16))) float act[];
+    _Float16* stage = reinterpret_cast<_Float16*>(act + TM8 * SS);
+    float* wmax = act + TM8 * SS + TM8 * 16;  // past the 2-plane stage (fp16: TM8*16*2*2 B)
+    const int tid = threadIdx.x;
+    const float* src = rows + (size_t)(blockIdx.x & 3) * TM8 * HP;
+    float m = 0.f;
+    for (int i = tid; i < TM8 * HP; i += 512) {
+        act[(i / HP) * SS + i % HP] = src[i];
+        m = fmaxf(m, fabsf(src[i]));
+    }
+    m = wave_max(m);
+    if ((tid & 63) == 0) wmax[tid >> 6] = m;
+    __syncthreads();
+    if (STAMP && tid == 0) {
+        stamps[blockIdx.x * 4 + 0] = __builtin_amdgcn_s_memtime();
+        stamps[blockIdx.x * 4 + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+    const int lane = tid & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31, ct = wv & 3, rh = wv >> 2;
+    for (int L = 0; L < LAYERS; ++L) {
+        float amax = 0.f;
+        for (int w = 0; w < 8; ++w) amax = fmaxf(amax, wmax[w]);
+        const float sa = pow2_scale(amax), inva = 1.f / sa;
+        f32x16 acc[2][2];
+        gemm32h_w8(act, Bh, stage, sa, acc);
+        __syncthreads();
+        float mm = 0.f;
+        for (int j = 0; j < 2; ++j) {
+            const float u = inva * colinv[(j == 0 ? ct : ct + 4) * 32 + l32];
+            float* col = act + (j == 0 ? ct : ct + 4) * 32 + l32 + 4 * h * SS + rh * 64 * SS;
+            for (int rt = 0; rt < 2; ++rt)
+                for (int i = 0; i < 16; ++i) {
+                    const float v = fmaxf(acc[rt][j][i] * u, 0.f);
+                    col[(rt * 32 + (i & 3) + 8 * (i >> 2)) * SS] = v;
+                    mm = fmaxf(mm, v);
+                }
+        }
+        mm = wave_max(mm);
+        if (lane == 0) wmax[wv] = mm;
+        __syncthreads();
+    }
+    if (STAMP && tid == 0) {
+        stamps[blockIdx.x * 4 + 2] = __builtin_amdgcn_s_memtime();
+        stamps[blockIdx.x * 4 + 3] = __builtin_amdgcn_s_memrealtime();
+    }
+    if (blockIdx.x < 4)
+        for (int i = tid; i < TM8 * HP; i += 512) out[(size_t)blockIdx.x * TM8 * HP + i] = act[(i / HP) * SS + i % HP];
 }
 
 // stamps[block][0..3] = memtime, memrealtime at the layer loop's start, then at its end
@@ -334,21 +779,70 @@ __global__ __launch_bounds__(kBlock, 2) void k_probe(const float* rows, const bf
     m = wave_max(m);
     if ((tid & 63) == 0) wmax[tid >> 6] = m;
     __syncthreads();
+    float inv_next = 1.f;
+    _Float16* planes = reinterpret_cast<_Float16*>(act) + 0;  // SHAPE 7: planes over the rows region
+    if constexpr (SHAPE == 7) {
+        // rows -> scaled planes (f32 rows of the probe input; the planes take 4 B per element)
+        const float sa = pow2_scale(fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3])));
+        inv_next = 1.f / sa;
+        float tmp[TM * HP / kBlock];
+        for (int t = 0; t < TM * HP / kBlock; ++t) {
+            const int i = tid + t * kBlock;
+            tmp[t] = act[(i / HP) * SS + i % HP] * sa;
+        }
+        __syncthreads();
+        for (int t = 0; t < TM * HP / kBlock; ++t) {
+            const int i = tid + t * kBlock;
+            const _Float16 hh = (_Float16)tmp[t];
+            planes[(i / HP) * PS2 + i % HP] = hh;
+            planes[(i / HP) * PS2 + i % HP + TM * PS2] = (_Float16)(tmp[t] - (float)hh);
+        }
+        __syncthreads();
+    }
     if (STAMP && tid == 0) {
         stamps[blockIdx.x * 4 + 0] = __builtin_amdgcn_s_memtime();
         stamps[blockIdx.x * 4 + 1] = __builtin_amdgcn_s_memrealtime();
     }
     for (int L = 0; L < LAYERS; ++L) {
-        if constexpr (SHAPE == 32) {
+        if constexpr (SHAPE == 7) {
+            f32x16 acc[2][2];
+            gemm32h_pre(planes, Bh, acc);
+            __syncthreads();  // every wave has read the planes
+            store_planes_h(acc, planes, wmax, colinv, inv_next);
+        } else if constexpr (SHAPE == 32) {
             f32x16 acc[2][2];
             gemm32(act, Bs, stage, acc);
             __syncthreads();
             store32(acc, act);
-        } else if constexpr (SHAPE == 3) {
+        } else if constexpr (SHAPE == 5) {
+            const float amax = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
+            const float sa = pow2_scale(amax), inva = 1.f / sa;
+            f32x4 acc[4][4];
+            gemm16h(act, Bh, reinterpret_cast<_Float16*>(stage), sa, acc);
+            __syncthreads();
+            const int lane = tid & 63, wv = wave_id();
+            float mm = 0.f;
+            for (int c = 0; c < 4; ++c) {
+                const float u = inva * colinv[wv * 64 + c * 16 + (lane & 15)];
+                for (int rt = 0; rt < 4; ++rt)
+                    for (int i = 0; i < 4; ++i) {
+                        acc[rt][c][i] = fmaxf(acc[rt][c][i] * u, 0.f);
+                        mm = fmaxf(mm, acc[rt][c][i]);
+                    }
+            }
+            store16(acc, act);
+            mm = wave_max(mm);
+            if (lane == 0) wmax[wv] = mm;
+        } else if constexpr (SHAPE == 3 || SHAPE == 4 || SHAPE == 6) {
             const float amax = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
             const float sa = pow2_scale(amax), inva = 1.f / sa;  // exact: powers of two
             f32x16 acc[2][2];
-            gemm32h(act, Bh, reinterpret_cast<_Float16*>(stage), sa, acc);
+            if constexpr (SHAPE == 3)
+                gemm32h(act, Bh, reinterpret_cast<_Float16*>(stage), sa, acc);
+            else if constexpr (SHAPE == 6)
+                gemm32h_db(act, Bh, reinterpret_cast<_Float16*>(stage), sa, acc);
+            else
+                gemm32h_k32(act, Bh, reinterpret_cast<_Float16*>(stage), sa, acc);
             __syncthreads();
             const int lane = tid & 63, wv = wave_id();
             float mm = 0.f;
@@ -375,8 +869,17 @@ __global__ __launch_bounds__(kBlock, 2) void k_probe(const float* rows, const bf
         stamps[blockIdx.x * 4 + 2] = __builtin_amdgcn_s_memtime();
         stamps[blockIdx.x * 4 + 3] = __builtin_amdgcn_s_memrealtime();
     }
-    if (blockIdx.x < 8)
-        for (int i = tid; i < TM * HP; i += kBlock) out[(size_t)blockIdx.x * TM * HP + i] = act[(i / HP) * SS + i % HP];
+    if (blockIdx.x < 8) {
+        if constexpr (SHAPE == 7) {
+            for (int i = tid; i < TM * HP; i += kBlock) {
+                const int o = (i / HP) * PS2 + i % HP;
+                out[(size_t)blockIdx.x * TM * HP + i] =
+                    ((float)planes[o] + (float)planes[o + TM * PS2]) * inv_next;
+            }
+        } else {
+            for (int i = tid; i < TM * HP; i += kBlock) out[(size_t)blockIdx.x * TM * HP + i] = act[(i / HP) * SS + i % HP];
+        }
+    }
 }
 
 static uint16_t bf16_rn(float x) {
@@ -475,18 +978,37 @@ int main(int argc, char** argv) {
     hipFuncSetAttribute((const void*)k_probe<16, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds16);
     hipFuncSetAttribute((const void*)k_probe<3, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds32);
     hipFuncSetAttribute((const void*)k_probe<3, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds32);
+    for (auto kf : {(const void*)k_probe<4, false>, (const void*)k_probe<4, true>, (const void*)k_probe<5, false>,
+                    (const void*)k_probe<5, true>, (const void*)k_probe<6, false>, (const void*)k_probe<6, true>,
+                    (const void*)k_probe<7, false>, (const void*)k_probe<7, true>})
+        hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds32);
+    for (auto kf : {(const void*)k_probe_w8<false>, (const void*)k_probe_w8<true>})
+        hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)((size_t)TM8 * SS * 4 + (size_t)TM8 * 16 * 2 * 2 + 64));
     for (int round = 0; round < 2; ++round)
-        for (int shape : {32, 16, 3}) {
+        for (int shape : {3, 8, 5}) {
             // FLOPs the matrix cores issue: 6 products (bf16 split) or 3 (fp16 split)
-            const double flop = 2.0 * TM * HP * HP * LAYERS * blocks * (shape == 3 ? 3 : 6);
+            const double flop = 2.0 * TM * HP * HP * LAYERS * blocks * (shape >= 3 && shape <= 8 ? 3 : 6);
             auto launch = [&](bool stamp) {
 #define L_(S, T) hipLaunchKernelGGL((k_probe<S, T>), dim3(blocks), dim3(kBlock), lds32, 0, d_rows, d_Bs, d_out, d_st, d_Bh, d_colinv)
                 if (shape == 32) {
                     if (stamp) L_(32, true); else L_(32, false);
                 } else if (shape == 16) {
                     if (stamp) L_(16, true); else L_(16, false);
-                } else {
+                } else if (shape == 3) {
                     if (stamp) L_(3, true); else L_(3, false);
+                } else if (shape == 4) {
+                    if (stamp) L_(4, true); else L_(4, false);
+                } else if (shape == 6) {
+                    if (stamp) L_(6, true); else L_(6, false);
+                } else if (shape == 7) {
+                    if (stamp) L_(7, true); else L_(7, false);
+                } else if (shape == 8) {
+                    const size_t l8 = (size_t)TM8 * SS * 4 + (size_t)TM8 * 16 * 2 * 2 + 64;
+                    if (stamp) hipLaunchKernelGGL((k_probe_w8<true>), dim3(blocks / 2), dim3(512), l8, 0, d_rows, d_out, d_st, d_Bh, d_colinv);
+                    else hipLaunchKernelGGL((k_probe_w8<false>), dim3(blocks / 2), dim3(512), l8, 0, d_rows, d_out, d_st, d_Bh, d_colinv);
+                } else {
+                    if (stamp) L_(5, true); else L_(5, false);
                 }
 #undef L_
             };
@@ -514,7 +1036,7 @@ int main(int argc, char** argv) {
             std::vector<unsigned long long> st((size_t)blocks * 4);
             hipMemcpy(st.data(), d_st, st.size() * 8, hipMemcpyDeviceToHost);
             std::vector<double> clk, cyc;
-            for (int b = 0; b < blocks; ++b) {
+            for (int b = 0; b < (shape == 8 ? blocks / 2 : blocks); ++b) {
                 const double dt = (double)(st[b * 4 + 2] - st[b * 4 + 0]);
                 const double dr = (double)(st[b * 4 + 3] - st[b * 4 + 1]);
                 if (dr > 0) {
@@ -535,7 +1057,7 @@ int main(int argc, char** argv) {
                    "\"bf16_TFs\": %.1f, \"frac_spec\": %.4f, \"clock_mhz_median\": %.0f, \"clock_mhz_p10\": %.0f, "
                    "\"clock_mhz_p90\": %.0f, \"wg_cycles_median\": %.0f, \"frac_at_held_clock\": %.4f, "
                    "\"err_rel\": %.3e, \"data\": %d}\n",
-                   round, shape == 32 ? "32x32x16" : shape == 16 ? "16x16x32" : "f16x3_32x32x16", blocks, warm, us, flop / us / 1e6,
+                   round, shape == 32 ? "32x32x16" : shape == 16 ? "16x16x32" : shape == 3 ? "f16x3_32x32x16" : shape == 4 ? "f16x3_32x32x16_k32stage" : shape == 6 ? "f16x3_32x32x16_dbstage_1barrier" : shape == 7 ? "f16x3_32x32x16_presplit_planes" : shape == 8 ? "f16x3_32x32x16_128rows_8waves" : "f16x3_16x16x32", blocks, warm, us, flop / us / 1e6,
                    flop / us / 1e6 / 2516.6, clk[clk.size() / 2], clk[clk.size() / 10], clk[clk.size() * 9 / 10],
                    cyc[cyc.size() / 2], flop / us / 1e6 / (2516.6 * clk[clk.size() / 2] / 2400.0), maxe / maxr, data);
             fflush(stdout);
