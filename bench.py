@@ -65,7 +65,8 @@ REGION_KERNEL = {"critic_rows": "k_td3_critic_rows", "actor_rows": "k_td3_actor_
 
 def pmc_traffic(region):
     """(bytes per launch, source) of the region's kernel from the committed PMC summary, else
-    (None, None)."""
+    (None, None). bytes per launch = WRITE_SIZE + FETCH_SIZE, the fetch doubled only for the
+    streaming kernels (tools/pmc_traffic.py); the source string carries the raw figure too."""
     try:
         with open(PMC_TRAFFIC) as f:
             t = json.load(f)
@@ -74,7 +75,8 @@ def pmc_traffic(region):
     k = t.get(REGION_KERNEL.get(region, ""))
     if not k:
         return None, None
-    return k["bytes_per_launch"], "profiles/pmc_traffic.json (%s)" % t["_meta"].get("command", "")
+    return k["bytes_per_launch"], "profiles/pmc_traffic.json (%s; raw %s B, fetch x%s)" % (
+        t["_meta"].get("command", ""), k.get("bytes_raw"), k.get("fetch_correction", 2.0))
 
 
 def parse():
