@@ -92,6 +92,8 @@ def parse():
     ap.add_argument("--envs-per-group", type=int, default=1024)
     ap.add_argument("--seed", type=int, default=1707366464)
     ap.add_argument("--shared-policy", action="store_true")
+    # shared policy: the next collect on a second stream beside the last epoch's all-reduce
+    ap.add_argument("--overlap-collect", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sweep", action="store_true")
     ap.add_argument("--no-utd-sweep", action="store_true")
@@ -321,7 +323,8 @@ def main():
     rank_batch = args.batch // ws if (args.shared_policy and ws > 1) else args.batch
     tr = VecTrainer(n_envs=args.envs, hidden=args.hidden, n_hidden=args.layers, batch=rank_batch,
                     updates_per_step=args.updates, seed=shard_seed(args.seed, rank),
-                    envs_per_group=args.envs_per_group, device=dev, grad_hook=hook)
+                    envs_per_group=args.envs_per_group, device=dev, grad_hook=hook,
+                    overlap_collect=args.overlap_collect and hook is not None)
     if args.shared_policy and ws > 1:  # same initial policy on every rank
         nets = list(tr.td3.networks().values())
         broadcast_params([n.params for n in nets])
@@ -442,7 +445,9 @@ def main():
                        "td3_epochs_per_step": args.updates,
                        "rank_batch": rank_batch,
                        "update_to_data": args.updates * args.batch / args.envs,
-                       "parallelism": ("dp%d-shared-policy" % ws if args.shared_policy and ws > 1
+                       "parallelism": ("dp%d-shared-policy%s" % (
+                                           ws, "-overlap-collect" if tr.overlap_collect else "")
+                                       if args.shared_policy and ws > 1
                                        else "independent-env-blocks x%d" % ws)},
             "roofline": roof,
             "step_kernel": step_k,

@@ -98,6 +98,8 @@ class TD3:
         self._st = None
         self._st_key = None
         self._rd = (None, None)
+        # td3_update's collect_ready event while it is still to be recorded (_hook / the end)
+        self._ready, self._ready_recorded = None, False
         self.actor_losses, self.critic_losses = [], []
 
     # ---- workspace, sized per batch
@@ -293,6 +295,9 @@ class TD3:
     def _hook(self, bucket, stream):
         # the collective runs on torch's current stream: make it the launch stream, so it starts
         # after the reduce and Adam starts after it
+        if self._ready is not None:  # the last epoch's replay reads and actor writes are issued
+            self._ready.record(stream)
+            self._ready, self._ready_recorded = None, True
         if stream is None:
             self.grad_hook(bucket)
         else:
@@ -484,11 +489,28 @@ class TD3:
 
     # robot.py:258-285
     def td3_update(self, replay, num_epochs=None, idx_fn=None, eps_fn=None, stream=None,
-                   track_losses=False):
+                   track_losses=False, collect_ready=None):
+        """`collect_ready` (a torch.cuda.Event, optional) is recorded on `stream` at the first
+        point after which nothing this update still has to issue reads the replay ring or writes
+        the actor: with a grad_hook and a final epoch that is not a policy epoch, just before
+        that epoch's critic all-reduce (so the next collect can run beside the collective and
+        the critics' Adam step), otherwise at the end."""
         n = self.cfg.num_epochs if num_epochs is None else num_epochs
+        self._ready, self._ready_recorded = None, False
+        try:
+            self._update(replay, n, idx_fn, eps_fn, stream, track_losses, collect_ready)
+        finally:
+            self._ready = None
+            if collect_ready is not None and not self._ready_recorded:
+                collect_ready.record(stream)
+
+    def _update(self, replay, n, idx_fn, eps_fn, stream, track_losses, collect_ready):
         if len(replay) < 1:
             return
         for epoch in range(n):
+            if (collect_ready is not None and epoch == n - 1 and self.grad_hook is not None and
+                    epoch % self.cfg.policy_update_delay != 0):
+                self._ready = collect_ready
             self.train_critic(replay, idx=idx_fn() if idx_fn else None,
                               eps=eps_fn() if eps_fn else None, stream=stream)
             if track_losses:

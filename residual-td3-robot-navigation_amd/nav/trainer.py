@@ -26,7 +26,7 @@ from .vec_env import ReplayRing, VecEnv
 class VecTrainer:
     def __init__(self, n_envs=65536, hidden=256, n_hidden=2, batch=32768, updates_per_step=2,
                  replay_capacity=None, seed=K.RANDOM_SEED, envs_per_group=1024, demos=True,
-                 device="cuda", field=None, grad_hook=None, fuse_tick=True):
+                 device="cuda", field=None, grad_hook=None, fuse_tick=True, overlap_collect=False):
         self.n = int(n_envs)
         self.device = torch.device(device)
         self.seed = int(seed)
@@ -57,6 +57,14 @@ class VecTrainer:
         # act + tick fused into one launch (False: the two launches; A/B and the fused-vs-unfused
         # parity test)
         self.fuse_tick = bool(fuse_tick)
+        # shared policy: the next step's collect on a second stream beside the last epoch's
+        # critic all-reduce and Adam step (bit-identical either way). Off by default: the two
+        # cross-stream waits per step cost ~24 us on one MI355X (profiles/r05u_shared_policy_host
+        # .json), so it pays only where the collective itself takes longer than that.
+        self.overlap_collect = bool(overlap_collect)
+        self._side = None
+        self._collect_ready = None  # recorded by the last learn() (td3_update collect_ready)
+        self._collected = None
 
     # robot.py:541-569 for every env
     def act(self, training=True, stream=None):
@@ -78,13 +86,43 @@ class VecTrainer:
             self.env.agent_step(self.action, self.replay, stream)
         self.steps += 1
 
-    def learn(self, stream=None):
+    def learn(self, stream=None, collect_ready=None):
         if len(self.replay) >= self.td3.cfg.batch_size and self.updates_per_step > 0:
-            self.td3.td3_update(self.replay, self.updates_per_step, stream=stream)
+            self.td3.td3_update(self.replay, self.updates_per_step, stream=stream,
+                                collect_ready=collect_ready)
+        elif collect_ready is not None:
+            collect_ready.record(stream)
 
     def step(self, stream=None):
-        self.collect(stream)
-        self.learn(stream)
+        if not self.overlap_collect or prof._active is not None:
+            self.sync_collect()
+            self.collect(stream)
+            self.learn(stream)
+            return
+        # overlapped form (shared policy): this collect reads only the actor and the env state
+        # and writes the env state and the replay ring, so it may start once the previous learn
+        # has issued its last replay read and actor write (td3_update's collect_ready: before
+        # the final critic-only epoch's all-reduce); the learn waits for the collect
+        main = stream if stream is not None else torch.cuda.current_stream(self.device)
+        if self._side is None:
+            self._side = torch.cuda.Stream(self.device)
+            self._collected = torch.cuda.Event()
+        side = self._side
+        if self._collect_ready is None:
+            side.wait_stream(main)
+        else:
+            side.wait_event(self._collect_ready)
+        self.collect(side)
+        self._collected.record(side)
+        main.wait_event(self._collected)
+        if self._collect_ready is None:
+            self._collect_ready = torch.cuda.Event()
+        self.learn(main, self._collect_ready)
+
+    def sync_collect(self):
+        """Make the next step's collect wait for everything issued on the current stream (after
+        host-side changes to the env state, the replay ring or the actor between steps)."""
+        self._collect_ready = None
 
     def env_steps(self):
         return self.steps * self.n
@@ -129,6 +167,7 @@ class VecTrainer:
         self.td3.load_state_dict(sd["td3"])
         self.steps = int(m["steps"])
         self.updates_per_step = int(m["updates_per_step"])
+        self.sync_collect()
 
     @classmethod
     def from_state_dict(cls, sd, device="cuda", grad_hook=None):

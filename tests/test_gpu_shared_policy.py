@@ -451,3 +451,90 @@ def test_shared_policy_through_real_collective_two_processes():
         d = float(np.abs(a - f.params.cpu().numpy()).max())
         print(f"{name}: max |diff| vs full batch {d:.3e}")
         assert d <= 2e-7, name
+
+
+def _overlap_worker(rank, ws, port, steps, q):
+    """One rank of the overlapped-collect check: the same shared-policy VecTrainer run twice in
+    this process, with and without the next collect beside the last epoch's critic all-reduce
+    (gloo), returning every parameter, the replay ring and the env state of both runs."""
+    import os
+    import sys
+    import torch.distributed as dist
+    from conftest import PKG, ROOT
+    for p in (ROOT, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    try:
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=ws)
+        from nav.dist import broadcast_params, make_grad_hook, shard_seed
+        from nav.trainer import VecTrainer
+        out = {}
+        for overlap in (True, False):
+            hook = make_grad_hook(ws)
+            tr = VecTrainer(n_envs=2048, hidden=256, n_hidden=2, batch=1024, updates_per_step=2,
+                            seed=shard_seed(2024, rank), envs_per_group=1024, device=DEV,
+                            grad_hook=hook, overlap_collect=overlap)
+            assert tr.overlap_collect is overlap
+            nets = list(tr.td3.networks().values())
+            broadcast_params([n.params for n in nets])
+            for n in nets:
+                n.pack()
+            for _ in range(steps):
+                tr.step()
+            torch.cuda.synchronize()
+            res = {k: n.params.cpu().numpy() for k, n in tr.td3.networks().items()}
+            res["replay"] = tr.replay.rows.cpu().numpy()
+            for k in tr.ENV_STATE:
+                res["env_" + k] = getattr(tr.env, k).cpu().numpy()
+            out[overlap] = (res, hook.calls)
+        q.put((rank, out))
+        dist.destroy_process_group()
+    except BaseException as ex:
+        q.put((rank, repr(ex)))
+        raise
+
+
+def test_overlapped_collect_bit_identical_two_processes():
+    """VecTrainer's overlapped step (shared policy: step k+1's collect on a second stream from
+    td3_update's collect_ready event, beside step k's final critic all-reduce and Adam step)
+    against the serial step, two processes over gloo on this GPU: every parameter, the replay ring
+    and the env state bit-identical per rank, and the ranks' parameters identical to each other
+    (robot.py:272-285 schedule: critic every epoch, actor on even epochs)."""
+    import socket
+    import torch.multiprocessing as mp
+    from nav import _lib
+    _lib.require_gpu()
+    steps = 8
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_overlap_worker, args=(r, 2, port, steps, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in range(2):
+            r, out = q.get(timeout=240)
+            assert not isinstance(out, str), out
+            res[r] = out
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    assert all(p.exitcode == 0 for p in procs)
+    for r in range(2):
+        on, calls_on = res[r][True]
+        off, calls_off = res[r][False]
+        assert calls_on == calls_off > 0
+        for k in off:
+            assert np.array_equal(on[k], off[k]), (r, k)
+    for k in ("actor", "critic1", "critic2", "target_actor", "target_critic1", "target_critic2"):
+        assert np.array_equal(res[0][True][0][k], res[1][True][0][k]), k
+    # the ranks' env blocks are independent (seed + rank)
+    assert not np.array_equal(res[0][True][0]["replay"], res[1][True][0]["replay"])

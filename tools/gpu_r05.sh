@@ -46,6 +46,7 @@ for step in "$@"; do
     tests) run gputest 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     alltests) run gputest_all 600 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread ;;
     acc) run accuracy 300 python -u -m pytest tests/test_gpu_mlp.py -m gpu -k "split_gemm_f32_accuracy or gradients_vs_reference or weight_grads_2layer" -v -s --timeout 120 --timeout-method thread ;;
+    sptests) run sptest 400 python -u -m pytest tests/test_gpu_shared_policy.py tests/test_gpu_checkpoint.py -m gpu -x -v --timeout 240 --timeout-method thread ;;
     dbgw) run dbg_wgrad 200 python tools/dbg_wgrad.py ;;
     mlptests) run mlptest 300 python -u -m pytest tests/test_gpu_mlp.py tests/test_gpu_fullsize.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;

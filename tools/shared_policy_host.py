@@ -4,7 +4,9 @@ At 8 ranks each rank runs 65 536 envs and samples B / 8 = 4 096 rows per epoch, 
 epoch is short and the host's issue of the learner launches can dominate. This times the bench
 step (one collect + 2 TD3 epochs, UTD 1) at rank batch 4 096 with an in-process hook that carries
 world_size = 8 but moves no data (the collective itself is not timed: it is the driver's 8-GPU
-run), against the hook-free learner at the same batch, interleaved, on one box.
+run), against the hook-free learner at the same batch, interleaved, on one box. "hook_overlap" adds
+overlap_collect=True (the next collect on a second stream beside the last epoch's all-reduce and
+critic Adam step), which here has no collective to hide and shows the cross-stream cost alone.
 
 python tools/shared_policy_host.py [--batch 4096] [--steps 200] [--rounds 3]
 """
@@ -45,6 +47,9 @@ def main():
                               envs_per_group=1024),
         "hook": VecTrainer(n_envs=65536, batch=args.batch, updates_per_step=2,
                            envs_per_group=1024, grad_hook=IdentityHook(args.world)),
+        "hook_overlap": VecTrainer(n_envs=65536, batch=args.batch, updates_per_step=2,
+                                   envs_per_group=1024, grad_hook=IdentityHook(args.world),
+                                   overlap_collect=True),
     }
     for tr in arms.values():
         for _ in range(10):
@@ -63,6 +68,7 @@ def main():
     out = {"batch": args.batch, "world_size_carried": args.world, "steps": args.steps,
            "ms_per_step": res, "best_ms": best,
            "hook_overhead": best["hook"] / best["no_hook"] - 1.0,
+           "hook_overlap_overhead": best["hook_overlap"] / best["no_hook"] - 1.0,
            "hook_calls": arms["hook"].td3.grad_hook.calls}
     print(json.dumps(out, indent=1))
 
