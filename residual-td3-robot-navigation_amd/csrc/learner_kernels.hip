@@ -49,6 +49,24 @@ struct WgradArgs {
     int64_t per_wave;       // rows per wave (multiple of 64)
 };
 
+// Phase probe of the weight-gradient kernels (variant builds with -DNAV_WGRAD_TRACE only;
+// tools/wgrad_trace.py): s_memtime per wave at numbered marks of 4 workgroups (blocks 0, 1, 128,
+// 255) per kernel (0 k_wgrad_fact, 1 k_wgrad); the last launch of each kernel wins.
+#ifdef NAV_WGRAD_TRACE
+__device__ unsigned long long g_wgrad_trace[2][4][8][8];
+#define WG_MARK(kid, k)                                                                        \
+    do {                                                                                       \
+        const int b_ = blockIdx.x == 0 ? 0 : blockIdx.x == 1 ? 1 : blockIdx.x == 128 ? 2         \
+                       : blockIdx.x == 255 ? 3 : -1;                                           \
+        if (b_ >= 0 && (threadIdx.x & 63) == 0)                                                \
+            g_wgrad_trace[kid][b_][threadIdx.x >> 6][k] = __builtin_readcyclecounter();         \
+    } while (0)
+#else
+#define WG_MARK(kid, k) \
+    do {                \
+    } while (0)
+#endif
+
 constexpr int WG_WAVES = 8;
 constexpr int WG_TOTAL = 256;  // workgroups that fill the chip (one 8-wave workgroup per CU)
 constexpr int WG_THREADS = WG_WAVES * 64;
@@ -208,15 +226,59 @@ NAV_DEV void row_maxima(const WgradArgs& a, int y, int64_t r_lo, int64_t r_hi, f
                         float (&X)[4]) {
     const int lane = threadIdx.x & 63, d_in = a.net[y].d_in, d_out = a.net[y].d_out;
     float g0 = 0.f, g1 = 0.f, x0 = 0.f, x1 = 0.f, x2 = 0.f, x3 = 0.f;
-    for (int64_t r = r_lo + lane; r < r_hi; r += 64) {
-        const float* g = a.dy[y] + r * a.ld_dy;
-        const float* x = a.in + r * a.ld_in + a.in_col;
-        g0 = fmaxf(g0, fabsf(g[0]));
-        if (d_out > 1) g1 = fmaxf(g1, fabsf(g[1]));
-        x0 = fmaxf(x0, fabsf(x[0]));
-        if (d_in > 1) x1 = fmaxf(x1, fabsf(x[1]));
-        if (d_in > 2) x2 = fmaxf(x2, fabsf(x[2]));
-        if (d_in > 3) x3 = fmaxf(x3, fabsf(x[3]));
+    // RU rows per lane per trip, every load of a trip issued before the first max (one memory
+    // round trip per 64 RU rows), whole-row vector loads where the layout allows (the rows are
+    // 32 B apart in the learner's batch: one load instruction per row instead of d_in)
+    constexpr int RU = 4;
+    const float* xin = a.in + a.in_col;
+    const bool xv4 = d_in == 4 && (a.ld_in & 3) == 0 && ((uintptr_t)xin & 15) == 0;
+    const bool xv2 = d_in == 2 && (a.ld_in & 1) == 0 && ((uintptr_t)xin & 7) == 0;
+    const bool gv2 = d_out == 2 && (a.ld_dy & 1) == 0 && ((uintptr_t)a.dy[y] & 7) == 0;
+#ifdef NAV_WG_TIMING_NOMAX  // timing-only variant (wrong results): no pre-pass loads
+    g0 = g1 = lane == 0 ? 1e-4f : 0.f;
+    x0 = x1 = x2 = x3 = lane == 0 ? 100.f : 0.f;
+    if (r_hi < 0)  // never
+#endif
+    for (int64_t rb = r_lo; rb < r_hi; rb += 64 * RU) {
+        float gv[RU][2], xv[RU][4];
+#pragma unroll
+        for (int u = 0; u < RU; ++u) {
+            gv[u][0] = gv[u][1] = 0.f;
+            xv[u][0] = xv[u][1] = xv[u][2] = xv[u][3] = 0.f;
+            if (rb + 64 * u >= r_hi) continue;  // wave-uniform
+            const int64_t r = rb + 64 * u + lane;
+            if (r >= r_hi) continue;
+            const float* g = a.dy[y] + r * a.ld_dy;
+            const float* x = xin + r * a.ld_in;
+            if (gv2) {
+                const float2 v = *reinterpret_cast<const float2*>(g);
+                gv[u][0] = v.x;
+                gv[u][1] = v.y;
+            } else {
+                gv[u][0] = g[0];
+                if (d_out > 1) gv[u][1] = g[1];
+            }
+            if (xv4) {
+                const float4 v = *reinterpret_cast<const float4*>(x);
+                xv[u][0] = v.x; xv[u][1] = v.y; xv[u][2] = v.z; xv[u][3] = v.w;
+            } else if (xv2) {
+                const float2 v = *reinterpret_cast<const float2*>(x);
+                xv[u][0] = v.x; xv[u][1] = v.y;
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (d_in > i) xv[u][i] = x[i];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < RU; ++u) {
+            g0 = fmaxf(g0, fabsf(gv[u][0]));
+            g1 = fmaxf(g1, fabsf(gv[u][1]));
+            x0 = fmaxf(x0, fabsf(xv[u][0]));
+            x1 = fmaxf(x1, fabsf(xv[u][1]));
+            x2 = fmaxf(x2, fabsf(xv[u][2]));
+            x3 = fmaxf(x3, fabsf(xv[u][3]));
+        }
     }
     // wave-uniform: scalar registers
     auto su = [](float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(wave_max_abs(v)))); };
@@ -274,27 +336,6 @@ NAV_DEV void wgrad_rows_mfma(const WgradArgs& a, int y, int n0, int k0, int64_t 
         }
     }
     if (r_lo >= r_hi) return;
-    // fp16 operand scales (mlp_common.h), folded into the operand MFMAs' constants (a power of two
-    // commutes with every rounding of the f32 chains): P column tile i by 2^ep[i] from the bound
-    // sum_d max|g_d| |Wo[d][n]| (max over the tile's 32 n), Q column k by 2^eq[j] from h0_bound
-    int ep[2], eq[2];
-    {
-        float G[2], X[4];
-        row_maxima(a, y, r_lo, r_hi, G, X);
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            float b = G[h] * fabsf(wob[i]);
-            b += __shfl_xor(b, 32, 64);
-#pragma unroll
-            for (int m = 1; m < 32; m <<= 1) b = fmaxf(b, __shfl_xor(b, m, 64));
-            ep[i] = pow2_exp(b);
-            wob[i] = ldexpf(wob[i], ep[i]);
-            eq[i] = pow2_exp(h0_bound(X, w0b[i][0], w0b[i][1], bob[i]));
-            w0b[i][0] = ldexpf(w0b[i][0], eq[i]);
-            w0b[i][1] = ldexpf(w0b[i][1], eq[i]);
-            bob[i] = ldexpf(bob[i], eq[i]);
-        }
-    }
     const float one = h == 0 ? 1.f : 0.f;
     const uint16_t* mk = a.masks[y] + (size_t)(nh - 1) * mask_rowtiles(M) * NTm * 64 +
                          (size_t)(n0 >> 5) * 64 + lane;
@@ -376,7 +417,35 @@ NAV_DEV void wgrad_rows_mfma(const WgradArgs& a, int y, int n0, int k0, int64_t 
     Raw cur = load(r_lo);
     Raw nxt = cur;
     if (r_lo + 32 < r_hi) nxt = load(r_lo + 32);
+    // (the first two tiles' loads are in flight under the bound pre-pass)
+    // fp16 operand scales (mlp_common.h), folded into the operand MFMAs' constants (a power of two
+    // commutes with every rounding of the f32 chains): P column tile i by 2^ep[i] from the bound
+    // sum_d max|g_d| |Wo[d][n]| (max over the tile's 32 n), Q column k by 2^eq[j] from h0_bound
+    int ep[2], eq[2];
+    {
+        float G[2], X[4];
+        WG_MARK(1, 2);
+        row_maxima(a, y, r_lo, r_hi, G, X);
+        WG_MARK(1, 3);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            float b = G[h] * fabsf(wob[i]);
+            b += __shfl_xor(b, 32, 64);
+#pragma unroll
+            for (int m = 1; m < 32; m <<= 1) b = fmaxf(b, __shfl_xor(b, m, 64));
+            ep[i] = pow2_exp(b);
+            wob[i] = ldexpf(wob[i], ep[i]);
+            eq[i] = pow2_exp(h0_bound(X, w0b[i][0], w0b[i][1], bob[i]));
+            w0b[i][0] = ldexpf(w0b[i][0], eq[i]);
+            w0b[i][1] = ldexpf(w0b[i][1], eq[i]);
+            bob[i] = ldexpf(bob[i], eq[i]);
+        }
+    }
     for (int64_t rt = r_lo; rt < r_hi; rt += 32) {
+#ifdef NAV_WG_PINGPONG
+        if ((((rt - r_lo) >> 5) + (wave_id() >> 2)) & 1) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+#endif
         Raw nn = nxt;
         if (rt + 64 < r_hi) nn = load(rt + 64);
         f32x16 P[2], Q[2];
@@ -407,6 +476,7 @@ NAV_DEV void wgrad_rows_mfma(const WgradArgs& a, int y, int n0, int k0, int64_t 
         cur = nxt;
         nxt = nn;
     }
+    WG_MARK(1, 4);
     // unscale: tile (i, j) by 2^-(ep[i] + eq[j]) (eq per lane column), exact
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -464,29 +534,8 @@ NAV_DEV void wgrad_rows_fact(const WgradArgs& a, int y, int n0, int k0, int64_t 
             bob[j] = h == 0 ? bb[c] : 0.f;
         }
     }
-    // the fp16 scales of Q_d = relu(h_0) g_d: h_0 column half j by 2^eh[j] (folded into the
-    // layer-0 constants: a power of two commutes with the fma chain's roundings), g_d by 2^eg[d]
-    int eh[2], eg[D];
+    int eh[2], eg[D];  // the fp16 operand scales (below, under the first tile's loads)
     float sg[D];
-    {
-        float G[2], X[4];
-        row_maxima(a, y, r_lo, r_hi, G, X);
-        // per 32-column half (wave-uniform, scalar registers: the 128-accumulator program has no
-        // vector register to spare)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            eh[j] = __builtin_amdgcn_readfirstlane(
-                pow2_exp_to(wave_max_abs(h0_bound(X, w0b[j][0], w0b[j][1], bob[j])), 7));
-            w0b[j][0] = ldexpf(w0b[j][0], eh[j]);
-            w0b[j][1] = ldexpf(w0b[j][1], eh[j]);
-            bob[j] = ldexpf(bob[j], eh[j]);
-        }
-#pragma unroll
-        for (int d = 0; d < D; ++d) {
-            eg[d] = pow2_exp_to(G[d], 8);
-            sg[d] = ldexpf(1.f, eg[d]);
-        }
-    }
     const float one = h == 0 ? 1.f : 0.f;
     const bool x23 = d_in > 2;
     const size_t mstride = (size_t)NTm * 64;
@@ -501,11 +550,19 @@ NAV_DEV void wgrad_rows_fact(const WgradArgs& a, int y, int n0, int k0, int64_t 
         float x0, x1;
         uint32_t m[NI];
     };
+    // the x row as one 16-B load when it is 4 aligned floats (both lane halves read the row)
+    const bool xrow4 = d_in == 4 && (ld_in & 3) == 0 && (((uintptr_t)(a.in + a.in_col)) & 15) == 0;
     auto load_raw = [&](int64_t rt, Raw& v) {
         const int64_t rx = rt + l32 < r_hi ? rt + l32 : r_lo;  // absent rows read row r_lo
         const float* x = a.in + a.in_col + rx * ld_in;
-        v.x0 = x[xk0];
-        v.x1 = x[xk1];
+        if (xrow4) {
+            const float4 u = *reinterpret_cast<const float4*>(x);
+            v.x0 = h ? u.y : u.x;
+            v.x1 = h ? u.w : u.z;
+        } else {
+            v.x0 = x[xk0];
+            v.x1 = x[xk1];
+        }
         const uint16_t* m = mp + (size_t)((rt - r_lo) >> 5) * mstride;
 #pragma unroll
         for (int i = 0; i < NI; ++i) v.m[i] = m[i * 64];
@@ -575,6 +632,10 @@ NAV_DEV void wgrad_rows_fact(const WgradArgs& a, int y, int n0, int k0, int64_t 
                         for (int d = 0; d < D; ++d) gs[s2][d][4 * qq + t] = g[t * ld_dy + d];
                 }
             }
+    };
+    // D = 2: the g scales on the loaded values (D = 1 folds them into the layer-0 constants)
+    auto scale_g = [&](float (&gs)[2][D][8]) {
+        if (D == 1) return;
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
@@ -582,19 +643,56 @@ NAV_DEV void wgrad_rows_fact(const WgradArgs& a, int y, int n0, int k0, int64_t 
 #pragma unroll
                 for (int t = 0; t < 8; ++t) gs[s2][d][t] *= sg[d];
     };
+    // d_out = 2 loads its 32 g values at the tile (prefetched they do not fit the registers)
+    constexpr bool GPF = D == 1;
+    Raw cur, nxt;
+    float gc[2][D][8], gn[2][D][8];
     if (r_lo < r_full) {
-        // d_out = 2 loads its 32 g values at the tile (prefetched they do not fit the registers)
-        constexpr bool GPF = D == 1;
-        Raw cur, nxt;
-        float gc[2][D][8], gn[2][D][8];
         load_raw(r_lo, cur);
         if (GPF) load_g(r_lo, gc);
+    }
+    // the fp16 scales of Q_d = relu(h_0) g_d: h_0 column half j by 2^eh[j] (folded into the
+    // layer-0 constants: a power of two commutes with the fma chain's roundings), g_d by 2^eg[d]
+    // (D = 1: folded into the same constants, so the g rows are used as loaded; D = 2: applied
+    // to the loaded g values). Computed under the first tile's loads.
+    {
+        float G[2], X[4];
+        WG_MARK(0, 2);
+        row_maxima(a, y, r_lo, r_hi, G, X);
+        WG_MARK(0, 3);
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            eg[d] = pow2_exp_to(G[d], 8);
+            sg[d] = D == 1 ? 1.f : ldexpf(1.f, eg[d]);
+        }
+        // per 32-column half (wave-uniform, scalar registers: the 128-accumulator program has no
+        // vector register to spare)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            eh[j] = __builtin_amdgcn_readfirstlane(
+                pow2_exp_to(wave_max_abs(h0_bound(X, w0b[j][0], w0b[j][1], bob[j])), 7));
+            // (the sum capped at 2^120: Z = h_0 2^eh stays finite for every finite h_0 bound)
+            if (D == 1) eh[j] = min(max(eh[j] + eg[0], -126), 120);
+            w0b[j][0] = ldexpf(w0b[j][0], eh[j]);
+            w0b[j][1] = ldexpf(w0b[j][1], eh[j]);
+            bob[j] = ldexpf(bob[j], eh[j]);
+        }
+        if (D == 1) eg[0] = 0;
+    }
+    if (r_lo < r_full) {
         for (int64_t rt = r_lo; rt < r_full; rt += 32) {
+#ifdef NAV_WG_PINGPONG  // A/B variant: the two waves of a SIMD take turns at the higher priority
+            if ((((rt - r_lo) >> 5) + (wave_id() >> 2)) & 1) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
+#endif
             if (rt + 32 < r_full) {
                 load_raw(rt + 32, nxt);
                 if (GPF) load_g(rt + 32, gn);
             }
-            if (!GPF) load_g(rt, gc);
+            if (!GPF) {
+                load_g(rt, gc);
+                scale_g(gc);
+            }
             tile(cur, gc);
             cur = nxt;
             if (GPF) {
@@ -607,6 +705,7 @@ NAV_DEV void wgrad_rows_fact(const WgradArgs& a, int y, int n0, int k0, int64_t 
             }
         }
     }
+    WG_MARK(0, 4);
     if (r_full < r_hi) {  // the last, partial tile of the rows (M % 32 rows)
         Raw cur;
         load_raw(r_full, cur);
@@ -654,6 +753,12 @@ NAV_DEV void wgrad_rows_fact(const WgradArgs& a, int y, int n0, int k0, int64_t 
 
 // The NI tiles of each wave summed across the 8 waves through LDS (R slots of NI*32 x 64 floats
 // in 128 KB: waves w and w + R share slot w % R, in wave order) and written as one slab tile.
+// Slot layout: per 32 x 32 block (i, j) and lane, the lane's 16 accumulator values contiguous
+// (16-B LDS accesses, 4 per block instead of 16 single-dword ones), the 4 chunks of a lane
+// rotated by (lane >> 2) & 3 so the 8 lanes of one LDS cycle hit distinct banks. The final pass
+// gives wave w the blocks w, w + 8, ...: 16 values per lane summed over the slots in slot order
+// (the same order as p_0 + p_R + p_1 + ... of a row-major slot), each stored to 32 consecutive
+// columns of a slab row per lane half.
 template <int NI>
 NAV_DEV void wgrad_reduce_write(const WgradArgs& a, int y, int split, int L, int n0, int k0,
                                 const f32x16 (&acc)[NI][2], float* red) {
@@ -663,29 +768,54 @@ NAV_DEV void wgrad_reduce_write(const WgradArgs& a, int y, int split, int L, int
     const MlpDev& net = a.net[y];
     const int hp = net.hp;
     const int wv = wave_id(), lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
-    float* mine = red + (wv % R) * T;
+    const int rot = (lane >> 2) & 3;
+    float4* mine = reinterpret_cast<float4*>(red + (wv % R) * T);
 #pragma unroll
     for (int round = 0; round < WG_WAVES / R; ++round) {
         if (wv / R == round) {
 #pragma unroll
             for (int i = 0; i < NI; ++i)
 #pragma unroll
-                for (int j = 0; j < 2; ++j)
+                for (int j = 0; j < 2; ++j) {
+                    float4* p = mine + ((i * 2 + j) * 64 + lane) * 4;
 #pragma unroll
-                    for (int e = 0; e < 16; ++e) {
-                        float* p = mine + (32 * i + acc_row(e, h)) * WG_TILE + 32 * j + l32;
-                        *p = round ? *p + acc[i][j][e] : acc[i][j][e];
+                    for (int c = 0; c < 4; ++c) {
+                        float4 v = make_float4(acc[i][j][4 * c], acc[i][j][4 * c + 1],
+                                               acc[i][j][4 * c + 2], acc[i][j][4 * c + 3]);
+                        if (round) {
+                            const float4 o = p[c ^ rot];
+                            v = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
+                        }
+                        p[c ^ rot] = v;
                     }
+                }
         }
         __syncthreads();
     }
     float* o = a.slabs[y] + (int64_t)split * hidden_w_count(net) + (int64_t)(L - 1) * hp * hp;
-    for (int idx = threadIdx.x; idx < T; idx += WG_THREADS) {
-        const int m = idx / WG_TILE, c = idx % WG_TILE;
-        float s = red[idx];
+    const float4* slots = reinterpret_cast<const float4*>(red);
+    for (int b = wv; b < NI * 2; b += WG_WAVES) {
+        const int i = b >> 1, j = b & 1;
+        float v[16];
 #pragma unroll
-        for (int w = 1; w < R; ++w) s += red[w * T + idx];
-        if (n0 + m < hp && k0 + c < hp) o[(int64_t)(n0 + m) * hp + k0 + c] = s;
+        for (int w = 0; w < R; ++w) {
+            const float4* p = slots + (size_t)w * (T / 4) + (b * 64 + lane) * 4;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const float4 u = p[c ^ rot];
+                if (w == 0) {
+                    v[4 * c] = u.x; v[4 * c + 1] = u.y; v[4 * c + 2] = u.z; v[4 * c + 3] = u.w;
+                } else {
+                    v[4 * c] += u.x; v[4 * c + 1] += u.y; v[4 * c + 2] += u.z; v[4 * c + 3] += u.w;
+                }
+            }
+        }
+        const int col = k0 + 32 * j + l32;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int n = n0 + 32 * i + acc_row(e, h);
+            if (n < hp && col < hp) o[(int64_t)n * hp + col] = v[e];
+        }
     }
 }
 
@@ -720,6 +850,7 @@ NAV_DEV void wave_rows(const WgradArgs& a, int split, int wv, int64_t& r_lo, int
 
 template <int NI, int D>
 NAV_DEV void wgrad_tile_fact(const WgradArgs& a, const TileJob& t, float* smem) {
+    WG_MARK(0, 0);
     // the bits -> A fragment table at LDS offset 0: entry b, dword d holds fp16 2.0 (0x4000) in its
     // low half when bit 2d of b is set and in its high half when bit 2d + 1 is
     uint4* tab = reinterpret_cast<uint4*>(smem);
@@ -732,16 +863,20 @@ NAV_DEV void wgrad_tile_fact(const WgradArgs& a, const TileJob& t, float* smem) 
         tab[b] = make_uint4(w[0], w[1], w[2], w[3]);
     }
     __syncthreads();
+    WG_MARK(0, 1);
     int64_t r_lo, r_hi;
     wave_rows(a, t.split, wave_id(), r_lo, r_hi);
     f32x16 out[NI][2];
     wgrad_rows_fact<NI, D>(a, t.y, t.n0, t.k0, r_lo, r_hi, reinterpret_cast<const char*>(tab), out);
+    WG_MARK(0, 5);
     wgrad_reduce_write<NI>(a, t.y, t.split, t.L, t.n0, t.k0, out, smem + 1024);
+    WG_MARK(0, 6);
 }
 
 // The tile job's partial over its split's rows, written as one slab tile (8 waves' partials
 // summed in wave order)
 NAV_DEV void wgrad_tile(const WgradArgs& a, const TileJob& t, float* smem) {
+    WG_MARK(1, 0);
     const int y = t.y, split = t.split, L = t.L, n0 = t.n0, k0 = t.k0;
     const int nh = a.net[y].n_hidden;
     const int wv = wave_id();
@@ -764,7 +899,9 @@ NAV_DEV void wgrad_tile(const WgradArgs& a, const TileJob& t, float* smem) {
     else if (qr) wgrad_rows<false, true>(a, y, L, n0, k0, r_lo, r_hi, stage, acc);
     else wgrad_rows<false, false>(a, y, L, n0, k0, r_lo, r_hi, stage, acc);
     // the 8 partial tiles meet in LDS, summed in wave order
+    WG_MARK(1, 5);
     wgrad_reduce_write<2>(a, y, split, L, n0, k0, acc, red);
+    WG_MARK(1, 6);
 }
 
 // grid: nets x tile jobs x splits workgroups of 8 waves (one kernel per path: each gets its own
@@ -1628,3 +1765,12 @@ int nav_strided_copy(const float* src, int32_t ld_src, int32_t col_src, float* d
 }
 
 }  // extern "C"
+
+#ifdef NAV_WGRAD_TRACE
+extern "C" int nav_wgrad_trace_read(unsigned long long* host, int n) {
+    const size_t bytes = sizeof(g_wgrad_trace);
+    if (!host || (size_t)n * sizeof(unsigned long long) < bytes) return NAV_EINVAL;
+    const hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wgrad_trace), bytes);
+    return e == hipSuccess ? 0 : -(int)e;
+}
+#endif

@@ -84,6 +84,10 @@ for step in "$@"; do
              run phase_${v}_16448 200 python "${W[@]}" tools/phase_trace.py --batch 16448
              run phase_${v}_tick 200 python "${W[@]}" tools/phase_trace.py --tick
            done ;;
+    wtrace) for v in ${TVARS:-wtrace}; do
+              run ${v}_32k 200 python tools/withlib.py "$ROOT/abl/libnavenv_$v.so" tools/wgrad_trace.py &&
+              run ${v}_16k 200 python tools/withlib.py "$ROOT/abl/libnavenv_$v.so" tools/wgrad_trace.py --batch 16384
+            done ;;
     clock) run clock 200 python tools/withlib.py "$ROOT/abl/libnavenv_clock.so" tools/clock_probe.py --seconds 3 ;;
     sphost) run sphost 300 python tools/shared_policy_host.py ;;
     shape) run shape 200 ./build/mfma_shape_probe 512 2.5 0 && run shape_dz 200 ./build/mfma_shape_probe 512 2.5 1 ;;
