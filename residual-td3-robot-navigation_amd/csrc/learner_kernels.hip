@@ -442,10 +442,6 @@ NAV_DEV void wgrad_rows_mfma(const WgradArgs& a, int y, int n0, int k0, int64_t 
         }
     }
     for (int64_t rt = r_lo; rt < r_hi; rt += 32) {
-#ifdef NAV_WG_PINGPONG
-        if ((((rt - r_lo) >> 5) + (wave_id() >> 2)) & 1) __builtin_amdgcn_s_setprio(1);
-        else __builtin_amdgcn_s_setprio(0);
-#endif
         Raw nn = nxt;
         if (rt + 64 < r_hi) nn = load(rt + 64);
         f32x16 P[2], Q[2];
@@ -681,10 +677,6 @@ NAV_DEV void wgrad_rows_fact(const WgradArgs& a, int y, int n0, int k0, int64_t 
     }
     if (r_lo < r_full) {
         for (int64_t rt = r_lo; rt < r_full; rt += 32) {
-#ifdef NAV_WG_PINGPONG  // A/B variant: the two waves of a SIMD take turns at the higher priority
-            if ((((rt - r_lo) >> 5) + (wave_id() >> 2)) & 1) __builtin_amdgcn_s_setprio(1);
-            else __builtin_amdgcn_s_setprio(0);
-#endif
             if (rt + 32 < r_full) {
                 load_raw(rt + 32, nxt);
                 if (GPF) load_g(rt + 32, gn);
