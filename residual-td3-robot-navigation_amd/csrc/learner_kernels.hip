@@ -47,6 +47,7 @@ struct WgradArgs {
     int fact;               // 1: the factored-Wo path (wgrad_tile_fact) for every tile
     int64_t per_split;      // rows per split (multiple of 64)
     int64_t per_wave;       // rows per wave (multiple of 64)
+    int64_t skew;           // rows moved from each of waves 4-7 to its SIMD partner wave w - 4
 };
 
 // Phase probe of the weight-gradient kernels (variant builds with -DNAV_WGRAD_TRACE only;
@@ -68,6 +69,12 @@ __device__ unsigned long long g_wgrad_trace[2][4][8][8];
 #endif
 
 constexpr int WG_WAVES = 8;
+#ifndef NAV_WG_SKEW_FACT
+#define NAV_WG_SKEW_FACT 64
+#endif
+#ifndef NAV_WG_SKEW_OPND
+#define NAV_WG_SKEW_OPND 128
+#endif
 constexpr int WG_TOTAL = 256;  // workgroups that fill the chip (one 8-wave workgroup per CU)
 constexpr int WG_THREADS = WG_WAVES * 64;
 constexpr int WG_TILE = 64;
@@ -831,13 +838,20 @@ NAV_DEV TileJob wgrad_job(const WgradArgs& a, int b, int total) {
     return t;
 }
 
-// split s's rows for wave wv: [r_lo, r_hi)
-NAV_DEV void wave_rows(const WgradArgs& a, int split, int wv, int64_t& r_lo, int64_t& r_hi) {
+// split s's rows for wave wv: [r_lo, r_hi). Waves w and w + 4 share a SIMD, and its arbiter
+// issues the older wave first: with equal rows the second wave of every SIMD reached the LDS
+// reduce ~9 k cycles after the first and ran that tail alone (profiles/r05z). `skew` rows (a
+// multiple of 32: whole tiles) move from wave w + 4 to wave w, so the pair finishes together.
+NAV_DEV void wave_rows(const WgradArgs& a, int split, int wv, int64_t skew, int64_t& r_lo,
+                       int64_t& r_hi) {
     const int64_t M = a.M;
     const int64_t s_lo = (int64_t)split * a.per_split < M ? (int64_t)split * a.per_split : M;
     const int64_t s_hi = s_lo + a.per_split < M ? s_lo + a.per_split : M;
-    r_lo = s_lo + wv * a.per_wave < s_hi ? s_lo + wv * a.per_wave : s_hi;
-    r_hi = r_lo + a.per_wave < s_hi ? r_lo + a.per_wave : s_hi;
+    const int64_t pa = a.per_wave + skew, pb = a.per_wave - skew;  // waves 0-3, 4-7
+    const int64_t off = wv < WG_WAVES / 2 ? wv * pa : (WG_WAVES / 2) * pa + (wv - WG_WAVES / 2) * pb;
+    const int64_t len = wv < WG_WAVES / 2 ? pa : pb;
+    r_lo = s_lo + off < s_hi ? s_lo + off : s_hi;
+    r_hi = r_lo + len < s_hi ? r_lo + len : s_hi;
 }
 
 template <int NI, int D>
@@ -857,7 +871,7 @@ NAV_DEV void wgrad_tile_fact(const WgradArgs& a, const TileJob& t, float* smem) 
     __syncthreads();
     WG_MARK(0, 1);
     int64_t r_lo, r_hi;
-    wave_rows(a, t.split, wave_id(), r_lo, r_hi);
+    wave_rows(a, t.split, wave_id(), a.skew, r_lo, r_hi);
     f32x16 out[NI][2];
     wgrad_rows_fact<NI, D>(a, t.y, t.n0, t.k0, r_lo, r_hi, reinterpret_cast<const char*>(tab), out);
     WG_MARK(0, 5);
@@ -872,8 +886,11 @@ NAV_DEV void wgrad_tile(const WgradArgs& a, const TileJob& t, float* smem) {
     const int y = t.y, split = t.split, L = t.L, n0 = t.n0, k0 = t.k0;
     const int nh = a.net[y].n_hidden;
     const int wv = wave_id();
+    const bool pr = L == nh - 1, qr = L == 1;
+    const bool full = n0 + WG_TILE <= a.net[y].hp && k0 + WG_TILE <= a.net[y].hp;
+    const bool opnd = pr && qr && full;  // the MFMA-operand path (32-row tiles: skew allowed)
     int64_t r_lo, r_hi;
-    wave_rows(a, split, wv, r_lo, r_hi);
+    wave_rows(a, split, wv, opnd ? a.skew : 0, r_lo, r_hi);
     float* red = smem;                                          // [8][64][64]
     float* stage = smem + WG_WAVES * WG_TILE * WG_TILE + wv * 2 * WG_STAGE_FLOATS;
     f32x16 acc[2][2];
@@ -883,9 +900,7 @@ NAV_DEV void wgrad_tile(const WgradArgs& a, const TileJob& t, float* smem) {
         for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-    const bool pr = L == nh - 1, qr = L == 1;
-    const bool full = n0 + WG_TILE <= a.net[y].hp && k0 + WG_TILE <= a.net[y].hp;
-    if (pr && qr && full) wgrad_rows_mfma(a, y, n0, k0, r_lo, r_hi, acc);
+    if (opnd) wgrad_rows_mfma(a, y, n0, k0, r_lo, r_hi, acc);
     else if (pr && qr) wgrad_rows<true, true>(a, y, L, n0, k0, r_lo, r_hi, stage, acc);
     else if (pr) wgrad_rows<true, false>(a, y, L, n0, k0, r_lo, r_hi, stage, acc);
     else if (qr) wgrad_rows<false, true>(a, y, L, n0, k0, r_lo, r_hi, stage, acc);
@@ -1406,6 +1421,11 @@ static int wgrad_args(const nav_mlp* nets, int32_t n_nets, int64_t M, const floa
     // 64-row aligned splits and per-wave ranges: a chunk's mask row tiles start on a tile boundary
     a.per_split = ((M + splits - 1) / splits + WG_CHUNK - 1) / WG_CHUNK * WG_CHUNK;
     a.per_wave = ((a.per_split + WG_WAVES - 1) / WG_WAVES + WG_CHUNK - 1) / WG_CHUNK * WG_CHUNK;
+    // whole 32-row tiles moved to the first wave of each SIMD pair, per 256 rows of a wave
+    // (tools/wgrad_bench.py, profiles/r05ad_ab_wgrad_skew.txt: 0 / 32 / 64 / 96 rows for the
+    // factored kernel -> 32.5 / 32.0 / 31.8 / 33.0 us, 0 / 64 / 96 / 128 for the operand path ->
+    // 27.4 / 27.4 / 27.1 / 26.8 us)
+    a.skew = (a.per_wave / 256) * (a.fact ? NAV_WG_SKEW_FACT : NAV_WG_SKEW_OPND);
     if ((int64_t)n_nets * a.n_hid * splits > ((int64_t)1 << 30)) return NAV_EINVAL;
     return 0;
 }

@@ -233,3 +233,62 @@ def test_headless_driver_with_learner(navmods):
     assert all(torch.isfinite(n.params).all() for n in nets.values())
     # the actor moved away from its initial parameters
     assert not torch.equal(robot.init_actor, nets["actor"].params)
+
+
+def test_td3_update_live_hyperparams_vs_oracle(navmods):
+    """robot.py's td3_update reads self.gamma / tau / policy_noise / noise_clip / max_action /
+    batch_size / num_epochs at every call (robot.py:258-339): the drop-in copies the agent's live
+    attributes into its learner config before each update. Two updates with every one of them
+    changed in between (including the batch size, which rebuilds the workspace and the cached
+    launch arguments) against the oracle run on the same numpy / torch draws: all six networks
+    within 5e-7 (Adam moves a weight by ~lr = 1e-5 per step)."""
+    from oracle.td3_oracle import TD3Oracle
+    environment, robot = navmods
+    rng = np.random.default_rng(5)
+    rb = robot.Robot(np.array([60.0, 40.0]))
+    for s in rng.uniform(0, 100, (400, 2)):
+        rb.memory.push(s, rng.uniform(-5, 5, 2), rng.uniform(-100, 0), s + rng.normal(0, 1, 2),
+                       bool(rng.uniform() < 0.1))
+    ag = rb.td3_agent
+    nets = ag.networks()
+    init = {k: [(W.numpy(), b.numpy()) for W, b in nets[k].export()]
+            for k in ("actor", "critic1", "critic2")}
+    ora = TD3Oracle(init["actor"], init["critic1"], init["critic2"], actor_lr=ag.cfg.actor_lr,
+                    critic_lr=ag.cfg.critic_lr, gamma=ag.gamma, tau=ag.tau,
+                    policy_noise=ag.policy_noise, noise_clip=ag.noise_clip,
+                    policy_update_delay=ag.policy_update_delay, max_action=ag.max_action)
+    rows = rb.memory.rows[:len(rb.memory)].cpu().numpy().astype(np.float64)
+    L = len(rows)
+    plans = [dict(seed=(11, 12), num_epochs=4),
+             dict(seed=(13, 14), num_epochs=3, gamma=0.9, tau=0.01, policy_noise=0.3,
+                  noise_clip=0.4, max_action=2.0, batch_size=64)]
+    for plan in plans:
+        for k in ("gamma", "tau", "policy_noise", "noise_clip", "max_action", "batch_size",
+                  "num_epochs"):
+            if k in plan:
+                setattr(ag, k, plan[k])
+        np.random.seed(plan["seed"][0])
+        torch.manual_seed(plan["seed"][1])
+        ag.td3_update(rb.memory)
+        torch.cuda.synchronize()
+        # the oracle on the same draws: np.random.choice per critic / actor sample in epoch
+        # order, torch.randn(B, 2) per critic epoch
+        ora.gamma, ora.tau, ora.max_action = ag.gamma, ag.tau, ag.max_action
+        ora.policy_noise, ora.noise_clip = ag.policy_noise, ag.noise_clip
+        B = ag.batch_size
+        np.random.seed(plan["seed"][0])
+        torch.manual_seed(plan["seed"][1])
+
+        def sample():
+            r = rows[np.random.choice(L, B, replace=False)]
+            return r[:, 0:2], r[:, 2:4], r[:, 4], r[:, 5:7], r[:, 7] > 0.5
+
+        ora.td3_update(sample, lambda: torch.randn(B, 2).numpy(), ag.num_epochs)
+    worst = 0.0
+    for name, onet in ora.networks().items():
+        for (W, b), (Wr, br) in zip(nets[name].export(), onet.params):
+            d = max(float((W - Wr).abs().max()), float((b - br).abs().max()))
+            worst = max(worst, d)
+            assert d <= 5e-7, (name, d)
+    print(f"max |diff| vs oracle after both updates: {worst:.2e}")
+    assert ag.cfg.max_action == 2.0 and ag.cfg.batch_size == 64 and ag.cfg.gamma == 0.9
