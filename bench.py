@@ -43,6 +43,8 @@ F16_MFMA_PEAK_TFS = 2516.6  # MI355X_MICROARCH.md: 1024 FLOP/clk/SIMD x 1024 SIM
 # split): the MFMA FLOPs per f32 product, and the network passes (forwards + row backwards) per
 # row block of each row kernel
 PRODUCTS_PER_PASS = 3
+# the median shader clock each row kernel holds under the bench loop (tools/clock_probe.py)
+HELD_CLOCK_MHZ = {"critic_rows": 1925.3, "actor_rows": 1964.5, "act_tick": 2048.1}
 ROOFLINE_VERSION = "r05: fp16 two-plane split, 3 products per f32 product (r03-r04: bf16 6)"
 
 
@@ -411,6 +413,14 @@ def main():
                                  "duration",
                     "mfma_flop_per_launch": mfma_flop,
                     "hidden_gemm_f32_flop_per_launch": hidden,
+                    # DVFS: the row kernels hold ~1.93 GHz, not the 2.4 GHz of the spec peak
+                    # (in-kernel s_memtime / s_memrealtime stamps, a -DNAV_CLOCK_STAMP build)
+                    "held_clock": {"mhz": HELD_CLOCK_MHZ.get(dominant),
+                                   "frac": (round(tfs / (F16_MFMA_PEAK_TFS *
+                                                         HELD_CLOCK_MHZ[dominant] / 2400.0), 4)
+                                            if dominant in HELD_CLOCK_MHZ else None),
+                                   "source": "profiles/r05l_clock_probe_fp16.json (median over "
+                                             "workgroups, 3 s of bench steps)"},
                     "f32_equiv": {"flop_per_launch": d["work_per_launch"],
                                   "achieved_TFs": round(ach / 1e12, 2),
                                   "note": "all of the kernel's f32 FLOPs (SURVEY 8(d)) / launch "

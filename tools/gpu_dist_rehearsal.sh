@@ -8,3 +8,4 @@ OUT=${1:-gpurun_out/dist_rehearsal.log}
 ARGS="--gpus 2 --steps 20 --warmup 2 --long-steps 0"
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py $ARGS > "$OUT" 2>&1
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29532 bench.py $ARGS --shared-policy >> "$OUT" 2>&1
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py $ARGS --shared-policy --overlap-collect >> "$OUT" 2>&1
