@@ -504,7 +504,10 @@ NAV_DEV void wgrad_rows_mfma(const WgradArgs& a, int y, int n0, int k0, int64_t 
 // (128 x 64) at D = 1 — the twin critics — for 128 accumulator registers.
 
 
-template <int NI, int D>
+// GV: dy rows packed (ld_dy = D) and 16-B aligned (float4 loads at fixed offsets); XV: x rows of 4
+// floats, 16-B aligned (one float4 load per row). Both are launch-uniform: the full-tile loop is
+// compiled per form, with running row pointers and no per-tile branch on the layout.
+template <int NI, int D, bool GV, bool XV>
 NAV_DEV void wgrad_rows_fact(const WgradArgs& a, int y, int n0, int k0, int64_t r_lo,
                              int64_t r_hi, const char* tab, f32x16 (&out)[NI][2]) {
     const MlpDev& net = a.net[y];
@@ -606,22 +609,22 @@ NAV_DEV void wgrad_rows_fact(const WgradArgs& a, int y, int n0, int k0, int64_t 
                 }
         }
     };
-    // whole tiles: dy rows as float4 (ld_dy = d_out and 16-B aligned, else element loads), one
-    // tile ahead like the x rows and mask words
-    const bool gvec = ld_dy == D && ((uintptr_t)dyp & 15) == 0;
     const int64_t r_full = r_lo + ((r_hi - r_lo) & ~(int64_t)31);
-    auto load_g = [&](int64_t rt, float (&gs)[2][D][8]) {
-        const float* gp = dyp + (rt + 4 * h) * ld_dy;  // row rt + 4h
+    constexpr int LDG = GV ? D : 0;  // the compile-time dy row stride of the GV form
+    const int ldg = GV ? LDG : ld_dy;
+    // the g values of rows rt + 4h + 16 s2 + 8 qq + t (register e = 8 s2 + 4 qq + t of the C
+    // layout) from the row pointer g0 = dy + (rt + 4h) ldg
+    auto load_g_at = [&](const float* gp, float (&gs)[2][D][8]) {
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
             for (int qq = 0; qq < 2; ++qq) {
-                const float* g = gp + (16 * s2 + 8 * qq) * ld_dy;
-                if (gvec && D == 1) {
+                const float* g = gp + (16 * s2 + 8 * qq) * ldg;
+                if (GV && D == 1) {
                     const float4 u = *reinterpret_cast<const float4*>(g);
                     gs[s2][0][4 * qq] = u.x; gs[s2][0][4 * qq + 1] = u.y;
                     gs[s2][0][4 * qq + 2] = u.z; gs[s2][0][4 * qq + 3] = u.w;
-                } else if (gvec) {
+                } else if (GV) {
                     const float4 u0 = *reinterpret_cast<const float4*>(g);
                     const float4 u1 = *reinterpret_cast<const float4*>(g + 4);
                     gs[s2][0][4 * qq] = u0.x; gs[s2][D - 1][4 * qq] = u0.y;
@@ -632,11 +635,11 @@ NAV_DEV void wgrad_rows_fact(const WgradArgs& a, int y, int n0, int k0, int64_t 
 #pragma unroll
                     for (int t = 0; t < 4; ++t)
 #pragma unroll
-                        for (int d = 0; d < D; ++d) gs[s2][d][4 * qq + t] = g[t * ld_dy + d];
+                        for (int d = 0; d < D; ++d) gs[s2][d][4 * qq + t] = g[t * ldg + d];
                 }
             }
     };
-    // D = 2: the g scales on the loaded values (D = 1 folds them into the layer-0 constants)
+    // the g scales on the loaded values (D = 2; D = 1 folds them into the layer-0 constants)
     auto scale_g = [&](float (&gs)[2][D][8]) {
         if (D == 1) return;
 #pragma unroll
@@ -646,18 +649,38 @@ NAV_DEV void wgrad_rows_fact(const WgradArgs& a, int y, int n0, int k0, int64_t 
 #pragma unroll
                 for (int t = 0; t < 8; ++t) gs[s2][d][t] *= sg[d];
     };
-    // d_out = 2 loads its 32 g values at the tile (prefetched they do not fit the registers)
+    // full tiles: running per-lane pointers (x row, mask words, g rows), every row in range, so no
+    // clamp; d_out = 1 loads its g values one tile ahead with the rest (d_out = 2 at the tile: its
+    // 32 prefetched values do not fit the registers)
     constexpr bool GPF = D == 1;
-    Raw cur, nxt;
-    float gc[2][D][8], gn[2][D][8];
-    if (r_lo < r_full) {
-        load_raw(r_lo, cur);
-        if (GPF) load_g(r_lo, gc);
-    }
-    // the fp16 scales of Q_d = relu(h_0) g_d: h_0 column half j by 2^eh[j] (folded into the
-    // layer-0 constants: a power of two commutes with the fma chain's roundings), g_d by 2^eg[d]
-    // (D = 1: folded into the same constants, so the g rows are used as loaded; D = 2: applied
-    // to the loaded g values). Computed under the first tile's loads.
+    const int64_t nfull = (r_full - r_lo) >> 5;
+    const float* xq = a.in + a.in_col + (r_lo + l32) * (int64_t)ld_in;
+    const uint16_t* mq = mp;
+    const float* gq = dyp + (r_lo + 4 * h) * (int64_t)ldg;
+    const int64_t xstep = 32 * (int64_t)ld_in, gstep = 32 * (int64_t)ldg;
+    auto load_full = [&](Raw& v, float (&gs)[2][D][8]) {
+        if (XV) {
+            const float4 u = *reinterpret_cast<const float4*>(xq);
+            v.x0 = h ? u.y : u.x;
+            v.x1 = h ? u.w : u.z;
+        } else {
+            v.x0 = xq[xk0];
+            v.x1 = xq[xk1];
+        }
+#pragma unroll
+        for (int i = 0; i < NI; ++i) v.m[i] = mq[i * 64];
+        if (GPF) load_g_at(gq, gs);
+        xq += xstep;
+        mq += mstride;
+        gq += gstep;
+    };
+    Raw c0, c1;
+    float g0[2][D][8], g1[2][D][8];
+    if (nfull > 0) load_full(c0, g0);
+    // the scales, computed under the first tile's loads: h_0 column half j by 2^eh[j] (folded into
+    // the layer-0 constants: a power of two commutes with the fma chain's roundings), g_d by
+    // 2^eg[d] (D = 1: folded into the same constants, so the g rows are used as loaded; D = 2:
+    // applied to the loaded g values)
     {
         float G[2], X[4];
         WG_MARK(0, 2);
@@ -682,26 +705,19 @@ NAV_DEV void wgrad_rows_fact(const WgradArgs& a, int y, int n0, int k0, int64_t 
         }
         if (D == 1) eg[0] = 0;
     }
-    if (r_lo < r_full) {
-        for (int64_t rt = r_lo; rt < r_full; rt += 32) {
-            if (rt + 32 < r_full) {
-                load_raw(rt + 32, nxt);
-                if (GPF) load_g(rt + 32, gn);
-            }
-            if (!GPF) {
-                load_g(rt, gc);
-                scale_g(gc);
-            }
-            tile(cur, gc);
-            cur = nxt;
-            if (GPF) {
+    for (int64_t t = 0; t < nfull; ++t) {
+        if (t + 1 < nfull) load_full(c1, g1);
+        if (!GPF) load_g_at(dyp + (r_lo + 32 * t + 4 * h) * (int64_t)ldg, g0);
+        scale_g(g0);
+        tile(c0, g0);
+        c0 = c1;
+        if (GPF) {
 #pragma unroll
-                for (int s2 = 0; s2 < 2; ++s2)
+            for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-                    for (int d = 0; d < D; ++d)
+                for (int d = 0; d < D; ++d)
 #pragma unroll
-                        for (int t = 0; t < 8; ++t) gc[s2][d][t] = gn[s2][d][t];
-            }
+                    for (int e = 0; e < 8; ++e) g0[s2][d][e] = g1[s2][d][e];
         }
     }
     WG_MARK(0, 4);
@@ -855,11 +871,11 @@ NAV_DEV void wave_rows(const WgradArgs& a, int split, int wv, int64_t skew, int6
 }
 
 template <int NI, int D>
-NAV_DEV void wgrad_tile_fact(const WgradArgs& a, const TileJob& t, float* smem) {
+NAV_DEV void wgrad_tile_fact(const WgradArgs& a, const TileJob& t, float* smem, uint4* tab) {
     WG_MARK(0, 0);
-    // the bits -> A fragment table at LDS offset 0: entry b, dword d holds fp16 2.0 (0x4000) in its
-    // low half when bit 2d of b is set and in its high half when bit 2d + 1 is
-    uint4* tab = reinterpret_cast<uint4*>(smem);
+    // the bits -> A fragment table (a static LDS array: its address is a constant, so a fragment
+    // read is one ds_read_b128 at the entry's offset): entry b, dword d holds fp16 2.0 (0x4000)
+    // in its low half when bit 2d of b is set and in its high half when bit 2d + 1 is
     if (threadIdx.x < 256) {
         const uint32_t b = threadIdx.x;
         uint32_t w[4];
@@ -873,9 +889,16 @@ NAV_DEV void wgrad_tile_fact(const WgradArgs& a, const TileJob& t, float* smem) 
     int64_t r_lo, r_hi;
     wave_rows(a, t.split, wave_id(), a.skew, r_lo, r_hi);
     f32x16 out[NI][2];
-    wgrad_rows_fact<NI, D>(a, t.y, t.n0, t.k0, r_lo, r_hi, reinterpret_cast<const char*>(tab), out);
+    const char* tb = reinterpret_cast<const char*>(tab);
+    const bool gv = a.ld_dy == D && ((uintptr_t)a.dy[t.y] & 15) == 0;
+    const bool xv = a.net[t.y].d_in == 4 && (a.ld_in & 3) == 0 &&
+                    ((uintptr_t)(a.in + a.in_col) & 15) == 0;
+    if (gv && xv) wgrad_rows_fact<NI, D, true, true>(a, t.y, t.n0, t.k0, r_lo, r_hi, tb, out);
+    else if (gv) wgrad_rows_fact<NI, D, true, false>(a, t.y, t.n0, t.k0, r_lo, r_hi, tb, out);
+    else if (xv) wgrad_rows_fact<NI, D, false, true>(a, t.y, t.n0, t.k0, r_lo, r_hi, tb, out);
+    else wgrad_rows_fact<NI, D, false, false>(a, t.y, t.n0, t.k0, r_lo, r_hi, tb, out);
     WG_MARK(0, 5);
-    wgrad_reduce_write<NI>(a, t.y, t.split, t.L, t.n0, t.k0, out, smem + 1024);
+    wgrad_reduce_write<NI>(a, t.y, t.split, t.L, t.n0, t.k0, out, smem);
     WG_MARK(0, 6);
 }
 
@@ -920,7 +943,8 @@ __global__ __launch_bounds__(WG_THREADS) void k_wgrad(WgradArgs a) {
 template <int NI, int D>
 __global__ __launch_bounds__(WG_THREADS) void k_wgrad_fact(WgradArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    wgrad_tile_fact<NI, D>(a, wgrad_job(a, blockIdx.x, gridDim.x), smem);
+    __shared__ uint4 tab[256];
+    wgrad_tile_fact<NI, D>(a, wgrad_job(a, blockIdx.x, gridDim.x), smem, tab);
 }
 
 // ---------------- optimizer / target update, refreshing the packed images ----------------
@@ -1441,7 +1465,8 @@ int nav_mlp_wgrad(const nav_mlp* nets, int32_t n_nets, int64_t M, const float* i
     if (rc) return rc;
     if (a.net[0].n_hidden < 2) return 0;
     const int64_t blocks = (int64_t)n_nets * a.n_hid * splits;
-    const size_t lds = wgrad_lds_bytes();
+    // the factored kernel: its 4 KB fragment table is static, the dynamic part the reduce slots
+    const size_t lds = a.fact ? (size_t)WG_WAVES * WG_TILE * WG_TILE * 4 : wgrad_lds_bytes();
     void (*k)(WgradArgs) = !a.fact ? k_wgrad
                            : a.tn == 128 ? k_wgrad_fact<4, 1> : k_wgrad_fact<2, 1>;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),

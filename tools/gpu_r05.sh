@@ -91,6 +91,7 @@ for step in "$@"; do
     clock) run clock 200 python tools/withlib.py "$ROOT/abl/libnavenv_clock.so" tools/clock_probe.py --seconds 3 ;;
     sphost) run sphost 300 python tools/shared_policy_host.py ;;
     config1) run config1 300 python tools/config1_run.py ;;
+    mix) run mix 100 ./build/mix_probe ;;
     shape) run shape 200 ./build/mfma_shape_probe 512 2.5 0 && run shape_dz 200 ./build/mfma_shape_probe 512 2.5 1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
