@@ -3,6 +3,11 @@
 // rounded once to f16) against the form the compiler emits for (half)(x - (float)hi)
 // (v_cvt_f32_f16 + v_pk_add_f32 + v_cvt_pk_f16_f32): bit-for-bit comparison of lo on random
 // values over 2^-40 .. 2^15 of both signs, fp16 rounding ties, and values whose lo is subnormal.
+// Result (r05ai): 0 of 4.2 M lo values differ. Adopted into split2_8 / gemm_cols as inline asm it
+// broke test_resume_is_bit_identical (r05aj): the compiler's hazard recognizer does not see an
+// inline-asm VALU write, so an MFMA (or LDS store) consuming the lo plane right after it gets no
+// wait states; the compiler itself never selects the mix instructions for this pattern (it emits
+// cvt_f32_f16 + v_pk_add/v_pk_fma), so the form was not kept.
 // build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off tools/probe/mix_probe.hip -o build/mix_probe
 #include <hip/hip_runtime.h>
 #include <cmath>
