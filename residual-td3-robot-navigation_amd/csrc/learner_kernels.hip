@@ -343,7 +343,6 @@ NAV_DEV void wgrad_rows_mfma(const WgradArgs& a, int y, int n0, int k0, int64_t 
         }
     }
     if (r_lo >= r_hi) return;
-    const float one = h == 0 ? 1.f : 0.f;
     const uint16_t* mk = a.masks[y] + (size_t)(nh - 1) * mask_rowtiles(M) * NTm * 64 +
                          (size_t)(n0 >> 5) * 64 + lane;
     const size_t mstride = (size_t)NTm * 64;
@@ -389,6 +388,11 @@ NAV_DEV void wgrad_rows_mfma(const WgradArgs& a, int y, int n0, int k0, int64_t 
         return v;
     };
     // operand MFMAs of one tile (results in the C layout, masked later by finish())
+    // the h_0 tiles start at the (scaled) bias of their column, set by VALU: the same C operand
+    // the K = 2 bias MFMA of (1, 0) x (b, 0) produced (exactly b), one f32 MFMA fewer per column
+    // half and tile; inputs 2, 3 only exist for d_in > 2 (the actor has 2)
+    float bc[2];  // set below, after the scales
+    const bool x23 = d_in > 2;
     auto issue = [&](int64_t rt, const Raw& v, f32x16 (&P)[2], f32x16 (&Q)[2]) {
         const bool ok = rt + l32 < r_hi && h < d_out;  // rows past r_hi: dz = 0, add nothing
         const float g = ok ? v.g : 0.f;
@@ -397,12 +401,15 @@ NAV_DEV void wgrad_rows_mfma(const WgradArgs& a, int y, int n0, int k0, int64_t 
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             P[i] = mfma(g, wob[i], zero);
-            Q[i] = mfma(one, bob[i], zero);
+            f32x16 b;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) b[e] = bc[i];
+            Q[i] = mfma(x0, w0b[i][0], b);
         }
+        if (x23) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i) Q[i] = mfma(x0, w0b[i][0], Q[i]);
-#pragma unroll
-        for (int i = 0; i < 2; ++i) Q[i] = mfma(x1, w0b[i][1], Q[i]);
+            for (int i = 0; i < 2; ++i) Q[i] = mfma(x1, w0b[i][1], Q[i]);
+        }
     };
     // ReLU derivative of the top layer on P (bit e of the lane's word as an all-ones mask) and
     // the layer-0 ReLU on Q (an integer max of the bit pattern: one v_max_i32)
@@ -446,6 +453,7 @@ NAV_DEV void wgrad_rows_mfma(const WgradArgs& a, int y, int n0, int k0, int64_t 
             w0b[i][0] = ldexpf(w0b[i][0], eq[i]);
             w0b[i][1] = ldexpf(w0b[i][1], eq[i]);
             bob[i] = ldexpf(bob[i], eq[i]);
+            bc[i] = bob[i] + __shfl_xor(bob[i], 32, 64);  // the column's scaled bias, both halves
         }
     }
     for (int64_t rt = r_lo; rt < r_hi; rt += 32) {
@@ -542,7 +550,7 @@ NAV_DEV void wgrad_rows_fact(const WgradArgs& a, int y, int n0, int k0, int64_t 
     }
     int eh[2], eg[D];  // the fp16 operand scales (below, under the first tile's loads)
     float sg[D];
-    const float one = h == 0 ? 1.f : 0.f;
+    float bcj[2];      // the scaled bias of the lane's column per half (below, with the scales)
     const bool x23 = d_in > 2;
     const size_t mstride = (size_t)NTm * 64;
     const uint16_t* mp = a.masks[y] + (size_t)mask_rowtiles(M) * mstride +  // layer 1's bits
@@ -580,8 +588,11 @@ NAV_DEV void wgrad_rows_fact(const WgradArgs& a, int y, int n0, int k0, int64_t 
         // one 32-column half j of the k side at a time (16 registers of h_0 live)
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-            const f32x16 zero = {};
-            f32x16 Z = mfma(one, bob[j], zero);
+            // the C operand starts at the column's scaled bias (exactly what the K = 2 bias MFMA
+            // of (1, 0) x (b, 0) produced), set by VALU: one f32 MFMA fewer per half and tile
+            f32x16 Z;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) Z[e] = bcj[j];
             Z = mfma(x0, w0b[j][0], Z);
             if (x23) Z = mfma(x1, w0b[j][1], Z);
             // registers 8s .. 8s+7 of the C layout are k step s (rows 16s + 8(t>>2) + 4h +
@@ -702,6 +713,7 @@ NAV_DEV void wgrad_rows_fact(const WgradArgs& a, int y, int n0, int k0, int64_t 
             w0b[j][0] = ldexpf(w0b[j][0], eh[j]);
             w0b[j][1] = ldexpf(w0b[j][1], eh[j]);
             bob[j] = ldexpf(bob[j], eh[j]);
+            bcj[j] = bob[j] + __shfl_xor(bob[j], 32, 64);  // the column's scaled bias, both halves
         }
         if (D == 1) eg[0] = 0;
     }
