@@ -585,7 +585,7 @@ NAV_DEV L0Pre load_l0(const MlpDev& net) {
         const int c = (j == 0 ? wc.t0 : wc.t1) * 32 + l32;
         p.wa[j] = has && h < d_in ? W0[c * d_in + h] : 0.f;
         p.wb[j] = has && 2 + h < d_in ? W0[c * d_in + 2 + h] : 0.f;
-        p.bias[j] = has && h == 0 ? b0[c] : 0.f;
+        p.bias[j] = has ? b0[c] : 0.f;  // the column's bias in both lane halves (the C operand)
     }
     return p;
 }
@@ -610,14 +610,13 @@ NAV_DEV void fwd_net(const MlpDev& net, float* act, _Float16* stage, const float
     const WoCols wo = load_wo<NT>(net);
     if (wo_out) *wo_out = wo;
     // ---- layer 0 (K = d_in <= 4) on MFMA, straight into the C layout of the wave's column
-    // tiles: the bias tile by a K = 2 product of (1, 0) x (b, 0) (exactly b), then x[:, 0:2] and
-    // x[:, 2:4] against W0's columns: each element is fma(x3, w3, fma(x2, w2, fma(x1, w1,
-    // fma(x0, w0, b)))) — layer0_unit's chain, bit for bit (absent inputs and weights are 0)
+    // tiles: the C tile starts at the bias (set by VALU), then x[:, 0:2] and (d_in > 2) x[:, 2:4]
+    // against W0's columns: each element is fma(x3, w3, fma(x2, w2, fma(x1, w1, fma(x0, w0, b))))
+    // — layer0_unit's chain, bit for bit (absent inputs and weights are 0)
     {
         const L0Pre l0 = pre ? *pre : load_l0<NT>(net);
-        const f32x16 zero = {};
         float m0[RT] = {};
-        const float one = h == 0 ? 1.f : 0.f;
+        const bool x23 = net.d_in > 2;
         // A operands: row l32 of each row tile, inputs h and 2 + h
         float xa[RT], xb[RT];
 #pragma unroll
@@ -632,12 +631,16 @@ NAV_DEV void fwd_net(const MlpDev& net, float* act, _Float16* stage, const float
             const int t = j == 0 ? wc.t0 : wc.t1;
             const int c = t * 32 + l32;
             const float wa = l0.wa[j], wb = l0.wb[j];
-            const f32x16 bias = mfma(one, l0.bias[j], zero);
+            // the C tile starts at the column's bias, set by VALU (exactly what the K = 2 MFMA of
+            // (1, 0) x (b, 0) gave); inputs 2, 3 only for d_in > 2
+            f32x16 bias;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) bias[i] = l0.bias[j];
             float* col = act + c + 4 * h * SS;
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt) {
                 f32x16 v = mfma(xa[rt], wa, bias);
-                v = mfma(xb[rt], wb, v);
+                if (x23) v = mfma(xb[rt], wb, v);
                 uint32_t bits = 0;
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
