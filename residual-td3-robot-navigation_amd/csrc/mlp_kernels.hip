@@ -58,7 +58,7 @@ NAV_DEV void publish_amax(float* slots, const float (&m)[RT]) {
 // l32][16q + 8h + j] and B[16q + 8h + j][col l32], j = 0..7 (the 32x32x16 operand maps). Every wave
 // runs the split and the barriers; waves without a column tile (NT < 4) skip only the MFMAs. The
 // result is unscaled before it is returned: the callers see acc = A . B in f32.
-template <int NT, int RT>
+template <int NT, int RT, int PFB = 1>
 NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const float* __restrict__ img,
                        _Float16* stage, f32x16 (&acc)[RT][2]) {
     constexpr int hp = NT * 32;
@@ -100,7 +100,10 @@ NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const float* __restr
     };
     // B planes PF steps ahead: one step for 64-row blocks (the register budget of the big row
     // kernels), two for 32-row blocks, whose step (6 MFMAs per wave) is shorter than an L2 hit
-    constexpr int PF = RT == 1 ? 2 : 1;
+    // B prefetch distance in k steps: 64-row blocks take the caller's PFB (2 in the critic row
+    // kernel and the forward / tick launches, 1 in the 256-register actor row kernel, where a
+    // second step of B fragments costs more than it hides: profiles/r05ap)
+    constexpr int PF = RT == 1 ? 2 : PFB;
     f16x8 bq0[PF + 1][2], bq1[PF + 1][2];
 #pragma unroll
     for (int d = 0; d < PF; ++d)
@@ -594,7 +597,7 @@ NAV_DEV L0Pre load_l0(const MlpDev& net) {
 // layer stays in registers (`top`, C layout) — its LDS rows are written only when save_mask asks
 // for its global copy — and the output layer's per-wave partials land in `red` (ready for out_y
 // after the trailing barrier).
-template <int NT, int RT>
+template <int NT, int RT, int PFB = 1>
 NAV_DEV void fwd_net(const MlpDev& net, float* act, _Float16* stage, const float* xin, float* red,
                      uint16_t* masks, int64_t n_rt, float* act_save, uint32_t save_mask,
                      int64_t row0, int64_t M, int64_t rt0, f32x16 (&top)[RT][2], int mk = -64,
@@ -664,7 +667,7 @@ NAV_DEV void fwd_net(const MlpDev& net, float* act, _Float16* stage, const float
         const float* bL = net.params + net.b_off[L];
         const float bb0 = wc.has0 ? bL[wc.t0 * 32 + l32] : 0.f;
         const float bb1 = wc.has1 ? bL[wc.t1 * 32 + l32] : 0.f;
-        gemm_cols<NT, RT>(act, SS, img_fwd(net, L), stage, acc);
+        gemm_cols<NT, RT, PFB>(act, SS, img_fwd(net, L), stage, acc);
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             if (!(j == 0 ? wc.has0 : wc.has1)) continue;
@@ -799,7 +802,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
 
     float* red = xin + TM * 4;  // [2][PARTS][TM]
     f32x16 top[RT][2];
-    fwd_net<NT, RT>(net, act, stage, xin, red, masks, n_rt, act_save, a.save_mask, row0, M, rt0, top,
+    fwd_net<NT, RT, 2>(net, act, stage, xin, red, masks, n_rt, act_save, a.save_mask, row0, M, rt0, top,
                     OUT_MODE == OUT_TICK ? NAV_TICK_MK : -64, &l0);
     const int rloc = tid % TM;
     const int j = tid / TM;
@@ -1044,7 +1047,7 @@ NAV_DEV void mask_and_store(f32x16 (&acc)[RT][2], const uint32_t (&mbits)[RT][2]
 // forward's ReLU bits in masks; leaves dz_0 in the LDS rows `act`. With es: the per-block edge
 // partials (every bias, dW0 from the input rows xin [TM][4], and dWo / dbo when h_top [M][hp] is
 // given); dz_L rows to dz for save_mask bits.
-template <int NT, int RT>
+template <int NT, int RT, int PFB = 1>
 NAV_DEV void bwd_net(const MlpDev& net, float* act, _Float16* stage, const float* dys, const float* xin,
                      const uint16_t* masks, int64_t n_rt, float* es, const float* h_top,
                      float* dz, uint32_t save_mask, int64_t row0, int64_t M, int64_t rt0,
@@ -1145,7 +1148,7 @@ NAV_DEV void bwd_net(const MlpDev& net, float* act, _Float16* stage, const float
         f32x16 acc[RT][2];
         uint32_t mbits[RT][2];
         load_mask_bits<NT, RT>(masks + (size_t)(L - 1) * mstride, rt0, mbits);
-        gemm_cols<NT, RT>(act, SS, img_bwd(net, L), stage, acc);
+        gemm_cols<NT, RT, PFB>(act, SS, img_bwd(net, L), stage, acc);
         NAV_MARK(mk + 3);
         __syncthreads();
         // layer 0's rows only when a reader follows (the caller's dx, the save copy); its edge
@@ -1326,7 +1329,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
     // Each pass's layer-0 constants are loaded one pass ahead (L0Pre).
     f32x16 top[RT][2];
     const L0Pre l0_ct1 = load_l0<NT>(a.critic_t[0]);
-    fwd_net<NT, RT>(a.actor_t, act, stage, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0, top, 2,
+    fwd_net<NT, RT, 2>(a.actor_t, act, stage, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0, top, 2,
                     &l0_at);
     if (tn >= 0 && tn < 2 * TM) {  // the noise's threads
         const int rloc = tn % TM, j = tn / TM;
@@ -1344,12 +1347,12 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
     // twin target critics on (s', a'), then y = r + gamma * min(q1', q2') * (1 - done), kept in
     // the row's thread
     const L0Pre l0_ct2 = load_l0<NT>(a.critic_t[1]);
-    fwd_net<NT, RT>(a.critic_t[0], act, stage, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0, top,
+    fwd_net<NT, RT, 2>(a.critic_t[0], act, stage, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0, top,
                     9, &l0_ct1);
     if (tid < TM) qv[tid] = out_y<RT>(a.critic_t[0], red, tid, 0);
     const int q0 = a.split_twins ? (int)blockIdx.y : 0;  // the first online critic of the block
     L0Pre l0_on = load_l0<NT>(a.critic[q0]);
-    fwd_net<NT, RT>(a.critic_t[1], act, stage, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0, top,
+    fwd_net<NT, RT, 2>(a.critic_t[1], act, stage, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0, top,
                     15, &l0_ct2);
     float yt = 0.f;
     if (tid < TM) {
@@ -1366,7 +1369,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
         if (a.split_twins && q != (int)blockIdx.y) continue;  // workgroup-uniform
         uint32_t top_bits[RT * 2];
         WoCols wo;
-        fwd_net<NT, RT>(a.critic[q], act, stage, xin, red, a.masks[q], n_rt, a.acts[q], a.save_mask, row0,
+        fwd_net<NT, RT, 2>(a.critic[q], act, stage, xin, red, a.masks[q], n_rt, a.acts[q], a.save_mask, row0,
                         B, rt0, top, 22 + 14 * q, &l0_on, top_bits, &wo);
         if (q == 0 && !a.split_twins) l0_on = load_l0<NT>(a.critic[1]);
         float* es = a.eslab[q] ? a.eslab[q] + (int64_t)blockIdx.x * a.ecount : nullptr;
@@ -1379,7 +1382,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
                 *reinterpret_cast<float4*>(dys + tid * 4) =
                     make_float4(red[kWaves * TM + tid], 0.f, 0.f, 0.f);  // loss_epilogue's dq
             __syncthreads();
-            bwd_net<NT, RT>(a.critic[q], act, stage, dys, xin, a.masks[q], n_rt, es, nullptr, a.dz[q],
+            bwd_net<NT, RT, 2>(a.critic[q], act, stage, dys, xin, a.masks[q], n_rt, es, nullptr, a.dz[q],
                             a.dz_save_mask, row0, B, rt0, 29 + 14 * q, top_bits, &wo, false);
             __syncthreads();  // the next forward's layer 0 overwrites the rows
         }
