@@ -21,6 +21,12 @@ namespace {
 
 // 32-row blocks double-buffer the split stage and pass one barrier per k step (r03zt)
 constexpr bool kStageDb1 = true;
+// B-fragment prefetch distance (k steps) of the 64-row GEMMs in the critic row kernel and the
+// forward / tick kernels (the actor row kernel keeps 1: profiles/r05aq)
+#ifndef NAV_PF_WIDE
+#define NAV_PF_WIDE 2
+#endif
+constexpr int kPfWide = NAV_PF_WIDE;
 
 template <int NT>
 struct WaveCols {
@@ -802,7 +808,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
 
     float* red = xin + TM * 4;  // [2][PARTS][TM]
     f32x16 top[RT][2];
-    fwd_net<NT, RT, 2>(net, act, stage, xin, red, masks, n_rt, act_save, a.save_mask, row0, M, rt0, top,
+    fwd_net<NT, RT, kPfWide>(net, act, stage, xin, red, masks, n_rt, act_save, a.save_mask, row0, M, rt0, top,
                     OUT_MODE == OUT_TICK ? NAV_TICK_MK : -64, &l0);
     const int rloc = tid % TM;
     const int j = tid / TM;
@@ -1329,7 +1335,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
     // Each pass's layer-0 constants are loaded one pass ahead (L0Pre).
     f32x16 top[RT][2];
     const L0Pre l0_ct1 = load_l0<NT>(a.critic_t[0]);
-    fwd_net<NT, RT, 2>(a.actor_t, act, stage, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0, top, 2,
+    fwd_net<NT, RT, kPfWide>(a.actor_t, act, stage, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0, top, 2,
                     &l0_at);
     if (tn >= 0 && tn < 2 * TM) {  // the noise's threads
         const int rloc = tn % TM, j = tn / TM;
@@ -1347,12 +1353,12 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
     // twin target critics on (s', a'), then y = r + gamma * min(q1', q2') * (1 - done), kept in
     // the row's thread
     const L0Pre l0_ct2 = load_l0<NT>(a.critic_t[1]);
-    fwd_net<NT, RT, 2>(a.critic_t[0], act, stage, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0, top,
+    fwd_net<NT, RT, kPfWide>(a.critic_t[0], act, stage, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0, top,
                     9, &l0_ct1);
     if (tid < TM) qv[tid] = out_y<RT>(a.critic_t[0], red, tid, 0);
     const int q0 = a.split_twins ? (int)blockIdx.y : 0;  // the first online critic of the block
     L0Pre l0_on = load_l0<NT>(a.critic[q0]);
-    fwd_net<NT, RT, 2>(a.critic_t[1], act, stage, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0, top,
+    fwd_net<NT, RT, kPfWide>(a.critic_t[1], act, stage, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0, top,
                     15, &l0_ct2);
     float yt = 0.f;
     if (tid < TM) {
@@ -1369,7 +1375,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
         if (a.split_twins && q != (int)blockIdx.y) continue;  // workgroup-uniform
         uint32_t top_bits[RT * 2];
         WoCols wo;
-        fwd_net<NT, RT, 2>(a.critic[q], act, stage, xin, red, a.masks[q], n_rt, a.acts[q], a.save_mask, row0,
+        fwd_net<NT, RT, kPfWide>(a.critic[q], act, stage, xin, red, a.masks[q], n_rt, a.acts[q], a.save_mask, row0,
                         B, rt0, top, 22 + 14 * q, &l0_on, top_bits, &wo);
         if (q == 0 && !a.split_twins) l0_on = load_l0<NT>(a.critic[1]);
         float* es = a.eslab[q] ? a.eslab[q] + (int64_t)blockIdx.x * a.ecount : nullptr;
@@ -1382,7 +1388,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
                 *reinterpret_cast<float4*>(dys + tid * 4) =
                     make_float4(red[kWaves * TM + tid], 0.f, 0.f, 0.f);  // loss_epilogue's dq
             __syncthreads();
-            bwd_net<NT, RT, 2>(a.critic[q], act, stage, dys, xin, a.masks[q], n_rt, es, nullptr, a.dz[q],
+            bwd_net<NT, RT, kPfWide>(a.critic[q], act, stage, dys, xin, a.masks[q], n_rt, es, nullptr, a.dz[q],
                             a.dz_save_mask, row0, B, rt0, 29 + 14 * q, top_bits, &wo, false);
             __syncthreads();  // the next forward's layer 0 overwrites the rows
         }
