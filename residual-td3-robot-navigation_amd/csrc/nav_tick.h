@@ -317,6 +317,14 @@ NAV_DEV TickStats agent_tick_in(const nav_params& p, const nav_env_soa& env, int
 #define NAV_DEMO_FLAT 8
 #endif
 constexpr int kDemoFlat = NAV_DEMO_FLAT;
+// sub-phase marks of the demo pass in the phase-trace build of the tick launch (marks 62, 63)
+#if defined(NAV_PHASE_TRACE) && defined(NAV_TRACE_MARK)
+#define DEMO_MARK(k) NAV_TRACE_MARK(k)
+#else
+#define DEMO_MARK(k) \
+    do {            \
+    } while (0)
+#endif
 
 template <int NE, int NT>
 struct DemoScratch {
@@ -376,6 +384,7 @@ NAV_DEV double demo_pass(const nav_params& p, const DemoIdx& d, DemoScratch<NE, 
         S.incl[tid] = len + add;
     }
     __syncthreads();
+    DEMO_MARK(62);  // cell starts gathered, lengths scanned
     const int T = S.incl[NE - 1];
     for (int t0 = tid * kDemoFlat; t0 < T; t0 += NT * kDemoFlat) {
         // owner slot of entry t0: the first slot whose inclusive prefix exceeds it
@@ -426,6 +435,7 @@ NAV_DEV double demo_pass(const nav_params& p, const DemoIdx& d, DemoScratch<NE, 
         }
         atomicMin(&S.best[cur_o], (unsigned long long)__double_as_longlong(cur));
     }
+    DEMO_MARK(63);  // this thread's trips done
     __syncthreads();
     if (owner && pend.need) {
         double m2;

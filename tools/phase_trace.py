@@ -44,8 +44,9 @@ def mark_names():
 def tick_names():
     # the fused act + tick launch (k_mlp_fwd OUT_TICK): fwd_net's marks from NAV_TICK_MK = 52
     n = {52 + i: f"act fwd {s}" for i, s in enumerate(FWD)}
-    n.update({58: "tick preamble", 59: "action epilogue + agent tick (wave 0)", 60: "demo pass",
-              61: "block stats"})
+    n.update({58: "tick preamble", 59: "action epilogue + agent tick (wave 0)",
+              62: "demo: cell starts + length scan", 63: "demo: candidate trips",
+              60: "demo: final barrier + rewards", 61: "block stats"})
     return n
 
 
@@ -72,7 +73,8 @@ def main():
     assert rc == 0, rc
     t = np.frombuffer(buf, dtype=np.uint64).reshape(nt, 4, 64).astype(np.int64)
     names = tick_names() if args.tick else mark_names()
-    marks = sorted(names)
+    # in time order (the demo pass's sub-phase marks 62, 63 come between 59 and 60)
+    marks = sorted(names, key=lambda m: {62: 59.3, 63: 59.6}.get(m, m))
     live = [wg for wg in range(nt) if t[wg, 0, marks[0]] != 0]  # blocks past the grid: absent
     t = t[live]
     out = {"marks": {}, "total": {}}
