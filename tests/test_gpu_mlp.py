@@ -768,7 +768,7 @@ def test_split_gemm_f32_accuracy_vs_fp64(nav, d_in, d_out, hidden, nh, M):
 
 
 @pytest.mark.parametrize("d_in,d_out,hidden", [(4, 1, 256), (4, 1, 192), (2, 2, 256)])
-@pytest.mark.parametrize("M,splits", [(1, 1), (31, 3), (33, 1), (100, 40), (2049, 7)])
+@pytest.mark.parametrize("M,splits", [(1, 1), (31, 3), (33, 1), (100, 40), (2049, 7), (33001, 16)])
 @pytest.mark.parametrize("dy_layout", ["packed", "misaligned", "strided"])
 def test_weight_grads_2layer_edge_cases(nav, d_in, d_out, hidden, M, splits, dy_layout):
     """nav_mlp_wgrad of a 2-hidden-layer net (the factored path for d_out = 1: 128- or 64-high n
@@ -776,7 +776,10 @@ def test_weight_grads_2layer_edge_cases(nav, d_in, d_out, hidden, M, splits, dy_
     32-row tile, a tile plus one row), more splits than rows, and dy rows that are packed,
     misaligned (not 16-B aligned: the element-load path) or strided (ld_dy = d_out + 1): the sum
     of the slabs against fp64 dW_1 = dz_1^T h_0 with the forward's own ReLU bits, within 1e-5 of
-    its scale, and the padded entries exactly 0."""
+    its scale, and the padded entries exactly 0. 33 001 rows in 16 splits (2 112-row splits, 320
+    rows per wave) give 384 / 256-row (factored path) and 448 / 192-row (operand path) wave ranges
+    — whole tiles moved to the first wave of each SIMD pair — and a ragged last split of 1 321 rows
+    that ends inside wave 3."""
     from nav._lib import descs, lib, parr, ptr, stream_handle
     from nav.mlp import forward
     nh = 2
