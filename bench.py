@@ -43,9 +43,49 @@ F16_MFMA_PEAK_TFS = 2516.6  # MI355X_MICROARCH.md: 1024 FLOP/clk/SIMD x 1024 SIM
 # split): the MFMA FLOPs per f32 product, and the network passes (forwards + row backwards) per
 # row block of each row kernel
 PRODUCTS_PER_PASS = 3
+
+
+def products_per_f32(region):
+    """fp16 MFMA products per f32 product: 3 (lo.hi + hi.lo + hi.hi), except the factored critic
+    weight gradient k_wgrad_fact, whose A operand (the ReLU bit) is exact in fp16: 2."""
+    return 2 if region == "mlp_wgrad_fact" else PRODUCTS_PER_PASS
+
+
 # the median shader clock each row kernel holds under the bench loop (tools/clock_probe.py)
 HELD_CLOCK_MHZ = {"critic_rows": 1925.3, "actor_rows": 1964.5, "act_tick": 2048.1}
 ROOFLINE_VERSION = "r05: fp16 two-plane split, 3 products per f32 product (r03-r04: bf16 6)"
+
+
+# what the path computes in: the hidden x hidden GEMMs are NOT fp32 MFMA but fp16 MFMA products
+# of a scaled two-plane split of each f32 operand (22 significant bits, lo.lo dropped), f32
+# accumulate; the thin layers, epilogues, losses and Adam in f32; the env state in f64
+DTYPE = ("f32-accurate MLP: fp16x2 split (22-bit operands) on fp16 MFMA, f32 accumulate; "
+         "f32 edge layers / losses / Adam; fp64 env state")
+ACCURACY = {"hidden_gemm_err_vs_fp64": "2.4e-7 .. 5.7e-7 of max|ref| (fp32 itself ~1e-7)",
+            "wgrad_err_vs_fp64": "1.7e-7 .. 8.1e-7 of scale",
+            "bound_tested": "2e-6 of max|ref|",
+            "test": "tests/test_gpu_mlp.py::test_split_gemm_f32_accuracy_vs_fp64",
+            "source": "profiles/r05i_accuracy.log"}
+# SURVEY 8(d)'s graded bytes per env-step: fused step + reward + done + stuck 105 B, the pure
+# Environment.step 24 B (f32 state, no replay row; this build keeps f64 state and writes a 32-B
+# replay row: 237 B / 48 B in its own accounting, prof.AGENT_STEP_BYTES / ENV_STEP_BYTES)
+GRADED_AGENT_STEP_BYTES = 105
+GRADED_ENV_STEP_BYTES = 24
+
+
+def graded_step_fracs(sweep):
+    """HBM fraction of the step kernels in SURVEY 8(d)'s byte accounting, from the sweep's event
+    times: per sweep size, agent_step at 105 B and env_step at 24 B per env-step."""
+    out = []
+    for row in sweep:
+        n = row["n_envs"]
+        e = {"n_envs": n}
+        for k, b in (("agent_step", GRADED_AGENT_STEP_BYTES), ("env_step", GRADED_ENV_STEP_BYTES)):
+            gbs = b * n / (row[k]["avg_us"] * 1e-6) / 1e9
+            e[k] = {"bytes_per_env_step": b, "GBps": round(gbs, 1),
+                    "frac": round(gbs / HBM_PEAK_GBS, 4)}
+        out.append(e)
+    return out
 
 
 def hidden_passes(region, rows):
@@ -59,7 +99,8 @@ def hidden_passes(region, rows):
 # command (tools/pmc_traffic.py, gfx950 correction applied); bench regions -> kernel names
 PMC_TRAFFIC = os.path.join(HERE, "profiles", "pmc_traffic.json")
 REGION_KERNEL = {"critic_rows": "k_td3_critic_rows", "actor_rows": "k_td3_actor_rows",
-                 "mlp_bwd": "k_mlp_bwd", "mlp_wgrad": "k_wgrad", "act": "k_mlp_fwd",
+                 "mlp_bwd": "k_mlp_bwd", "mlp_wgrad": "k_wgrad",
+                 "mlp_wgrad_fact": "k_wgrad_fact", "act": "k_mlp_fwd",
                  "agent_step": "k_agent_step", "env_step": "k_env_step",
                  "act_tick": "k_mlp_fwd<tick>", "env_step_k": "k_env_step_k",
                  "grad_reduce": "k_grad_reduce", "demo_reward": "k_demo_reward_idx"}
@@ -110,7 +151,56 @@ def parse():
                     help="no HIP events inside the timed region (overhead check; no roofline)")
     ap.add_argument("--sweep-only", type=int, default=0,
                     help="only run the step-kernel sweep at this N (profiling helper)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="test helper: only the rank launch + gloo rendezvous, no GPU")
     return ap.parse_args()
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args, argv):
+    """`bench.py --gpus N` (N > 1) without an outer torch.distributed.run: start one as a CHILD
+    process (never exec: this parent may not replace itself), one rank per GPU, each rank this
+    same script with the same arguments. The ranks inherit stdout, so rank 0's single JSON line is
+    this command's output; the exit code is the launcher's, non-zero when any rank fails. Nothing
+    here touches the GPU (device_count does not initialise it on this image)."""
+    import subprocess
+    n = args.gpus
+    if not args.launch_check and os.environ.get("NAV_DIST_REHEARSAL") != "1":
+        have = torch.cuda.device_count()
+        if have < n:
+            print(f"bench.py: --gpus {n} but {have} GPU(s) visible", file=sys.stderr, flush=True)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on these hosts
+    return subprocess.run(cmd, env=env).returncode
+
+
+def launch_check(ws, rank):
+    """--launch-check: the N > 1 launch path without a GPU (CPU test): each rank joins a gloo
+    group, the ranks' ids are summed, rank 0 prints one JSON line with n_gpus = world size."""
+    import torch.distributed as dist
+    if ws > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo")
+    t = torch.tensor([float(rank)])
+    if ws > 1:
+        dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": ws, "rank_sum": int(t.item())}),
+              flush=True)
+    if ws > 1:
+        dist.destroy_process_group()
 
 
 def dist_setup(args):
@@ -304,6 +394,16 @@ def utd_sweep(args, dev, points=((8192, 2), (32768, 2), (32768, 8)), steps=30):
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            return launch_ranks(args, sys.argv[1:])
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        print(f"bench.py: WORLD_SIZE={os.environ['WORLD_SIZE']} but --gpus {args.gpus}",
+              file=sys.stderr, flush=True)
+        return 2
+    if args.launch_check:
+        return launch_check(int(os.environ.get("WORLD_SIZE", "1")),
+                            int(os.environ.get("RANK", "0")))
     ws, rank, local = dist_setup(args)
     from nav import prof
     from nav._lib import lib, require_gpu
@@ -341,13 +441,17 @@ def main():
         for _ in range(2):
             tr.step()
     breakdown = bd.summary()
-    dominant = max(breakdown, key=lambda k: breakdown[k]["total_ms"])
+    # the dominant KERNEL (the all-reduce region is a collective, reported apart)
+    dominant = max((k for k in breakdown if k != "allreduce"),
+                   key=lambda k: breakdown[k]["total_ms"])
 
     # ---- timed region
     # the dominant kernel's launches are bracketed by HIP event pairs on its launch stream, one
     # launch in EVENT_SAMPLE (each record stalls the stream a few us; bracketing every launch
-    # cost 2.6 % of the step, profiles/r03c_bench.json value vs timed_long)
-    timer = prof.KernelTimer([] if args.no_timed_events else [dominant],
+    # cost 2.6 % of the step, profiles/r03c_bench.json value vs timed_long); with a shared
+    # policy the all-reduce messages are sampled the same way
+    tracked = [dominant] + (["allreduce"] if hook is not None else [])
+    timer = prof.KernelTimer([] if args.no_timed_events else tracked,
                              sample_every=EVENT_SAMPLE)
     barrier(ws)
     torch.cuda.synchronize()
@@ -399,18 +503,24 @@ def main():
             hp = (args.hidden + 31) // 32 * 32
             rows = args.envs if dominant in ("act", "act_tick") else rank_batch
             layer = (args.layers - 1) * 2.0 * rows * hp * hp
-            hidden = hidden_passes(dominant, rows) * layer
-            mfma_flop = PRODUCTS_PER_PASS * hidden
+            if dominant in ("mlp_wgrad", "mlp_wgrad_fact"):
+                # the weight-gradient regions carry their hidden x hidden f32 FLOPs as work
+                hidden = d["work_per_launch"]
+            else:
+                hidden = hidden_passes(dominant, rows) * layer
+            products = products_per_f32(dominant)
+            mfma_flop = products * hidden
             tfs = mfma_flop / (d["avg_us"] * 1e-6) / 1e12
             roof = {"bound": "mfma", "kernel": dominant, "achieved": round(tfs, 1),
                     "peak": F16_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                     "frac": round(tfs / F16_MFMA_PEAK_TFS, 4),
                     "version": ROOFLINE_VERSION,
+                    "fp16_products_per_f32_product": products,
                     "peak_note": "fp16 dense MFMA peak: the hidden x hidden f32 GEMMs run on the "
-                                 "fp16 matrix cores as 3 products of a power-of-two-scaled "
-                                 "two-plane fp16 split (f32 accuracy, pinned vs fp64); achieved "
-                                 "= those MFMA FLOPs per launch / the launch's event-timed "
-                                 "duration",
+                                 "fp16 matrix cores as %d products of a power-of-two-scaled "
+                                 "two-plane fp16 split (22-bit operands, f32 accumulate; pinned "
+                                 "vs fp64); achieved = those MFMA FLOPs per launch / the "
+                                 "launch's event-timed duration" % products,
                     "mfma_flop_per_launch": mfma_flop,
                     "hidden_gemm_f32_flop_per_launch": hidden,
                     # DVFS: the row kernels hold ~1.93 GHz, not the 2.4 GHz of the spec peak
@@ -423,8 +533,10 @@ def main():
                                              "workgroups, 3 s of bench steps)"},
                     "f32_equiv": {"flop_per_launch": d["work_per_launch"],
                                   "achieved_TFs": round(ach / 1e12, 2),
-                                  "note": "all of the kernel's f32 FLOPs (SURVEY 8(d)) / launch "
-                                          "time; the f32 MFMA peak is 157.3 TF"},
+                                  "note": "the kernel's algorithmic f32 FLOPs (SURVEY 8(d)) / "
+                                          "launch time. NOT f32-pipe work: the hidden GEMMs "
+                                          "execute on the fp16 pipe (above), so this rate may "
+                                          "exceed the 157.3 TF f32 MFMA peak"},
                     "traffic": traffic, "traffic_source": traffic_src,
                     "avg_us": round(d["avg_us"], 2), "launches_timed": d["launches"],
                     "launches": timer.seen[dominant], "event_sample": EVENT_SAMPLE}
@@ -437,6 +549,9 @@ def main():
             step_k = {"kernel": "nav_agent_step", "n_envs": sweep[-1]["n_envs"],
                       "avg_us": big["avg_us"], "bytes_per_env_step": prof.AGENT_STEP_BYTES,
                       "GBps": big["GBps"], "frac": round(big["GBps"] / HBM_PEAK_GBS, 4),
+                      # SURVEY 8(d)'s graded accounting (f32 state, no replay row): the fused
+                      # tick 105 B, the pure Environment.step 24 B, at 2^24 and at 65 536 envs
+                      "graded": graded_step_fracs(sweep),
                       "env_step_k": sweep[-1]["env_step_k"],
                       "at_65536": sweep[0]["agent_step"]}
         # CPU baseline: rank 0 at N = 1 only (a reported baseline, not part of the scaling runs)
@@ -447,7 +562,8 @@ def main():
             "value": value, "unit": "env-steps/s", "n_gpus": ws, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": 1e3 * dt / args.steps,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "fp32 MLP (MFMA) / fp64 env state",
+            "dtype": DTYPE,
+            "accuracy": ACCURACY,
             "data": "synthetic (Philox start/goal pairs, generated fields, batched-CEM demo sets)",
             "config": {"workload": "config3: 65536 envs + residual-TD3 (2x256 MLPs)",
                        "envs_per_gpu": args.envs, "envs_per_group": args.envs_per_group,
@@ -471,12 +587,23 @@ def main():
             "utd_sweep": utd,
         }
         if hook is not None:
-            line["allreduce"] = {"messages_per_step": hook.calls / max(1, tr.steps),
-                                 "bytes_per_step": hook.bytes / max(1, tr.steps)}
+            ar = ksum.get("allreduce")
+            line["allreduce"] = {
+                "messages_per_step": hook.calls / max(1, tr.steps),
+                "bytes_per_step": hook.bytes / max(1, tr.steps),
+                "backend": torch.distributed.get_backend() if ws > 1 else None,
+                # event pair on the learner's stream around 1 message in EVENT_SAMPLE inside the
+                # timed region (the collective's stream waits for the first event, the learner's
+                # stream for the collective before the second)
+                "avg_us_per_message": round(ar["avg_us"], 2) if ar else None,
+                "avg_bytes_per_message": ar["work_per_launch"] if ar else None,
+                "messages_timed": ar["launches"] if ar else 0,
+                "ms_per_step": (ar["avg_us"] * 1e-3 * hook.calls / max(1, tr.steps)
+                                if ar else None)}
         print(json.dumps(line), flush=True)
     if ws > 1:
         torch.distributed.destroy_process_group()
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -241,11 +241,6 @@ NAV_DEV void row_maxima(const WgradArgs& a, int y, int64_t r_lo, int64_t r_hi, f
     const bool xv4 = d_in == 4 && (a.ld_in & 3) == 0 && ((uintptr_t)xin & 15) == 0;
     const bool xv2 = d_in == 2 && (a.ld_in & 1) == 0 && ((uintptr_t)xin & 7) == 0;
     const bool gv2 = d_out == 2 && (a.ld_dy & 1) == 0 && ((uintptr_t)a.dy[y] & 7) == 0;
-#ifdef NAV_WG_TIMING_NOMAX  // timing-only variant (wrong results): no pre-pass loads
-    g0 = g1 = lane == 0 ? 1e-4f : 0.f;
-    x0 = x1 = x2 = x3 = lane == 0 ? 100.f : 0.f;
-    if (r_hi < 0)  // never
-#endif
     for (int64_t rb = r_lo; rb < r_hi; rb += 64 * RU) {
         float gv[RU][2], xv[RU][4];
 #pragma unroll
@@ -303,6 +298,18 @@ NAV_DEV float h0_bound(const float (&X)[4], float wa, float wb, float bias) {
     const int h = (threadIdx.x & 63) >> 5;
     const float part = (h ? X[1] : X[0]) * fabsf(wa) + (h ? X[3] : X[2]) * fabsf(wb) + fabsf(bias);
     return part + __shfl_xor(part, 32, 64);
+}
+
+// The largest exponent <= e at which a constant of magnitude <= m stays finite when scaled by
+// 2^e (m 2^e < 2^126). The h_0 scale comes from the bound above, which is tiny when the inputs
+// and the bias are: the layer-0 weights scaled by it would overflow to inf and a zero input row
+// then give 0 * inf = NaN in the operand MFMA. Binds only in that degenerate case (the bound's
+// own 2^14 target keeps e below it otherwise), so normal results are unchanged.
+NAV_DEV int cap_exp_finite(int e, float m) {
+    if (!(m > 0.f)) return e;
+    int E;
+    (void)frexpf(m, &E);  // m = f 2^E, f in [0.5, 1)
+    return min(e, 126 - E);
 }
 
 // The MFMA-operand path for a full 64 x 64 tile of a 2-hidden-layer network with d_out = 2 (the
@@ -449,7 +456,9 @@ NAV_DEV void wgrad_rows_mfma(const WgradArgs& a, int y, int n0, int k0, int64_t 
             for (int m = 1; m < 32; m <<= 1) b = fmaxf(b, __shfl_xor(b, m, 64));
             ep[i] = pow2_exp(b);
             wob[i] = ldexpf(wob[i], ep[i]);
-            eq[i] = pow2_exp(h0_bound(X, w0b[i][0], w0b[i][1], bob[i]));
+            float wm = fmaxf(fmaxf(fabsf(w0b[i][0]), fabsf(w0b[i][1])), fabsf(bob[i]));
+            wm = fmaxf(wm, __shfl_xor(wm, 32, 64));
+            eq[i] = cap_exp_finite(pow2_exp(h0_bound(X, w0b[i][0], w0b[i][1], bob[i])), wm);
             w0b[i][0] = ldexpf(w0b[i][0], eq[i]);
             w0b[i][1] = ldexpf(w0b[i][1], eq[i]);
             bob[i] = ldexpf(bob[i], eq[i]);
@@ -710,6 +719,9 @@ NAV_DEV void wgrad_rows_fact(const WgradArgs& a, int y, int n0, int k0, int64_t 
                 pow2_exp_to(wave_max_abs(h0_bound(X, w0b[j][0], w0b[j][1], bob[j])), 7));
             // (the sum capped at 2^120: Z = h_0 2^eh stays finite for every finite h_0 bound)
             if (D == 1) eh[j] = min(max(eh[j] + eg[0], -126), 120);
+            eh[j] = __builtin_amdgcn_readfirstlane(cap_exp_finite(
+                eh[j], wave_max_abs(fmaxf(fmaxf(fabsf(w0b[j][0]), fabsf(w0b[j][1])),
+                                          fabsf(bob[j])))));
             w0b[j][0] = ldexpf(w0b[j][0], eh[j]);
             w0b[j][1] = ldexpf(w0b[j][1], eh[j]);
             bob[j] = ldexpf(bob[j], eh[j]);

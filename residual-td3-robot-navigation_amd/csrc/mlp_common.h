@@ -94,66 +94,6 @@ NAV_DEV f32x16 mfma(float a, float b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
 
-// ---- fp32 GEMMs on the bf16 matrix cores (the hidden x hidden products) ----
-// Every f32 operand x is split EXACTLY into three bf16 x = hi + mid + lo (hi = bf16(x),
-// mid = bf16(x - hi), lo = x - hi - mid, each step round-to-nearest; the remainders are exact in
-// f32 and lo has <= 8 significant bits), and a product sum_k a_k b_k is formed from the six
-// partial products hh + hm + mh + mm + hl + lh on v_mfma_f32_32x32x16_bf16 (f32 accumulate). The
-// three dropped ones (ml, lm, ll) are below 2^-23 |a||b| in total: the GEMM carries f32 accuracy
-// (probe tools/probe/split_gemm_probe.hip: rms error vs fp64 6.5e-7 against 5.8e-7 for the exact
-// f32 MFMA chain) at 16/6 of the f32 MFMA rate (bf16 MFMA is 16x f32 MFMA on gfx950).
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-
-NAV_DEV f32x16 mfma16(bf16x8 a, bf16x8 b, f32x16 c) {
-    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
-
-struct Split3 {
-    bf16x8 h, m, l;
-};
-
-NAV_DEV void split1(float x, __bf16& h, __bf16& m, __bf16& l) {
-    h = (__bf16)x;
-    const float r = x - (float)h;
-    m = (__bf16)r;
-    l = (__bf16)(r - (float)m);
-}
-
-// 8 consecutive-k f32 values -> the three bf16 fragments
-NAV_DEV Split3 split8(float4 x0, float4 x1) {
-    const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-    Split3 s;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        __bf16 h, m, l;
-        split1(v[j], h, m, l);
-        s.h[j] = h;
-        s.m[j] = m;
-        s.l[j] = l;
-    }
-    return s;
-}
-
-// acc += a . b over one 16-deep k step, the six partial products smallest first
-NAV_DEV f32x16 mfma_x6(const Split3& a, const bf16x8 (&b)[3], f32x16 c) {
-    c = mfma16(a.m, b[1], c);
-    c = mfma16(a.l, b[0], c);
-    c = mfma16(a.h, b[2], c);
-    c = mfma16(a.m, b[0], c);
-    c = mfma16(a.h, b[1], c);
-    return mfma16(a.h, b[0], c);
-}
-
-// the same with both operands split in registers
-NAV_DEV f32x16 mfma_x6s(const Split3& a, const Split3& b, f32x16 c) {
-    c = mfma16(a.m, b.m, c);
-    c = mfma16(a.l, b.h, c);
-    c = mfma16(a.h, b.l, c);
-    c = mfma16(a.m, b.h, c);
-    c = mfma16(a.h, b.m, c);
-    return mfma16(a.h, b.h, c);
-}
-
 // Entry (plane p, k step q = k / 16, lane half h = (k / 8) & 1, column n) of a 16-bit B-operand
 // image of one hp x hp matrix B[k][n] (k = the product's K): the 8 values of plane p of
 // B[16q + 8h + j][n], j = 0..7 — one 16-B load per lane per plane and k step, 32 lanes of a
@@ -169,10 +109,10 @@ __host__ __device__ inline int64_t split_entry(int hp, int p, int k, int n) {
 // products lo.hi + hi.lo + hi.hi on v_mfma_f32_32x32x16_f16 (fp16 x fp16 is exact in the f32
 // accumulator); the dropped lo.lo is below 2^-22 |a||b|. The scales keep both planes out of fp16
 // overflow and the lo plane's absolute precision (2^-24 in scaled units, the fp16 subnormal step)
-// at 2^-37 of the operand's max: A (the LDS rows) per workgroup and GEMM, from the block's
+// at 2^-37 of the operand's max: A (the LDS rows) per 32-row tile and GEMM, from the tile's
 // max |a| that the producing epilogue publishes (publish_amax); B per column n, from the
 // column's max |b|, stored with the image. The accumulators are unscaled by ldexp(acc, -(ea +
-// e_n)), exact. Half the MFMAs of the three-plane bf16 split (six products) at a smaller error
+// e_n)), exact. Half the MFMAs of round 4's three-plane bf16 split (six products) at a smaller error
 // (probe tools/probe/mfma_shape_probe.hip: 6.6e-7 vs 7.9e-7 relative to fp64 on uniform rows,
 // 2.7e-7 vs 3.9e-7 on dz-like rows spanning 1e-9 .. 6e-5; 99 vs 156 us per 8-layer launch).
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
@@ -187,31 +127,11 @@ struct Split2 {
 };
 
 // acc += a . b over one 16-deep k step, the three products smallest first
-#ifndef NAV_MFMA16_TIMING
 NAV_DEV f32x16 mfma_x3(const Split2& a, const f16x8 (&b)[2], f32x16 c) {
     c = mfma_h(a.l, b[0], c);
     c = mfma_h(a.h, b[1], c);
     return mfma_h(a.h, b[0], c);
 }
-#else
-// Timing-only variant build (wrong results): the same MFMA cycles on v_mfma_f32_16x16x32_f16,
-// two per 32x32x16 product, to measure the shape's clock effect inside the real row kernels.
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef float f32x8 __attribute__((ext_vector_type(8)));
-NAV_DEV f32x16 mfma_x3(const Split2& a, const f16x8 (&b)[2], f32x16 c) {
-    f32x4 c0 = __builtin_shufflevector(c, c, 0, 1, 2, 3);
-    f32x4 c1 = __builtin_shufflevector(c, c, 4, 5, 6, 7);
-    c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a.l, b[0], c0, 0, 0, 0);
-    c1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[0], a.l, c1, 0, 0, 0);
-    c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a.h, b[1], c0, 0, 0, 0);
-    c1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[1], a.h, c1, 0, 0, 0);
-    c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a.h, b[0], c0, 0, 0, 0);
-    c1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[0], a.h, c1, 0, 0, 0);
-    const f32x8 t = __builtin_shufflevector(c0, c1, 0, 1, 2, 3, 4, 5, 6, 7);
-    const f32x8 u = __builtin_shufflevector(c, c, 8, 9, 10, 11, 12, 13, 14, 15);
-    return __builtin_shufflevector(t, u, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
-}
-#endif
 
 // the same with both operands split in registers: a.lo b.hi + a.hi b.lo + a.hi b.hi
 NAV_DEV f32x16 mfma_x3s(const Split2& a, const Split2& b, f32x16 c) {

@@ -3,15 +3,16 @@
 //
 // Forward / row-backward: one 256-thread workgroup = 4 waves = a block of 64 rows (32 for small
 // batches) kept in LDS as fp32 (row stride hp+4) across all layers. Hidden x hidden layers run on
-// the bf16 matrix cores (v_mfma_f32_32x32x16_bf16) at fp32 accuracy: both fp32 operands are split
-// exactly into three bf16 planes (hi + mid + lo == x) and the six partial products that carry
-// 2^-24-relative weight are accumulated in fp32 (mlp_common.h; tests/test_gpu_mlp.py pins the
-// result against an fp64 reference at 2e-6 of scale). Every wave owns 1-2 32-column tiles of all
-// the block's rows; the A operand is split once per k step into an LDS stage shared by the 4
-// waves, the B operand streams from the L2-resident split weight image (refreshed by Adam /
-// Polyak). The thin input layer (K = d_in <= 4) and the bias run on f32 MFMA (layer0_unit's fma
-// chain bit for bit), the output layer (N = 1 or 2) on the VALU with a lane-transpose reduce; ReLU
-// derivatives travel from forward to backward as C-layout bit masks. The cross-row weight
+// the fp16 matrix cores (v_mfma_f32_32x32x16_f16) at f32-class accuracy: each fp32 operand is
+// scaled by a power of two (A per 32-row tile, B per column) and split into two fp16 planes
+// (hi + lo carries 22 significant bits), and the three products lo.hi + hi.lo + hi.hi accumulate
+// in fp32 (mlp_common.h; tests/test_gpu_mlp.py pins the result against an fp64 reference at 2e-6
+// of scale). Every wave owns 1-2 32-column tiles of all the block's rows; the A operand is split
+// once per k step into an LDS stage shared by the 4 waves, the B operand streams from the
+// L2-resident split weight image (refreshed after Adam / Polyak). The thin input layer (K = d_in
+// <= 4) and the bias run on f32 MFMA (layer0_unit's fma chain bit for bit), the output layer (N =
+// 1 or 2) on the VALU with a lane-transpose reduce; ReLU derivatives travel from forward to
+// backward as C-layout bit masks. The cross-row weight
 // gradients and the reduce + Adam are learner_kernels.hip.
 #include "mlp_common.h"
 #include "nav_tick.h"

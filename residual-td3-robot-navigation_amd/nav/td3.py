@@ -149,8 +149,11 @@ class TD3:
         net = nets[0]
         splits = self.splits_a if net is self.actor_network else self.splits_c
         if net.n_hidden > 1:
-            with prof.region("mlp_wgrad", len(nets) * prof.mlp_wgrad_flops(net.hidden,
-                                                                           net.n_hidden, M)):
+            # k_wgrad_fact (d_out 1, 2 hidden layers, whole 64-wide tiles: 2 fp16 products per
+            # f32 product) is timed apart from k_wgrad (3 products): their rooflines differ
+            fact = net.d_out == 1 and net.n_hidden == 2 and net.hp % 64 == 0
+            with prof.region("mlp_wgrad_fact" if fact else "mlp_wgrad",
+                             len(nets) * prof.mlp_wgrad_flops(net.hidden, net.n_hidden, M)):
                 lib().nav_mlp_wgrad(descs(*nets), len(nets), M, ptr(inp), ld_in, in_col,
                                     parr(*acts), parr(*dz), parr(*dy), ld_dy, parr(*masks),
                                     parr(*hslabs), splits, s)
@@ -298,11 +301,16 @@ class TD3:
         if self._ready is not None:  # the last epoch's replay reads and actor writes are issued
             self._ready.record(stream)
             self._ready, self._ready_recorded = None, True
+        # region "allreduce": an event pair on the launch stream around the message (the
+        # collective's stream waits for it and it for the collective), when a timer asks
+        nbytes = bucket.numel() * bucket.element_size()
         if stream is None:
-            self.grad_hook(bucket)
+            with prof.region("allreduce", nbytes):
+                self.grad_hook(bucket)
         else:
             with torch.cuda.stream(stream):
-                self.grad_hook(bucket)
+                with prof.region("allreduce", nbytes):
+                    self.grad_hook(bucket)
 
     def _critic_epoch_fast(self, replay, idx, eps, s, stream):
         c = self.cfg

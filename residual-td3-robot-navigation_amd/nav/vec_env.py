@@ -244,6 +244,7 @@ class VecEnv:
         return base
 
     def stats(self):
-        """Sum of the per-block rows: reward (as pushed; without the demo term only after the
-        two-launch nav_agent_step + nav_demo_reward form), done, goal, stuck, ended."""
+        """Sum of the per-block rows: reward (the final pushed reward, demo term included, in
+        every launch form: the demo-reward launches rewrite the reward column), done, goal,
+        stuck, ended."""
         return self.block_stats.sum(0)[:5].tolist()

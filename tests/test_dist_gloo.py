@@ -133,3 +133,32 @@ def test_shared_policy_allreduce_equals_full_batch_world2():
         _bucket_step(net, opt, X, Y, None)
     flat = torch.cat([t.reshape(-1) for t in net.tensors()]).numpy()
     np.testing.assert_allclose(flats[0], flat, rtol=0, atol=1e-6)
+
+
+def _bench(args, env_extra=None):
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env,
+                          capture_output=True, text=True, timeout=240)
+
+
+def test_bench_gpus_n_launches_n_ranks():
+    """`bench.py --gpus 2` with no outer torch.distributed.run starts the ranks itself (a child
+    launcher): two ranks join one group and rank 0's line says n_gpus 2 (the rank ids sum to 1)."""
+    import json
+    r = _bench(["--gpus", "2", "--launch-check"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout  # exactly one JSON line: rank 0's
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["rank_sum"] == 1
+    r1 = _bench(["--launch-check"])  # N = 1: no launcher, one process
+    assert r1.returncode == 0 and json.loads(r1.stdout.strip())["n_gpus"] == 1
+
+
+def test_bench_world_size_mismatch_fails():
+    r = _bench(["--gpus", "4", "--launch-check"], {"WORLD_SIZE": "2", "RANK": "0"})
+    assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr

@@ -1,10 +1,11 @@
 """GPU parity of the MFMA MLP kernels and the TD3 learner.
 
-Numerics: the row kernels' hidden x hidden GEMMs run on the fp16 matrix cores with both fp32
-operands scaled by powers of two and split into two fp16 planes (x 2^e = hi + lo to 22 bits) and
-the three products lo.hi + hi.lo + hi.hi accumulated in fp32; the weight-gradient kernels on the
-bf16 matrix cores with an exact three-plane bf16 split — fp32 accuracy either way, pinned here
-against an fp64 reference (max |err| / scale <= 2e-6; a two-plane bf16 split, a 16-bit-mantissa
+Numerics: every hidden x hidden GEMM (the row kernels and both weight-gradient kernels) runs on
+the fp16 matrix cores with its fp32 operands scaled by powers of two and split into two fp16
+planes (x 2^e = hi + lo to 22 significant bits): the three products lo.hi + hi.lo + hi.hi
+accumulate in fp32 (k_wgrad_fact: two, its A operand — the ReLU bit — is exact in fp16). The
+result is f32-class, not bit-fp32: pinned here against an fp64 reference at max |err| / scale
+<= 2e-6 (measured 2.4-5.7e-7; fp32 itself ~1e-7; a two-plane bf16 split, a 16-bit-mantissa
 GEMM, measures 6-8e-6 and fails it). The thin layers are fp32 fma chains. Against a
 torch fp32 reference of the same op the outputs and gradients agree to rtol 1e-4 / 1e-3 with an atol
 scaled by the operand magnitudes (stated per test)."""
@@ -827,6 +828,49 @@ def test_weight_grads_2layer_edge_cases(nav, d_in, d_out, hidden, M, splits, dy_
     err = (got[:hidden, :hidden] - ref).abs().max().item()
     assert err <= 1e-5 * scale, (err, scale)
     assert (got[hidden:, :] == 0).all() and (got[:, hidden:] == 0).all()
+
+
+@pytest.mark.parametrize("d_in,d_out", [(4, 1), (2, 2)])
+def test_weight_grads_tiny_inputs_stay_finite(nav, d_in, d_out):
+    """Degenerate h_0 scale: every input row 0 and a tiny bias (|b0| ~ 1e-36) make
+    the h_0 bound tiny, so its power-of-two scale is large; folded into large layer-0 weights
+    (|W0| in [256, 400]) it would overflow them to inf and the zero inputs would give 0 * inf =
+    NaN in the operand MFMAs. The scale is capped to keep those constants finite: both kernel
+    paths (factored d_out = 1, operand d_out = 2) must match fp64 dW_1 within 1e-5 of scale."""
+    from nav._lib import descs, lib, parr, ptr, stream_handle
+    from nav.mlp import DeviceMLP, forward
+    from oracle.td3_oracle import make_mlp_params
+    nh, hidden, M, splits = 2, 256, 4096, 4
+    p = make_mlp_params(77, [d_in, hidden, hidden, d_out])
+    rng = np.random.default_rng(5)
+    W0, b0 = p[0]
+    p[0] = ((rng.uniform(256, 400, W0.shape) * rng.choice([-1, 1], W0.shape)).astype(np.float32),
+            (rng.uniform(0.5, 1, b0.shape) * 1e-36 * rng.choice([-1, 1], b0.shape))
+            .astype(np.float32))
+    net = DeviceMLP(d_in, d_out, hidden, nh, DEV).load(p)
+    layers = [(torch.tensor(W), torch.tensor(b)) for W, b in p]
+    hp = net.hp
+    x = torch.zeros(M, d_in)
+    dy = torch.randn(M, d_out, generator=torch.Generator().manual_seed(9))
+    xd, dyd = x.to(DEV), dy.to(DEV).contiguous()
+    out = torch.zeros(M, d_out, device=DEV)
+    acts = torch.zeros(nh, M, hp, device=DEV)
+    masks = net.mask_buffer(M)
+    forward([net], xd, d_in, 0, [out], d_out, 0, M, acts=[acts], masks=[masks])
+    L = lib()
+    hs = torch.full((splits, max(4, L.nav_mlp_hidden_count(hp, nh))), float("nan"), device=DEV)
+    dz = torch.zeros(nh, M, hp, device=DEV)
+    assert L.nav_mlp_wgrad(descs(net), 1, M, ptr(xd), d_in, 0, parr(acts), parr(dz), parr(dyd),
+                           d_out, parr(masks), parr(hs), splits, stream_handle()) == 0
+    torch.cuda.synchronize()
+    got = hs.cpu().double().sum(0)[:hp * hp].view(hp, hp)
+    assert torch.isfinite(got).all()
+    bits = relu_bits(masks, nh, hp, hidden, M)
+    _, zs = _f64_forward(layers, x)
+    ref = ((dy.double() @ layers[nh][0].double()) * bits[1].double()).t() @ torch.relu(zs[0])
+    scale = ref.abs().max().item()
+    assert scale > 0
+    assert (got[:hidden, :hidden] - ref).abs().max().item() <= 1e-5 * scale
 
 
 def _fp16_image(packed, off, hp):
