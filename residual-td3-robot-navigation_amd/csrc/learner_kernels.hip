@@ -69,6 +69,10 @@ __device__ unsigned long long g_wgrad_trace[2][4][8][8];
 #endif
 
 constexpr int WG_WAVES = 8;
+// the factored form for d_out = 2 as well (A/B builds only; the product takes wgrad_rows_mfma)
+#ifndef NAV_WG_FACT_D2
+#define NAV_WG_FACT_D2 0
+#endif
 #ifndef NAV_WG_SKEW_FACT
 #define NAV_WG_SKEW_FACT 64
 #endif
@@ -973,7 +977,7 @@ __global__ __launch_bounds__(WG_THREADS) void k_wgrad_fact(WgradArgs a) {
 
 // ---------------- optimizer / target update, refreshing the packed images ----------------
 struct PackInfo {
-    int hp, n_hidden;
+    int hp, n_hidden, d_out;
     int64_t w_off[kMaxLayers];
     float* packed;
 };
@@ -986,6 +990,9 @@ struct PackInfo {
 // forward image's column n is W_L's row n (B[k][n] = W_L[n][k]: float4 reads along the row), the
 // backward image's is W_L's column n (B[k][n] = W_L[k][n]: 16 lanes on 64 consecutive bytes).
 // hp / 16 <= 16 k chunks: one load round trip and no second pass over W.
+// For d_out = 1 the TOP hidden layer's backward image holds Wt[k][n] = Wo[k] * W_L[k][n] (f32
+// products) instead of W_L: the row backward's top GEMM then takes the forward's ReLU bits as
+// its exact fp16 A operand and applies dL/dq per row after the sum (mlp_kernels.hip gemm_bits).
 struct PackJob {
     const float* p;
     PackInfo pk;
@@ -1025,6 +1032,11 @@ __global__ __launch_bounds__(kBlock) void k_pack_img(PackArgs a) {
         } else {
 #pragma unroll
             for (int t = 0; t < 16; ++t) v[t] = W[(int64_t)(k0 + t) * hp + n];
+            if (J.pk.d_out == 1 && L == J.pk.n_hidden - 1) {  // workgroup-uniform
+                const float* Wo = J.p + J.pk.w_off[J.pk.n_hidden];
+#pragma unroll
+                for (int t = 0; t < 16; ++t) v[t] = Wo[k0 + t] * v[t];
+            }
         }
 #pragma unroll
         for (int t = 0; t < 16; ++t) m = fmaxf(m, fabsf(v[t]));
@@ -1362,6 +1374,7 @@ PackInfo pack_info(const MlpDev& d, float* packed) {
     PackInfo pk;
     pk.hp = d.hp;
     pk.n_hidden = d.n_hidden;
+    pk.d_out = d.d_out;
     for (int l = 0; l < kMaxLayers; ++l) pk.w_off[l] = l <= d.n_hidden ? d.w_off[l] : 0;
     pk.packed = d.n_hidden > 1 ? packed : nullptr;
     return pk;
@@ -1465,7 +1478,7 @@ static int wgrad_args(const nav_mlp* nets, int32_t n_nets, int64_t M, const floa
     // the factored path for the critics (d_out = 1); the actor's d_out = 2 would need two
     // accumulator sets and two splits per element (measured slower than wgrad_rows_mfma: 40 vs
     // 34 us at 2x256, profiles/r04c)
-    a.fact = wgrad_fact_ok(hp, nh) && a.net[0].d_out == 1;
+    a.fact = wgrad_fact_ok(hp, nh) && (a.net[0].d_out == 1 || NAV_WG_FACT_D2);
     // 64-row aligned splits and per-wave ranges: a chunk's mask row tiles start on a tile boundary
     a.per_split = ((M + splits - 1) / splits + WG_CHUNK - 1) / WG_CHUNK * WG_CHUNK;
     a.per_wave = ((a.per_split + WG_WAVES - 1) / WG_WAVES + WG_CHUNK - 1) / WG_CHUNK * WG_CHUNK;
@@ -1492,6 +1505,7 @@ int nav_mlp_wgrad(const nav_mlp* nets, int32_t n_nets, int64_t M, const float* i
     // the factored kernel: its 4 KB fragment table is static, the dynamic part the reduce slots
     const size_t lds = a.fact ? (size_t)WG_WAVES * WG_TILE * WG_TILE * 4 : wgrad_lds_bytes();
     void (*k)(WgradArgs) = !a.fact ? k_wgrad
+                           : a.net[0].d_out == 2 ? k_wgrad_fact<2, 2>
                            : a.tn == 128 ? k_wgrad_fact<4, 1> : k_wgrad_fact<2, 1>;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

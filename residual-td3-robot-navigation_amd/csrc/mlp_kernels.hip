@@ -218,8 +218,219 @@ NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const float* __restr
     }
 }
 
+// ---- the top hidden layer's row backward of a d_out = 1 network on its ReLU bits ----
+// dz_{L-1}[r][c] = e_{L-1}[r][c] * sum_n dz_L[r][n] W_L[n][c] with dz_L[r][n] = e_L[r][n] g[r]
+// Wo[n] (g = dL/dq, e = the forward's ReLU bits) is g[r] * sum_n e_L[r][n] Wt[n][c], Wt[n][c] =
+// Wo[n] W_L[n][c]: the A operand is the bit matrix itself, exact in fp16 (0 / 1.0), so only B (the
+// Wt image, k_pack_img) is split and each k step takes 2 products instead of 3; no A rows, no
+// split stage, no barrier in the product. The bits come row-major from LDS: word w of row r holds
+// e_L[r][32 w .. 32 w + 31] (bits_stage), one byte per lane and k step picks a 16-B fragment of
+// the 256-entry table of 8 fp16 zeros / ones.
+#ifndef NAV_BITS_VALUFRAG
+#define NAV_BITS_VALUFRAG 0
+#endif
+constexpr int kBitTab = 256 * 4;  // floats of the fragment table (256 x 16 B)
+// LDS words per row of the bit image: NT + 1 (odd: the 32 lanes of a half read 32 rows without a
+// bank conflict)
+template <int NT>
+constexpr int bit_ws() { return NT + 1; }
+
+// The fragment table (entry b: fp16 bit j of b at element j) and the bit image of the lanes'
+// C-layout mask words (mb[rt][j]: bit i = row c_row(rt, i, h), column t_j * 32 + l32) into the
+// scratch at `scr` (tab [256][4] u32, then bits [TM][bit_ws] u32, then g [TM]). One ballot per
+// (row tile, column tile, C element) yields a row's word for the wave's column tile (lanes h = 0:
+// row +0, h = 1: row +4); writelane parks it at the row's lane, lanes 0-31 carry the first tile
+// and 32-63 the second, and one store per row tile writes both.
+template <int NT, int RT>
+NAV_DEV void bits_stage(float* scr, const uint32_t (&mb)[RT][2], const float* dys) {
+    constexpr int TM = RT * 32, WS = bit_ws<NT>();
+    const int tid = threadIdx.x, lane = tid & 63;
+    const WaveCols<NT> wc(wave_id());
+    static_assert((kBitTab + TM * WS + TM) * 4 <= TM * (NT * 32 + 4) * 4,
+                  "the bit scratch fits in the block's LDS rows");
+    uint32_t* tab = reinterpret_cast<uint32_t*>(scr);
+    uint32_t* bw = tab + kBitTab;
+    float* gq = reinterpret_cast<float*>(bw + TM * WS);
+    {
+        const uint32_t b = (uint32_t)tid;  // kBlock = 256 entries
+        uint4 e;
+        e.x = ((b & 1u) ? 0x3C00u : 0u) | ((b & 2u) ? 0x3C000000u : 0u);
+        e.y = ((b & 4u) ? 0x3C00u : 0u) | ((b & 8u) ? 0x3C000000u : 0u);
+        e.z = ((b & 16u) ? 0x3C00u : 0u) | ((b & 32u) ? 0x3C000000u : 0u);
+        e.w = ((b & 64u) ? 0x3C00u : 0u) | ((b & 128u) ? 0x3C000000u : 0u);
+        reinterpret_cast<uint4*>(tab)[tid] = e;
+    }
+    if (tid < TM) gq[tid] = dys[tid * 4];
+    // per row tile: lanes 0-31 build the column words of the wave's first tile, lanes 32-63 of
+    // its second (one exchange across the halves: lane (h, l32) holds rows +4h of both), then a
+    // 32 x 32 bit transpose inside each half (5 butterfly exchanges) leaves row l32's word of its
+    // half's tile in lane l32. VGPR shuffles only: a ballot form (v_cmp to an SGPR pair, selects
+    // on it) gave timing-dependent words in the older workgroup of a co-resident pair
+    // (tools/dbg_bits.py, profiles/r06g).
+    const int h = lane >> 5;
+    auto spread = [](uint32_t w) {  // nibble k of a 16-bit word -> bits 8k .. 8k + 3
+        return (w & 0xFu) | ((w & 0xF0u) << 4) | ((w & 0xF00u) << 8) | ((w & 0xF000u) << 12);
+    };
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+        const uint32_t send = h ? mb[rt][0] : mb[rt][1];
+        const uint32_t recv = (uint32_t)__shfl_xor((int)send, 32, 64);
+        const uint32_t w0 = h ? recv : mb[rt][0], w1 = h ? mb[rt][1] : recv;
+        // bit r of x = E[rt * 32 + r][column (tile h) * 32 + l32]
+        uint32_t x = spread(w0) | (spread(w1) << 4);
+#pragma unroll
+        for (int st = 0; st < 5; ++st) {
+            const int sft = 16 >> st;
+            const uint32_t m = st == 0 ? 0x0000FFFFu : st == 1 ? 0x00FF00FFu
+                             : st == 2 ? 0x0F0F0F0Fu : st == 3 ? 0x33333333u : 0x55555555u;
+            const uint32_t y = (uint32_t)__shfl_xor((int)x, sft, 64);
+            x = (lane & sft) ? (((y >> sft) & m) | (x & ~m)) : ((x & m) | ((y & m) << sft));
+        }
+        if (h == 0 ? wc.has0 : wc.has1)
+            bw[(rt * 32 + (lane & 31)) * WS + (h == 0 ? wc.t0 : wc.t1)] = x;
+    }
+}
+
+// acc[rt][j] = g[row] * (E[TM rows][hp] (bit image) x Wt[hp][tile t_j]) from bits_stage's
+// scratch and the Wt image (B planes PF steps ahead as in gemm_cols; the A fragments one step
+// ahead). Unscaled and multiplied by g[row] before it returns.
+template <int NT, int RT, int PFB = 1>
+NAV_DEV void gemm_bits(const float* scr, const float* __restrict__ img, f32x16 (&acc)[RT][2]) {
+    constexpr int hp = NT * 32;
+    constexpr int nq = hp / 16;
+    constexpr int TM = RT * 32, WS = bit_ws<NT>();
+    constexpr size_t PL = (size_t)nq * 2 * hp;
+    constexpr size_t STEP = 2 * (size_t)hp;
+    const int lane = threadIdx.x & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
+    const WaveCols<NT> wc(wv);
+    const uint4* tab = reinterpret_cast<const uint4*>(scr);
+    const uint32_t* bw = reinterpret_cast<const uint32_t*>(scr) + kBitTab;
+    const float* gq = reinterpret_cast<const float*>(bw + TM * WS);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[rt][j][i] = 0.f;
+    // the zero accumulators as registers: folded into an inline-constant C operand, the first
+    // product's untied destination was allocated over its own B fragment, and the results came
+    // out timing-dependent (a few rows per launch; tools/dbg_bits.py, profiles/r06d)
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) pin_value(acc[rt][j]);
+    const int t0 = wc.has0 ? wc.t0 : 0, t1 = wc.has1 ? wc.t1 : t0;
+    const int* ex = image_exps(img, hp);
+    const int eb0 = ex[t0 * 32 + l32], eb1 = ex[t1 * 32 + l32];
+    const char* Bb = reinterpret_cast<const char*>(img);
+    const uint32_t o0 = (uint32_t)(h * hp + t0 * 32 + l32) * 16u;
+    const uint32_t o1 = (uint32_t)(h * hp + t1 * 32 + l32) * 16u;
+    auto ldB = [&](uint32_t o, int p, int q) {
+        return *reinterpret_cast<const f16x8*>(Bb + (o + (uint32_t)((p * PL + q * STEP) * 16)));
+    };
+    // B prefetch distance in k steps as gemm_cols
+    constexpr int PF = RT == 1 ? 2 : PFB;
+    f16x8 bq0[PF + 1][2], bq1[PF + 1][2];
+#pragma unroll
+    for (int d = 0; d < PF; ++d)
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const int qd = d < nq ? d : nq - 1;
+            bq0[d][p] = ldB(o0, p, qd);
+            bq1[d][p] = ldB(o1, p, qd);
+        }
+    // the lane's row words (row rt * 32 + l32; word q / 2 covers k steps q, q + 1) and the A
+    // fragment of step q: byte 2 (q & 1) + h of word q / 2
+    const uint32_t* wrow = bw + l32 * WS;
+    uint32_t w[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) w[rt] = wrow[rt * 32 * WS];
+    auto frag = [&](int q, int rt) {
+        const uint32_t byte = (w[rt] >> (16 * (q & 1) + 8 * h)) & 0xFFu;
+#if NAV_BITS_VALUFRAG
+        // bits 2m, 2m + 1 -> fp16 1.0 / 0 in the two halves of dword m: (b0 | b1 << 16) * 0x3C00
+        (void)tab;
+        uint4 e;
+        uint32_t d[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const uint32_t t = byte >> (2 * m);
+            d[m] = __builtin_amdgcn_mul_u24((t & 1u) | ((t & 2u) << 15), 0x3C00u);
+        }
+        e.x = d[0]; e.y = d[1]; e.z = d[2]; e.w = d[3];
+        return __builtin_bit_cast(f16x8, e);
+#else
+        return __builtin_bit_cast(f16x8, tab[byte]);
+#endif
+    };
+    f16x8 af[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) af[rt] = frag(0, rt);
+    const bool favored = (blockIdx.x / kCUs) & 1;  // gemm_cols' co-resident balance
+    if (favored) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int q = 0; q < nq; ++q) {
+        // step q + 1's operands first in program order (in flight under step q's MFMAs)
+        const int qb = q + PF;
+        if (qb < nq) {
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+                bq0[qb % (PF + 1)][p] = ldB(o0, p, qb);
+                bq1[qb % (PF + 1)][p] = ldB(o1, p, qb);
+            }
+        }
+        f16x8 an[RT];
+        if (q + 1 < nq) {
+            if ((q & 1) == 1) {
+#pragma unroll
+                for (int rt = 0; rt < RT; ++rt) w[rt] = wrow[rt * 32 * WS + ((q + 1) >> 1)];
+            }
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) an[rt] = frag(q + 1, rt);
+        }
+        if (wc.has0) {  // wave-uniform
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) {
+                const f16x8(&b0)[2] = bq0[q % (PF + 1)];
+                acc[rt][0] = mfma_h(af[rt], b0[1], acc[rt][0]);
+                acc[rt][0] = mfma_h(af[rt], b0[0], acc[rt][0]);
+                if (NT >= 8 || wc.has1) {
+                    const f16x8(&b1)[2] = bq1[q % (PF + 1)];
+                    acc[rt][1] = mfma_h(af[rt], b1[1], acc[rt][1]);
+                    acc[rt][1] = mfma_h(af[rt], b1[0], acc[rt][1]);
+                }
+            }
+        }
+        if (q + 1 < nq) {
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) af[rt] = an[rt];
+        }
+        // a scheduling fence per k step: without a barrier in the loop the scheduler would sink
+        // the prefetched loads down to their uses (a full L2 / LDS round trip exposed per step)
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    if (favored) __builtin_amdgcn_s_setprio(0);
+    // unscale 2^-e_n (exact), then dL/dq of the element's row, in place one group of 4 rows at
+    // a time (fenced: hoisting every g load and keeping the unscaled copies beside the
+    // accumulators pushed the row kernels past 256 registers, one workgroup per CU)
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const float4 g = *reinterpret_cast<const float4*>(gq + rt * 32 + 8 * m + 4 * h);
+            const float gv[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int i = 4 * m + u;
+                acc[rt][0][i] = ldexpf(acc[rt][0][i], -eb0) * gv[u];
+                acc[rt][1][i] = ldexpf(acc[rt][1][i], -eb1) * gv[u];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+}
+
 // the fp16 B images of hidden layer L (1 .. n_hidden-1): forward (B[k][n] = W_L[n][k]) and
-// backward (B[k][n] = W_L[k][n])
+// backward (B[k][n] = W_L[k][n]; for d_out = 1 the top layer's is Wo[k] W_L[k][n], gemm_bits)
 NAV_DEV const float* img_fwd(const MlpDev& net, int L) {
     return net.packed + (int64_t)(L - 1) * 2 * split_image_floats(net.hp);
 }
@@ -1054,7 +1265,11 @@ NAV_DEV void mask_and_store(f32x16 (&acc)[RT][2], const uint32_t (&mbits)[RT][2]
 // forward's ReLU bits in masks; leaves dz_0 in the LDS rows `act`. With es: the per-block edge
 // partials (every bias, dW0 from the input rows xin [TM][4], and dWo / dbo when h_top [M][hp] is
 // given); dz_L rows to dz for save_mask bits.
-template <int NT, int RT, int PFB = 1>
+// BM: the top layer's product form. 0: every layer on gemm_cols (any d_out); 1: d_out = 1, the
+// top layer on gemm_bits, the layers below on gemm_cols (n_hidden >= 3); 2: d_out = 1 and
+// n_hidden = 2, gemm_bits only. Compile-time, so a kernel carries only the forms it runs (both
+// forms in one function took the row kernels past 256 registers: one workgroup per CU).
+template <int NT, int RT, int PFB = 1, int BM = 0>
 NAV_DEV void bwd_net(const MlpDev& net, float* act, _Float16* stage, const float* dys, const float* xin,
                      const uint16_t* masks, int64_t n_rt, float* es, const float* h_top,
                      float* dz, uint32_t save_mask, int64_t row0, int64_t M, int64_t rt0,
@@ -1099,9 +1314,16 @@ NAV_DEV void bwd_net(const MlpDev& net, float* act, _Float16* stage, const float
         }
     }
 
+    // d_out = 1: the top layer's backward product runs on the forward's ReLU bits (gemm_bits; the
+    // Wt image is the only backward image of that layer); its dz rows are still formed (and
+    // copied out) where save_mask asks for them
+    constexpr bool bits_path = BM > 0;
+    const bool save_top = (save_mask >> (nh - 1)) & 1u;
     // top hidden layer: dz = (dy . Wo) * relu'(.), in the C layout: one K = 2 MFMA per tile of
     // dy rows (lane l32 = row, h = output) against Wo's columns, fma(dy1, w1, dy0 w0) — the
-    // chain the weight-gradient kernel recomputes — then the forward's ReLU bits
+    // chain the weight-gradient kernel recomputes — then the forward's ReLU bits. On the bits
+    // path these registers only feed the layer's bias partials (and are skipped without es).
+    uint32_t mb[RT][2];
     {
         const float* Wo = net.params + net.w_off[nh];
         const uint16_t* mk = masks + (size_t)(nh - 1) * mstride;
@@ -1112,7 +1334,6 @@ NAV_DEV void bwd_net(const MlpDev& net, float* act, _Float16* stage, const float
             const float4 g = *reinterpret_cast<const float4*>(dys + (rt * 32 + l32) * 4);
             ga[rt] = h < d_out ? (h ? g.y : g.x) : 0.f;
         }
-        uint32_t mb[RT][2];
         if (top_bits) {  // the forward's bits of this top layer, still in registers
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt)
@@ -1121,19 +1342,33 @@ NAV_DEV void bwd_net(const MlpDev& net, float* act, _Float16* stage, const float
         } else {
             load_mask_bits<NT, RT>(mk, rt0, mb);
         }
-        f32x16 z[RT][2];
+        if (!bits_path || (es && nh > 1) || save_top) {
+            f32x16 z[RT][2];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const bool has = j == 0 ? wc.has0 : wc.has1;
-            const int c = (j == 0 ? wc.t0 : has ? wc.t1 : wc.t0) * 32 + l32;
-            // the forward's Wo registers: wo.w[output][tile] holds Wo[output][c] (0 when absent)
-            const float wb = wo_in ? (h ? wo_in->w[1][j] : wo_in->w[0][j])
-                                   : has && h < d_out ? Wo[h * hp + c] : 0.f;
+            for (int j = 0; j < 2; ++j) {
+                const bool has = j == 0 ? wc.has0 : wc.has1;
+                const int c = (j == 0 ? wc.t0 : has ? wc.t1 : wc.t0) * 32 + l32;
+                // the forward's Wo registers: wo.w[output][tile] holds Wo[output][c] (0 when absent)
+                const float wb = wo_in ? (h ? wo_in->w[1][j] : wo_in->w[0][j])
+                                       : has && h < d_out ? Wo[h * hp + c] : 0.f;
 #pragma unroll
-            for (int rt = 0; rt < RT; ++rt) z[rt][j] = mfma(ga[rt], wb, zero);
+                for (int rt = 0; rt < RT; ++rt) z[rt][j] = mfma(ga[rt], wb, zero);
+            }
+            if (bits_path && !save_top)
+                mask_regs<NT, RT>(z, mb);
+            else
+                mask_and_store<NT, RT>(z, mb, act, SS,
+                                       !bits_path && nh > 1 ? amax_slots<TM>(stage) : nullptr);
+            if (es && nh > 1) edge_regs<NT, RT>(net, z, xin, nh - 1, es);
         }
-        mask_and_store<NT, RT>(z, mb, act, SS, nh > 1 ? amax_slots<TM>(stage) : nullptr);
-        if (es && nh > 1) edge_regs<NT, RT>(net, z, xin, nh - 1, es);
+        if (bits_path) {
+            if (save_top) {  // the top layer's dz rows themselves, before the scratch reuses act
+                __syncthreads();
+                copy_rows<NT, RT>(act, SS, dz + (int64_t)(nh - 1) * MH, row0, M);
+                __syncthreads();
+            }
+            bits_stage<NT, RT>(act, mb, dys);
+        }
     }
     NAV_MARK(mk + 1);
     __syncthreads();
@@ -1147,16 +1382,12 @@ NAV_DEV void bwd_net(const MlpDev& net, float* act, _Float16* stage, const float
         }
         if ((save_mask >> L) & 1u) copy_rows<NT, RT>(act, SS, dz + (int64_t)L * MH, row0, M);
     };
-    finish_layer(nh - 1);
+    if (!bits_path) finish_layer(nh - 1);
     NAV_MARK(mk + 2);
 
-    // hidden layers, top-down: dz_{L-1} = (dz_L . W_L) * relu'(act_{L-1}), B = packed Wb_L
-    for (int L = nh - 1; L >= 1; --L) {
-        f32x16 acc[RT][2];
-        uint32_t mbits[RT][2];
-        load_mask_bits<NT, RT>(masks + (size_t)(L - 1) * mstride, rt0, mbits);
-        gemm_cols<NT, RT, PFB>(act, SS, img_bwd(net, L), stage, acc);
-        NAV_MARK(mk + 3);
+    // after layer L's product (acc = dz_L . W_L): mask with layer L - 1's bits, its rows to LDS
+    // where a reader follows, its edge partials
+    auto after_product = [&](int L, f32x16 (&acc)[RT][2], const uint32_t (&mbits)[RT][2]) {
         __syncthreads();
         // layer 0's rows only when a reader follows (the caller's dx, the save copy); its edge
         // partials come from the registers
@@ -1168,6 +1399,27 @@ NAV_DEV void bwd_net(const MlpDev& net, float* act, _Float16* stage, const float
         __syncthreads();
         NAV_MARK(mk + 4);
         finish_layer(L - 1);
+    };
+    int Ltop = nh - 1;
+    if (bits_path) {
+        f32x16 acc[RT][2];
+        uint32_t mbits[RT][2];
+        load_mask_bits<NT, RT>(masks + (size_t)(nh - 2) * mstride, rt0, mbits);
+        gemm_bits<NT, RT, PFB>(act, img_bwd(net, nh - 1), acc);
+        NAV_MARK(mk + 3);
+        after_product(nh - 1, acc, mbits);
+        Ltop = nh - 2;
+    }
+    // hidden layers, top-down: dz_{L-1} = (dz_L . W_L) * relu'(act_{L-1}), B = packed Wb_L
+    if constexpr (BM != 2) {
+        for (int L = Ltop; L >= 1; --L) {
+            f32x16 acc[RT][2];
+            uint32_t mbits[RT][2];
+            load_mask_bits<NT, RT>(masks + (size_t)(L - 1) * mstride, rt0, mbits);
+            gemm_cols<NT, RT, PFB>(act, SS, img_bwd(net, L), stage, acc);
+            NAV_MARK(mk + 3);
+            after_product(L, acc, mbits);
+        }
     }
     NAV_MARK(mk + 5);
 
@@ -1184,7 +1436,7 @@ NAV_DEV float dx_unit(const MlpDev& net, const float* act, int rloc, int jj) {
     return acc;
 }
 
-template <int NT, int RT>
+template <int NT, int RT, int BM>
 __global__ __launch_bounds__(kBlock, 1) void k_mlp_bwd(BwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     constexpr int hp = NT * 32, SS = hp + 4, TM = RT * 32;
@@ -1216,8 +1468,8 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_bwd(BwdArgs a) {
         *reinterpret_cast<float4*>(xin + tid * 4) = make_float4(xi[0], xi[1], xi[2], xi[3]);
     }
     __syncthreads();
-    bwd_net<NT, RT>(net, act, stage, dys, xin, a.masks[y], n_rt, es, a.h_top[y], a.dz[y], a.save_mask,
-                    row0, M, rt0);
+    bwd_net<NT, RT, 1, BM>(net, act, stage, dys, xin, a.masks[y], n_rt, es, a.h_top[y], a.dz[y],
+                           a.save_mask, row0, M, rt0);
 
     // dx = dz_0 . W0 : thread = (row, input)
     if (a.dx[y]) {
@@ -1278,7 +1530,9 @@ struct CriticRowsArgs {
 // critics with mse_loss's gradient, the loss and the output layers' gradient partials, and
 // (row_backward) each online critic's row backward with its W0 / bias partials right after its
 // forward, while its rows and ReLU bits are fresh.
-template <int NT, int RT>
+// CBM: the critics' row-backward form (bwd_net's BM: 0 for one hidden layer, else 1), chosen by
+// the launcher from n_hidden
+template <int NT, int RT, int CBM>
 __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     constexpr int hp = NT * 32, SS = hp + 4, TM = RT * 32;
@@ -1389,7 +1643,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
                 *reinterpret_cast<float4*>(dys + tid * 4) =
                     make_float4(red[kWaves * TM + tid], 0.f, 0.f, 0.f);  // loss_epilogue's dq
             __syncthreads();
-            bwd_net<NT, RT, kPfWide>(a.critic[q], act, stage, dys, xin, a.masks[q], n_rt, es, nullptr, a.dz[q],
+            bwd_net<NT, RT, kPfWide, CBM>(a.critic[q], act, stage, dys, xin, a.masks[q], n_rt, es, nullptr, a.dz[q],
                             a.dz_save_mask, row0, B, rt0, 29 + 14 * q, top_bits, &wo, false);
             __syncthreads();  // the next forward's layer 0 overwrites the rows
         }
@@ -1423,7 +1677,7 @@ struct ActorRowsArgs {
 // critic-1 forward on (s, pi(s)), backward of -mean(Q) through critic 1 to its action input
 // (critic grads discarded, as zero_grad does), and the actor's row backward with its edge
 // partials.
-template <int NT, int RT>
+template <int NT, int RT, int CBM>
 __global__ __launch_bounds__(kBlock, 1) void k_td3_actor_rows(ActorRowsArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     constexpr int hp = NT * 32, SS = hp + 4, TM = RT * 32;
@@ -1470,8 +1724,8 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_actor_rows(ActorRowsArgs a) {
     fwd_net<NT, RT>(a.critic, act, stage, xin, red, a.masks_c, n_rt, nullptr, 0u, row0, B, rt0, top,
                     -64, &l0_c, top_bits, &wo);
     if (tid < TM && a.q && row0 + tid < B) a.q[row0 + tid] = out_y<RT>(a.critic, red, tid, 0);
-    bwd_net<NT, RT>(a.critic, act, stage, dys, xin, a.masks_c, n_rt, nullptr, nullptr, nullptr, 0u, row0,
-                    B, rt0, -64, top_bits, &wo);
+    bwd_net<NT, RT, 1, CBM>(a.critic, act, stage, dys, xin, a.masks_c, n_rt, nullptr, nullptr,
+                                    nullptr, 0u, row0, B, rt0, -64, top_bits, &wo);
     if (tid < 2 * TM) {
         const int rloc = tid % TM, j = tid / TM;
         const int64_t r = row0 + rloc;
@@ -1541,7 +1795,11 @@ void launch_fwd_k(const FwdArgs& a, int n_nets, hipStream_t st) {
 template <int NT, int RT>
 void launch_bwd_k(const BwdArgs& a, int n_nets, hipStream_t st) {
     const size_t lds = lds_bytes(NT * 32, RT * 32);
-    auto k = k_mlp_bwd<NT, RT>;
+    // d_out = 1 networks' top backward image is the Wt image: their top product is gemm_bits
+    const int nh = a.net[0].n_hidden;
+    auto k = a.net[0].d_out != 1 || nh < 2 ? k_mlp_bwd<NT, RT, 0>
+             : nh == 2                      ? k_mlp_bwd<NT, RT, 2>
+                                            : k_mlp_bwd<NT, RT, 1>;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
     const dim3 grid((unsigned)((a.M + RT * 32 - 1) / (RT * 32)), (unsigned)n_nets);
@@ -1554,7 +1812,9 @@ void launch_critic_rows_k(const CriticRowsArgs& a, hipStream_t st) {
     const size_t lds =
         ((size_t)TM * (NT * 32 + 4) + TM * 4 + red_floats(TM) + TM * 8 + TM + TM * 4) * 4 +
         stage_bytes(TM);
-    auto k = k_td3_critic_rows<NT, RT>;
+    // form 1 also for 2 hidden layers (its gemm_cols loop then runs no layer): the form-2
+    // instantiation came out at 286 registers (one workgroup per CU), form 1 at 236
+    auto k = a.critic[0].n_hidden == 1 ? k_td3_critic_rows<NT, RT, 0> : k_td3_critic_rows<NT, RT, 1>;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
     hipLaunchKernelGGL(k, dim3((unsigned)((a.B + TM - 1) / TM), a.split_twins ? 2u : 1u),
@@ -1566,7 +1826,7 @@ void launch_actor_rows_k(const ActorRowsArgs& a, hipStream_t st) {
     constexpr int TM = RT * 32;
     const size_t lds = ((size_t)TM * (NT * 32 + 4) + TM * 4 + red_floats(TM) + TM * 8) * 4 +
                        stage_bytes(TM);
-    auto k = k_td3_actor_rows<NT, RT>;
+    auto k = a.critic.n_hidden == 1 ? k_td3_actor_rows<NT, RT, 0> : k_td3_actor_rows<NT, RT, 1>;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
     hipLaunchKernelGGL(k, dim3((unsigned)((a.B + TM - 1) / TM)), dim3(kBlock), lds, st, a);

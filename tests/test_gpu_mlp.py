@@ -894,7 +894,7 @@ def _pow2_exp(m):
 
 def _assert_images_exact(net, tag):
     """Every hidden x hidden weight: the forward image (B[k][n] = W[n][k]) and the backward image
-    (B[k][n] = W[k][n]) hold, per column n with e_n = pow2_exp(max_k |B[k][n]|), hi =
+    (B[k][n] = W[k][n]; for d_out = 1 the top layer's is Wt[k][n] = Wo[k] W[k][n] in f32) hold, per column n with e_n = pow2_exp(max_k |B[k][n]|), hi =
     fp16_rne(B 2^e_n) and lo = fp16_rne(B 2^e_n - hi) bit for bit, and (hi + lo) 2^-e_n equals B
     within 2^-22 of the column's max (11 + 11 significant bits)."""
     hp, nh = net.hp, net.n_hidden
@@ -904,7 +904,11 @@ def _assert_images_exact(net, tag):
     for L in range(1, nh):
         w_off = net.offsets[L][0]
         W = flat[w_off:w_off + hp * hp].view(hp, hp)
-        for which, off, Bk in (("fwd", (L - 1) * 2 * img, W.t()), ("bwd", (L - 1) * 2 * img + img, W)):
+        Wb = W
+        if net.d_out == 1 and L == nh - 1:  # the top layer's Wt image: Wo[k] * W[k][n] (f32)
+            wo = flat[net.offsets[nh][0]:net.offsets[nh][0] + hp]
+            Wb = wo[:, None] * W
+        for which, off, Bk in (("fwd", (L - 1) * 2 * img, W.t()), ("bwd", (L - 1) * 2 * img + img, Wb)):
             P, e = _fp16_image(pk, off, hp)
             cmax = Bk.abs().max(0).values
             want = torch.tensor([_pow2_exp(float(m)) for m in cmax], dtype=torch.int32)

@@ -20,10 +20,10 @@ case $unit in
            objs=${objs/$B\/learner_kernels.o/abl\/$name.o} ;;
   env) /opt/rocm/bin/hipcc $FL $flags -c $P/csrc/env_kernels.hip -o abl/$name.o
        objs=${objs/$B\/env_kernels.o/abl\/$name.o} ;;
-  mlp0) /opt/rocm/bin/hipcc $FL -mllvm -amdgpu-mfma-vgpr-form=1 -mllvm -amdgpu-sched-strategy=max-ilp $flags -DNAV_MLP_PART=0 -c $P/csrc/mlp_kernels.hip -o abl/$name.o
+  mlp0) /opt/rocm/bin/hipcc $FL -mllvm -amdgpu-mfma-vgpr-form=1 -mllvm -amdgpu-sched-strategy=max-ilp -fno-slp-vectorize $flags -DNAV_MLP_PART=0 -c $P/csrc/mlp_kernels.hip -o abl/$name.o
         objs=${objs/$B\/mlp_kernels.o/abl\/$name.o} ;;
   mlp[1-8]) n=${unit#mlp}
-        /opt/rocm/bin/hipcc $FL -mllvm -amdgpu-mfma-vgpr-form=1 -mllvm -amdgpu-sched-strategy=max-ilp $flags -DNAV_MLP_PART=$n -c $P/csrc/mlp_kernels.hip -o abl/$name.o
+        /opt/rocm/bin/hipcc $FL -mllvm -amdgpu-mfma-vgpr-form=1 -mllvm -amdgpu-sched-strategy=max-ilp -fno-slp-vectorize $flags -DNAV_MLP_PART=$n -c $P/csrc/mlp_kernels.hip -o abl/$name.o
         objs=${objs/$B\/mlp_nt$n.o/abl\/$name.o} ;;
   mlp8agpr) /opt/rocm/bin/hipcc $FL $flags -DNAV_MLP_PART=8 -c $P/csrc/mlp_kernels.hip -o abl/$name.o
         objs=${objs/$B\/mlp_nt8.o/abl\/$name.o} ;;

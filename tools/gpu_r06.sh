@@ -98,6 +98,9 @@ for step in "$@"; do
             run launch_shared 300 python bench.py --gpus 2 --steps 20 --warmup 2 --long-steps 0 --shared-policy &&
             run launch_overlap 300 python bench.py --gpus 2 --steps 20 --warmup 2 --long-steps 0 --shared-policy --overlap-collect
             unset NAV_DIST_REHEARSAL ;;
+    dbgvar) for v in $DVARS; do run dbg_$v 120 python tools/withlib.py "$ROOT/abl/libnavenv_$v.so" tools/dbg_bits.py --batch 16421; done ;;
+    dbgbits) run dbgbits_16421 120 python tools/dbg_bits.py --batch 16421 &&
+             run dbgbits_2048 120 python tools/dbg_bits.py --batch 2048 ;;
     config1) run config1 300 python tools/config1_run.py ;;
     mix) run mix 100 ./build/mix_probe ;;
     shape) run shape 200 ./build/mfma_shape_probe 512 2.5 0 && run shape_dz 200 ./build/mfma_shape_probe 512 2.5 1 ;;
