@@ -69,10 +69,6 @@ __device__ unsigned long long g_wgrad_trace[2][4][8][8];
 #endif
 
 constexpr int WG_WAVES = 8;
-// the factored form for d_out = 2 as well (A/B builds only; the product takes wgrad_rows_mfma)
-#ifndef NAV_WG_FACT_D2
-#define NAV_WG_FACT_D2 0
-#endif
 #ifndef NAV_WG_SKEW_FACT
 #define NAV_WG_SKEW_FACT 64
 #endif
@@ -1477,8 +1473,8 @@ static int wgrad_args(const nav_mlp* nets, int32_t n_nets, int64_t M, const floa
     a.n_hid = (nh - 1) * a.TN * a.TT;
     // the factored path for the critics (d_out = 1); the actor's d_out = 2 would need two
     // accumulator sets and two splits per element (measured slower than wgrad_rows_mfma: 40 vs
-    // 34 us at 2x256, profiles/r04c)
-    a.fact = wgrad_fact_ok(hp, nh) && (a.net[0].d_out == 1 || NAV_WG_FACT_D2);
+    // 34 us at 2x256 on bf16, profiles/r04c; on the fp16 split 31.9 vs 25.4 us, r06r)
+    a.fact = wgrad_fact_ok(hp, nh) && a.net[0].d_out == 1;
     // 64-row aligned splits and per-wave ranges: a chunk's mask row tiles start on a tile boundary
     a.per_split = ((M + splits - 1) / splits + WG_CHUNK - 1) / WG_CHUNK * WG_CHUNK;
     a.per_wave = ((a.per_split + WG_WAVES - 1) / WG_WAVES + WG_CHUNK - 1) / WG_CHUNK * WG_CHUNK;
@@ -1505,7 +1501,6 @@ int nav_mlp_wgrad(const nav_mlp* nets, int32_t n_nets, int64_t M, const float* i
     // the factored kernel: its 4 KB fragment table is static, the dynamic part the reduce slots
     const size_t lds = a.fact ? (size_t)WG_WAVES * WG_TILE * WG_TILE * 4 : wgrad_lds_bytes();
     void (*k)(WgradArgs) = !a.fact ? k_wgrad
-                           : a.net[0].d_out == 2 ? k_wgrad_fact<2, 2>
                            : a.tn == 128 ? k_wgrad_fact<4, 1> : k_wgrad_fact<2, 1>;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -226,9 +226,6 @@ NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const float* __restr
 // split stage, no barrier in the product. The bits come row-major from LDS: word w of row r holds
 // e_L[r][32 w .. 32 w + 31] (bits_stage), one byte per lane and k step picks a 16-B fragment of
 // the 256-entry table of 8 fp16 zeros / ones.
-#ifndef NAV_BITS_VALUFRAG
-#define NAV_BITS_VALUFRAG 0
-#endif
 constexpr int kBitTab = 256 * 4;  // floats of the fragment table (256 x 16 B)
 // LDS words per row of the bit image: NT + 1 (odd: the 32 lanes of a half read 32 rows without a
 // bank conflict)
@@ -241,6 +238,32 @@ constexpr int bit_ws() { return NT + 1; }
 // (row tile, column tile, C element) yields a row's word for the wave's column tile (lanes h = 0:
 // row +0, h = 1: row +4); writelane parks it at the row's lane, lanes 0-31 carry the first tile
 // and 32-63 the second, and one store per row tile writes both.
+// lane ^ M_ across the wave: DPP moves inside 16-lane rows for M_ <= 8 (out_partials, bits_stage)
+template <int M_>
+NAV_DEV float lane_xor(float v) {
+    const int x = __float_as_int(v);
+    if constexpr (M_ == 1) {
+        return __int_as_float(__builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false));  // [1,0,3,2]
+    } else if constexpr (M_ == 2) {
+        return __int_as_float(__builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, false));  // [2,3,0,1]
+    } else if constexpr (M_ == 4) {
+        const int m7 = __builtin_amdgcn_mov_dpp(x, 0x141, 0xF, 0xF, false);  // l ^ 7
+        return __int_as_float(__builtin_amdgcn_mov_dpp(m7, 0x1B, 0xF, 0xF, false));  // ^ 3
+    } else if constexpr (M_ == 8) {
+        return __int_as_float(__builtin_amdgcn_mov_dpp(x, 0x128, 0xF, 0xF, false));  // ror 8
+    } else {
+        return __shfl_xor(v, M_, 64);
+    }
+}
+
+// one stage of the 32 x 32 bit transpose: lanes l and l ^ S swap the off-diagonal S x S blocks
+// (lane_xor: DPP row moves for S <= 8, one ds_bpermute for 16)
+template <int S>
+NAV_DEV uint32_t bfly_stage(uint32_t x, int lane, uint32_t m) {
+    const uint32_t y = __float_as_uint(lane_xor<S>(__uint_as_float(x)));
+    return (lane & S) ? (((y >> S) & m) | (x & ~m)) : ((x & m) | ((y & m) << S));
+}
+
 template <int NT, int RT>
 NAV_DEV void bits_stage(float* scr, const uint32_t (&mb)[RT][2], const float* dys) {
     constexpr int TM = RT * 32, WS = bit_ws<NT>();
@@ -278,14 +301,11 @@ NAV_DEV void bits_stage(float* scr, const uint32_t (&mb)[RT][2], const float* dy
         const uint32_t w0 = h ? recv : mb[rt][0], w1 = h ? mb[rt][1] : recv;
         // bit r of x = E[rt * 32 + r][column (tile h) * 32 + l32]
         uint32_t x = spread(w0) | (spread(w1) << 4);
-#pragma unroll
-        for (int st = 0; st < 5; ++st) {
-            const int sft = 16 >> st;
-            const uint32_t m = st == 0 ? 0x0000FFFFu : st == 1 ? 0x00FF00FFu
-                             : st == 2 ? 0x0F0F0F0Fu : st == 3 ? 0x33333333u : 0x55555555u;
-            const uint32_t y = (uint32_t)__shfl_xor((int)x, sft, 64);
-            x = (lane & sft) ? (((y >> sft) & m) | (x & ~m)) : ((x & m) | ((y & m) << sft));
-        }
+        x = bfly_stage<16>(x, lane, 0x0000FFFFu);
+        x = bfly_stage<8>(x, lane, 0x00FF00FFu);
+        x = bfly_stage<4>(x, lane, 0x0F0F0F0Fu);
+        x = bfly_stage<2>(x, lane, 0x33333333u);
+        x = bfly_stage<1>(x, lane, 0x55555555u);
         if (h == 0 ? wc.has0 : wc.has1)
             bw[(rt * 32 + (lane & 31)) * WS + (h == 0 ? wc.t0 : wc.t1)] = x;
     }
@@ -347,21 +367,8 @@ NAV_DEV void gemm_bits(const float* scr, const float* __restrict__ img, f32x16 (
     for (int rt = 0; rt < RT; ++rt) w[rt] = wrow[rt * 32 * WS];
     auto frag = [&](int q, int rt) {
         const uint32_t byte = (w[rt] >> (16 * (q & 1) + 8 * h)) & 0xFFu;
-#if NAV_BITS_VALUFRAG
-        // bits 2m, 2m + 1 -> fp16 1.0 / 0 in the two halves of dword m: (b0 | b1 << 16) * 0x3C00
-        (void)tab;
-        uint4 e;
-        uint32_t d[4];
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-            const uint32_t t = byte >> (2 * m);
-            d[m] = __builtin_amdgcn_mul_u24((t & 1u) | ((t & 2u) << 15), 0x3C00u);
-        }
-        e.x = d[0]; e.y = d[1]; e.z = d[2]; e.w = d[3];
-        return __builtin_bit_cast(f16x8, e);
-#else
+        // (fragments built by VALU from the byte instead: neutral, r06r)
         return __builtin_bit_cast(f16x8, tab[byte]);
-#endif
     };
     f16x8 af[RT];
 #pragma unroll
@@ -624,22 +631,6 @@ NAV_DEV void store_mask(const f32x16 (&acc)[RT][2], uint16_t* mask, int64_t rt0)
 // mask order 1, 2, 4, 8, 16, so the big early stages are DPP moves inside a 16-lane row (xor 1 /
 // 2: quad_perm, xor 4: half-row mirror then quad_perm, xor 8: row rotate by 8) and only the last,
 // single-element one crosses rows (ds_bpermute).
-template <int M_>
-NAV_DEV float lane_xor(float v) {
-    const int x = __float_as_int(v);
-    if constexpr (M_ == 1) {
-        return __int_as_float(__builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false));  // [1,0,3,2]
-    } else if constexpr (M_ == 2) {
-        return __int_as_float(__builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, false));  // [2,3,0,1]
-    } else if constexpr (M_ == 4) {
-        const int m7 = __builtin_amdgcn_mov_dpp(x, 0x141, 0xF, 0xF, false);  // l ^ 7
-        return __int_as_float(__builtin_amdgcn_mov_dpp(m7, 0x1B, 0xF, 0xF, false));  // ^ 3
-    } else if constexpr (M_ == 8) {
-        return __int_as_float(__builtin_amdgcn_mov_dpp(x, 0x128, 0xF, 0xF, false));  // ror 8
-    } else {
-        return __shfl_xor(v, M_, 64);
-    }
-}
 
 // one halving stage of the transpose-reduce: lanes with bit M_ set keep the upper half of the
 // list (n entries) and send the lower half to lane ^ M_

@@ -101,6 +101,9 @@ for step in "$@"; do
     dbgvar) for v in $DVARS; do run dbg_$v 120 python tools/withlib.py "$ROOT/abl/libnavenv_$v.so" tools/dbg_bits.py --batch 16421; done ;;
     dbgbits) run dbgbits_16421 120 python tools/dbg_bits.py --batch 16421 &&
              run dbgbits_2048 120 python tools/dbg_bits.py --batch 2048 ;;
+    wgab) for r in 1 2 3; do for v in "" $WVARS; do tag=${v:-base}
+            W=(); [ -n "$v" ] && W=(tools/withlib.py "$ROOT/abl/libnavenv_$v.so")
+            run wgab_${tag}_$r 120 python "${W[@]}" tools/wgrad_bench.py; done; done ;;
     config1) run config1 300 python tools/config1_run.py ;;
     mix) run mix 100 ./build/mix_probe ;;
     shape) run shape 200 ./build/mfma_shape_probe 512 2.5 0 && run shape_dz 200 ./build/mfma_shape_probe 512 2.5 1 ;;
