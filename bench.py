@@ -40,20 +40,40 @@ F16_MFMA_PEAK_TFS = 2516.6  # MI355X_MICROARCH.md: 1024 FLOP/clk/SIMD x 1024 SIM
 #                             (dense fp16 = bf16 rate)
 # The row kernels' hidden x hidden f32 GEMMs run on the fp16 matrix cores as 3 products of a
 # scaled two-plane split (lo.hi + hi.lo + hi.hi; rounds 3-4: 6 products of a three-plane bf16
-# split): the MFMA FLOPs per f32 product, and the network passes (forwards + row backwards) per
-# row block of each row kernel
+# split); since round 6 the top layer's row backward of the d_out = 1 critics takes 2 (its A
+# operand is the forward's ReLU bit, exact in fp16: gemm_bits)
 PRODUCTS_PER_PASS = 3
+PRODUCTS_BITS = 2
 
 
 def products_per_f32(region):
-    """fp16 MFMA products per f32 product: 3 (lo.hi + hi.lo + hi.hi), except the factored critic
-    weight gradient k_wgrad_fact, whose A operand (the ReLU bit) is exact in fp16: 2."""
+    """fp16 MFMA products per f32 product of the weight-gradient kernels: 3, except the factored
+    critic weight gradient k_wgrad_fact, whose A operand (the ReLU bit) is exact in fp16: 2."""
     return 2 if region == "mlp_wgrad_fact" else PRODUCTS_PER_PASS
+
+
+def layer_products(region, rows, layers):
+    """fp16 products x hidden-layer GEMMs one row block of the region's kernel runs (each such
+    GEMM is 2 x rows x hp^2 FLOP per product). A forward pass: (layers - 1) hidden GEMMs at 3; a
+    critic (d_out = 1) row backward: its top layer at 2 (gemm_bits) + the rest at 3; the actor's
+    row backward (d_out = 2): all at 3. critic_rows: target actor + 2 target critics + 2 online
+    forwards + 2 critic backwards (at batches <= 2048 the twins split into two workgroups that
+    each repeat the 3 target passes); actor_rows: actor + critic forwards, critic backward, actor
+    backward; the acting forward / tick: one forward."""
+    h = layers - 1
+    fwd = 3 * h
+    cbwd = (PRODUCTS_BITS + 3 * (h - 1)) if h >= 1 else 0
+    if region == "critic_rows":
+        return (8 if rows <= 2048 else 5) * fwd + 2 * cbwd
+    if region == "actor_rows":
+        return 2 * fwd + cbwd + 3 * h
+    return fwd if region in ("act", "act_tick") else 0
 
 
 # the median shader clock each row kernel holds under the bench loop (tools/clock_probe.py)
 HELD_CLOCK_MHZ = {"critic_rows": 1925.3, "actor_rows": 1964.5, "act_tick": 2048.1}
-ROOFLINE_VERSION = "r05: fp16 two-plane split, 3 products per f32 product (r03-r04: bf16 6)"
+ROOFLINE_VERSION = ("r06: fp16 two-plane split, 3 products per f32 product, 2 in the critics' "
+                    "top-layer row backward (r05: 3 everywhere; r03-r04: bf16 6)")
 
 
 # what the path computes in: the hidden x hidden GEMMs are NOT fp32 MFMA but fp16 MFMA products
@@ -88,13 +108,6 @@ def graded_step_fracs(sweep):
     return out
 
 
-def hidden_passes(region, rows):
-    """Hidden x hidden GEMM passes per row block: critic_rows 7 (target actor, 2 target critics,
-    2 online forwards, 2 row backwards), or 10 at batches <= 2048 where the twins split into two
-    workgroups that each repeat the 3 target passes; actor_rows 4; the acting forward 1."""
-    if region == "critic_rows":
-        return 10 if rows <= 2048 else 7
-    return {"actor_rows": 4, "act": 1, "act_tick": 1}.get(region, 0)
 # HBM bytes per launch from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this same
 # command (tools/pmc_traffic.py, gfx950 correction applied); bench regions -> kernel names
 PMC_TRAFFIC = os.path.join(HERE, "profiles", "pmc_traffic.json")
@@ -502,14 +515,17 @@ def main():
             # fp16 dense peak; the f32-equivalent rate of all its FLOPs is a separate key
             hp = (args.hidden + 31) // 32 * 32
             rows = args.envs if dominant in ("act", "act_tick") else rank_batch
-            layer = (args.layers - 1) * 2.0 * rows * hp * hp
             if dominant in ("mlp_wgrad", "mlp_wgrad_fact"):
                 # the weight-gradient regions carry their hidden x hidden f32 FLOPs as work
                 hidden = d["work_per_launch"]
+                products = products_per_f32(dominant)
+                mfma_flop = products * hidden
             else:
-                hidden = hidden_passes(dominant, rows) * layer
-            products = products_per_f32(dominant)
-            mfma_flop = products * hidden
+                lp = layer_products(dominant, rows, args.layers)
+                mfma_flop = lp * 2.0 * rows * hp * hp
+                passes = {"critic_rows": 10 if rows <= 2048 else 7, "actor_rows": 4}
+                hidden = passes.get(dominant, 1) * (args.layers - 1) * 2.0 * rows * hp * hp
+                products = "3 (2 in the critics' top-layer row backward)"
             tfs = mfma_flop / (d["avg_us"] * 1e-6) / 1e12
             roof = {"bound": "mfma", "kernel": dominant, "achieved": round(tfs, 1),
                     "peak": F16_MFMA_PEAK_TFS, "unit": "TFLOP/s",
@@ -517,10 +533,10 @@ def main():
                     "version": ROOFLINE_VERSION,
                     "fp16_products_per_f32_product": products,
                     "peak_note": "fp16 dense MFMA peak: the hidden x hidden f32 GEMMs run on the "
-                                 "fp16 matrix cores as %d products of a power-of-two-scaled "
+                                 "fp16 matrix cores as products of a power-of-two-scaled "
                                  "two-plane fp16 split (22-bit operands, f32 accumulate; pinned "
-                                 "vs fp64); achieved = those MFMA FLOPs per launch / the "
-                                 "launch's event-timed duration" % products,
+                                 "vs fp64); achieved = the MFMA FLOPs those products issue per "
+                                 "launch / the launch's event-timed duration",
                     "mfma_flop_per_launch": mfma_flop,
                     "hidden_gemm_f32_flop_per_launch": hidden,
                     # DVFS: the row kernels hold ~1.93 GHz, not the 2.4 GHz of the spec peak
