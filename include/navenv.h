@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define NAV_ABI_VERSION 10
+#define NAV_ABI_VERSION 11
 #define NAV_EINVAL (-100000)
 
 #define NAV_WORLD_CELLS 100 /* field = float32 [100][100][2] (speed, angle), x-major: cell cx*100+cy
@@ -96,7 +96,9 @@ typedef struct nav_replay {
  * hidden width padded to a multiple of 32 with zeros (exact: relu(0)=0, zero rows/cols add 0):
  *   W0 [hp][d_in], b0 [hp], {Wl [hp][hp], bl [hp]} x (n_hidden-1), Wo [d_out][hp], bo [d_out]
  * plus `packed` = per hidden->hidden layer the fp16 MFMA B-operand images of the forward
- * (B[k][n] = W[n][k]) then of the backward (B[k][n] = W[k][n]) product: per column n an exponent
+ * (B[k][n] = W[n][k]) then of the backward (B[k][n] = W[k][n]; for d_out = 1 the top hidden
+ * layer's backward image holds B[k][n] = fl32(Wo[0][k] W[k][n]), the operand of the row
+ * backward's bit-operand product, ABI 11) product: per column n an exponent
  * e_n (B's column max |B| 2^e_n in [2^13, 2^14)) and each entry as two fp16 planes hi =
  * fp16(B 2^e_n), lo = fp16(B 2^e_n - hi) (22 significant bits), laid out [plane 2][hp/16][2][hp][8]
  * (entry (p, k/16, (k/8)&1, n, k&7)) followed by int32 e[hp]: hp^2 + hp floats per image; rebuilt

@@ -13,7 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libnavenv.so")
 _lib_path = LIB_PATH
 NAV_EINVAL = -100000
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 _dp = C.POINTER(C.c_double)
 _vp = C.c_void_p

@@ -67,7 +67,7 @@ def test_gfx950_code_object_present(navlib):
 def test_abi_and_layout(navlib):
     from nav.mlp import layer_offsets
     from nav._lib import NavMlp
-    assert navlib.nav_abi_version() == 10
+    assert navlib.nav_abi_version() == 11
     assert navlib.nav_demo_index_res() in (1, 2, 4, 8)
     # the CPU port's index (cpu_baseline) is built at the same resolution
     from oracle import oracle as O
