@@ -75,6 +75,10 @@ __host__ __device__ inline int64_t edge_to_flat(const MlpDev& d, int64_t e) {
 
 inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// ReLU as an integer max of the bit pattern: one v_max_i32 (fmaxf costs a NaN-quieting
+// v_max_f32 x, x first). Negative values and -0 give +0; finite results equal fmaxf(v, 0).
+NAV_DEV float relu(float v) { return __int_as_float(max(__float_as_int(v), 0)); }
+
 // One hidden unit of layer 0 (K = d_in <= 4; absent inputs and weights are 0). The forward and the
 // weight-gradient kernel's recompute of h_0 share this fma order, so both produce the same bits.
 NAV_DEV float layer0_unit(float4 x, float w0, float w1, float w2, float w3, float b) {
@@ -83,7 +87,7 @@ NAV_DEV float layer0_unit(float4 x, float w0, float w1, float w2, float w3, floa
     v = fmaf(x.y, w1, v);
     v = fmaf(x.z, w2, v);
     v = fmaf(x.w, w3, v);
-    return fmaxf(v, 0.f);
+    return relu(v);
 }
 
 // dL/dz of the top hidden layer before its ReLU mask: dy . Wo[:, n] (d_out <= 2; absent = 0).

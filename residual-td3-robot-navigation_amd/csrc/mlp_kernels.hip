@@ -806,7 +806,9 @@ NAV_DEV L0Pre load_l0(const MlpDev& net) {
 // layer stays in registers (`top`, C layout) — its LDS rows are written only when save_mask asks
 // for its global copy — and the output layer's per-wave partials land in `red` (ready for out_y
 // after the trailing barrier).
-template <int NT, int RT, int PFB = 1>
+// DIN: the network's d_in when the caller knows it (2 actor, 4 critic; 0: read net.d_in), so the
+// layer-0 product has no branch on the input count
+template <int NT, int RT, int PFB = 1, int DIN = 0>
 NAV_DEV void fwd_net(const MlpDev& net, float* act, _Float16* stage, const float* xin, float* red,
                      uint16_t* masks, int64_t n_rt, float* act_save, uint32_t save_mask,
                      int64_t row0, int64_t M, int64_t rt0, f32x16 (&top)[RT][2], int mk = -64,
@@ -828,7 +830,7 @@ NAV_DEV void fwd_net(const MlpDev& net, float* act, _Float16* stage, const float
     {
         const L0Pre l0 = pre ? *pre : load_l0<NT>(net);
         float m0[RT] = {};
-        const bool x23 = net.d_in > 2;
+        const bool x23 = DIN == 0 ? net.d_in > 2 : DIN > 2;
         // A operands: row l32 of each row tile, inputs h and 2 + h
         float xa[RT], xb[RT];
 #pragma unroll
@@ -856,7 +858,7 @@ NAV_DEV void fwd_net(const MlpDev& net, float* act, _Float16* stage, const float
                 uint32_t bits = 0;
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
-                    const float r = fmaxf(v[i], 0.f);
+                    const float r = relu(v[i]);
                     col[(rt * 32 + (i & 3) + 8 * (i >> 2)) * SS] = r;
                     bits |= (r > 0.f ? 1u : 0u) << i;
                     m0[rt] = fmaxf(m0[rt], r);
@@ -884,7 +886,7 @@ NAV_DEV void fwd_net(const MlpDev& net, float* act, _Float16* stage, const float
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-                for (int i = 0; i < 16; ++i) acc[rt][j][i] = fmaxf(acc[rt][j][i] + b, 0.f);
+                for (int i = 0; i < 16; ++i) acc[rt][j][i] = relu(acc[rt][j][i] + b);
         }
     };
     auto mask_of = [&](int L) { return masks ? masks + (size_t)L * n_rt * NT * 64 : nullptr; };
@@ -1011,7 +1013,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_mlp_fwd(FwdArgs a) {
 
     float* red = xin + TM * 4;  // [2][PARTS][TM]
     f32x16 top[RT][2];
-    fwd_net<NT, RT, kPfWide>(net, act, stage, xin, red, masks, n_rt, act_save, a.save_mask, row0, M, rt0, top,
+    fwd_net<NT, RT, kPfWide, IN_MODE == IN_BASELINE ? 2 : 0>(net, act, stage, xin, red, masks, n_rt, act_save, a.save_mask, row0, M, rt0, top,
                     OUT_MODE == OUT_TICK ? NAV_TICK_MK : -64, &l0);
     const int rloc = tid % TM;
     const int j = tid / TM;
@@ -1581,7 +1583,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
     // Each pass's layer-0 constants are loaded one pass ahead (L0Pre).
     f32x16 top[RT][2];
     const L0Pre l0_ct1 = load_l0<NT>(a.critic_t[0]);
-    fwd_net<NT, RT, kPfWide>(a.actor_t, act, stage, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0, top, 2,
+    fwd_net<NT, RT, kPfWide, 2>(a.actor_t, act, stage, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0, top, 2,
                     &l0_at);
     if (tn >= 0 && tn < 2 * TM) {  // the noise's threads
         const int rloc = tn % TM, j = tn / TM;
@@ -1599,12 +1601,12 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
     // twin target critics on (s', a'), then y = r + gamma * min(q1', q2') * (1 - done), kept in
     // the row's thread
     const L0Pre l0_ct2 = load_l0<NT>(a.critic_t[1]);
-    fwd_net<NT, RT, kPfWide>(a.critic_t[0], act, stage, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0, top,
+    fwd_net<NT, RT, kPfWide, 4>(a.critic_t[0], act, stage, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0, top,
                     9, &l0_ct1);
     if (tid < TM) qv[tid] = out_y<RT>(a.critic_t[0], red, tid, 0);
     const int q0 = a.split_twins ? (int)blockIdx.y : 0;  // the first online critic of the block
     L0Pre l0_on = load_l0<NT>(a.critic[q0]);
-    fwd_net<NT, RT, kPfWide>(a.critic_t[1], act, stage, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0, top,
+    fwd_net<NT, RT, kPfWide, 4>(a.critic_t[1], act, stage, xin, red, nullptr, n_rt, nullptr, 0u, row0, B, rt0, top,
                     15, &l0_ct2);
     float yt = 0.f;
     if (tid < TM) {
@@ -1621,7 +1623,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a)
         if (a.split_twins && q != (int)blockIdx.y) continue;  // workgroup-uniform
         uint32_t top_bits[RT * 2];
         WoCols wo;
-        fwd_net<NT, RT, kPfWide>(a.critic[q], act, stage, xin, red, a.masks[q], n_rt, a.acts[q], a.save_mask, row0,
+        fwd_net<NT, RT, kPfWide, 4>(a.critic[q], act, stage, xin, red, a.masks[q], n_rt, a.acts[q], a.save_mask, row0,
                         B, rt0, top, 22 + 14 * q, &l0_on, top_bits, &wo);
         if (q == 0 && !a.split_twins) l0_on = load_l0<NT>(a.critic[1]);
         float* es = a.eslab[q] ? a.eslab[q] + (int64_t)blockIdx.x * a.ecount : nullptr;
@@ -1699,7 +1701,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_actor_rows(ActorRowsArgs a) {
     __syncthreads();
     // the actor's top hidden layer stays in registers until dL/da is known (its dWo partials)
     f32x16 topa[RT][2];
-    fwd_net<NT, RT>(a.actor, act, stage, xin, red, a.masks_a, n_rt, a.acts, a.save_mask, row0, B, rt0,
+    fwd_net<NT, RT, 1, 2>(a.actor, act, stage, xin, red, a.masks_a, n_rt, a.acts, a.save_mask, row0, B, rt0,
                     topa, -64, &l0_a);
     const L0Pre l0_c = load_l0<NT>(a.critic);  // in flight under the action epilogue
     if (tid < 2 * TM) {
@@ -1712,7 +1714,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_td3_actor_rows(ActorRowsArgs a) {
     f32x16 top[RT][2];
     uint32_t top_bits[RT * 2];
     WoCols wo;
-    fwd_net<NT, RT>(a.critic, act, stage, xin, red, a.masks_c, n_rt, nullptr, 0u, row0, B, rt0, top,
+    fwd_net<NT, RT, 1, 4>(a.critic, act, stage, xin, red, a.masks_c, n_rt, nullptr, 0u, row0, B, rt0, top,
                     -64, &l0_c, top_bits, &wo);
     if (tid < TM && a.q && row0 + tid < B) a.q[row0 + tid] = out_y<RT>(a.critic, red, tid, 0);
     bwd_net<NT, RT, 1, CBM>(a.critic, act, stage, dys, xin, a.masks_c, n_rt, nullptr, nullptr,

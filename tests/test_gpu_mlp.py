@@ -693,6 +693,47 @@ def _f64_forward(layers, x):
     return h, zs
 
 
+@pytest.mark.parametrize("M", [4096, 16421])
+def test_split_gemm_per_row_accuracy_rows_spanning_binades(nav, M):
+    """Per-row accuracy of the split GEMM's A operand: the A scale is per 32-row
+    tile, so a row far below its tile's maximum keeps fewer significant bits in the lo plane
+    (fp16 subnormals). Rows of x scaled by 2^-u, u uniform in [0, 20] (biases zeroed, so the
+    layer-1 input and output of a row scale with it): each row of h_1 against fp64, relative to
+    that row's own max, within 4 (2^-22 + 2^(s - 37)) where 2^-s is the row's h_0 max over its
+    tile's — the bound of the scaled two-plane split (the lo plane's absolute step is 2^-24 of a
+    scaled maximum in [2^13, 2^14)). Rows near their tile's max meet f32-class accuracy; rows
+    2^-20 below it ~2^-17."""
+    from nav.mlp import DeviceMLP, forward
+    from oracle.td3_oracle import make_mlp_params
+    d_in, d_out, hidden, nh = 4, 1, 256, 2
+    p = make_mlp_params(91, [d_in, hidden, hidden, d_out])
+    p = [(W, b * 0) for W, b in p]
+    net = DeviceMLP(d_in, d_out, hidden, nh, DEV).load(p)
+    layers = [(torch.tensor(W), torch.tensor(b)) for W, b in p]
+    g = torch.Generator().manual_seed(77 + M)
+    u = torch.randint(0, 21, (M, 1), generator=g).float()
+    x = (torch.randn(M, d_in, generator=g) * torch.pow(2.0, -u)).contiguous()
+    out = torch.zeros(M, d_out, device=DEV)
+    acts = torch.zeros(nh, M, net.hp, device=DEV)
+    forward([net], x.to(DEV), d_in, 0, [out], d_out, 0, M, acts=[acts], save_mask=3)
+    torch.cuda.synchronize()
+    _, zs = _f64_forward(layers, x)
+    h0 = torch.relu(zs[0])
+    h1 = torch.relu(zs[1])
+    got = acts[1].cpu().double()[:, :hidden]
+    rmax0 = h0.abs().amax(1)
+    tmax0 = rmax0.view(-1)[:M - M % 32].view(-1, 32).amax(1).repeat_interleave(32)
+    tmax0 = torch.cat([tmax0, rmax0[M - M % 32:].max().expand(M % 32)]) if M % 32 else tmax0
+    ok = rmax0 > 0
+    s = torch.log2(tmax0[ok] / rmax0[ok]).clamp(min=0)
+    err = (got[ok] - h1[ok]).abs().amax(1) / h1[ok].abs().amax(1).clamp(min=1e-300)
+    bound = 4 * (2.0 ** -22 + torch.pow(2.0, s - 37))
+    live = h1[ok].abs().amax(1) > 0
+    assert bool((err[live] <= bound[live]).all()), float((err[live] / bound[live]).max())
+    print("per-row err: max %.2e, median %.2e; rows with s > 12: max %.2e" % (
+        err[live].max(), err[live].median(), err[live & (s > 12)].max()))
+
+
 @pytest.mark.parametrize("d_in,d_out,hidden,nh", [(2, 2, 200, 3), (4, 1, 200, 3), (2, 2, 256, 2),
                                                   (4, 1, 256, 2), (4, 1, 192, 2)])
 @pytest.mark.parametrize("M", [4097, 16421])
