@@ -45,8 +45,8 @@ struct WgradArgs {
     int TN;                 // tn-high tiles across hp
     int n_hid;              // tile jobs per network = (nh - 1) * TN * TT
     int fact;               // 1: the factored-Wo path (wgrad_tile_fact) for every tile
-    int64_t per_split;      // rows per split (multiple of 64)
-    int64_t per_wave;       // rows per wave (multiple of 64)
+    int64_t per_split;      // rows per split (multiple of 32)
+    int64_t per_wave;       // rows per wave (multiple of 32)
     int64_t skew;           // rows moved from each of waves 4-7 to its SIMD partner wave w - 4
 };
 
@@ -154,12 +154,13 @@ NAV_DEV void wgrad_rows(const WgradArgs& a, int y, int L, int n0, int k0, int64_
             cg.x = ok ? g[0] : 0.f;
             cg.y = ok && d_out > 1 ? g[1] : 0.f;
             const int64_t rt0 = rb >> 5;
+            const bool t1 = rb + 32 < r_hi;  // a range may end after the chunk's first tile
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
                 for (int t = 0; t < 2; ++t) {
-                    const uint16_t* w = mk + ((rt0 + t) * NTm + (i ? tm1 : tm0)) * 64 + l32;
-                    cm[i][t] = (uint32_t)w[0] | ((uint32_t)w[32] << 16);
+                    const uint16_t* w = mk + ((rt0 + (t && t1)) * NTm + (i ? tm1 : tm0)) * 64 + l32;
+                    cm[i][t] = t && !t1 ? 0u : (uint32_t)w[0] | ((uint32_t)w[32] << 16);
                 }
         }
     };
@@ -180,6 +181,7 @@ NAV_DEV void wgrad_rows(const WgradArgs& a, int y, int L, int n0, int k0, int64_
         if (more) load(rb + WG_CHUNK);  // next chunk in flight under this one
 #pragma unroll
         for (int s = 0; s < WG_CHUNK / 2; ++s) {
+            if (rb + 2 * s >= r_hi) break;  // wave-uniform: a range's last chunk may be short
             const int rr = 2 * s + h;  // row of this lane half inside the chunk
             float p[2], q[2];
             if (PR) {
@@ -1475,9 +1477,11 @@ static int wgrad_args(const nav_mlp* nets, int32_t n_nets, int64_t M, const floa
     // accumulator sets and two splits per element (measured slower than wgrad_rows_mfma: 40 vs
     // 34 us at 2x256 on bf16, profiles/r04c; on the fp16 split 31.9 vs 25.4 us, r06r)
     a.fact = wgrad_fact_ok(hp, nh) && a.net[0].d_out == 1;
-    // 64-row aligned splits and per-wave ranges: a chunk's mask row tiles start on a tile boundary
-    a.per_split = ((M + splits - 1) / splits + WG_CHUNK - 1) / WG_CHUNK * WG_CHUNK;
-    a.per_wave = ((a.per_split + WG_WAVES - 1) / WG_WAVES + WG_CHUNK - 1) / WG_CHUNK * WG_CHUNK;
+    // 32-row aligned splits and per-wave ranges: a chunk's mask row tiles start on a tile
+    // boundary (at 64-row granularity a 100-row batch ran on 2 of the 8 waves: config 1's k_wgrad
+    // 19.7 us, the generic path's rows loop ~30 k cycles, profiles/r06zf)
+    a.per_split = ((M + splits - 1) / splits + 31) / 32 * 32;
+    a.per_wave = ((a.per_split + WG_WAVES - 1) / WG_WAVES + 31) / 32 * 32;
     // whole 32-row tiles moved to the first wave of each SIMD pair, per 256 rows of a wave
     // (tools/wgrad_bench.py, profiles/r05ad_ab_wgrad_skew.txt: 0 / 32 / 64 / 96 rows for the
     // factored kernel -> 32.5 / 32.0 / 31.8 / 33.0 us, 0 / 64 / 96 / 128 for the operand path ->

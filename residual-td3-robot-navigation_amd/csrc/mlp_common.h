@@ -221,8 +221,10 @@ constexpr int kTraced = 64;
 #define NAV_TRACED_SLOT() (blockIdx.x % 8 == 0 && blockIdx.x / 8 < kTraced ? (int)blockIdx.x / 8 : -1)
 #else
 constexpr int kTraced = 4;
+// (grid row 0 only: split twins would race on the slots)
 #define NAV_TRACED_SLOT()                                                                      \
-    (blockIdx.x == 0 ? 0 : blockIdx.x == 1 ? 1 : blockIdx.x == 200 ? 2 : blockIdx.x == 511 ? 3 : -1)
+    (blockIdx.y != 0 ? -1 : blockIdx.x == 0 ? 0 : blockIdx.x == 1 ? 1 : blockIdx.x == 200 ? 2   \
+                          : blockIdx.x == 511 ? 3 : -1)
 #endif
 __device__ unsigned long long g_phase_trace[kTraced][kBlock / 64][64];
 #define NAV_MARK(k)                                                                            \

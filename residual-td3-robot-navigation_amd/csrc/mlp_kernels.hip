@@ -22,6 +22,17 @@ namespace {
 
 // 32-row blocks double-buffer the split stage and pass one barrier per k step (r03zt)
 constexpr bool kStageDb1 = true;
+// 32-row blocks split the whole layer's A once, then run the product without barriers
+// (gemm_cols_whole); NAV_WHOLE1=0 restores the per-step stage (A/B)
+#ifndef NAV_WHOLE1
+#define NAV_WHOLE1 1
+#endif
+constexpr bool kWholeStage1 = NAV_WHOLE1;
+// L2 warmer workgroups beside small row-kernel grids (warm_l2); NAV_WARM=0 for A/B
+#ifndef NAV_WARM
+#define NAV_WARM 1
+#endif
+[[maybe_unused]] constexpr bool kWarmL2 = NAV_WARM;
 // B-fragment prefetch distance (k steps) of the 64-row GEMMs in the critic row kernel and the
 // forward / tick kernels (the actor row kernel keeps 1: profiles/r05aq)
 #ifndef NAV_PF_WIDE
@@ -43,6 +54,7 @@ struct WaveCols {
 // then scale every row identically, so the forward stays bit-identical across block heights.
 template <int TM>
 NAV_DEV float* amax_slots(_Float16* stage);
+NAV_DEV _Float16* whole_stage(_Float16* stage);
 
 template <int RT>
 NAV_DEV void publish_amax(float* slots, const float (&m)[RT]) {
@@ -65,9 +77,116 @@ NAV_DEV void publish_amax(float* slots, const float (&m)[RT]) {
 // l32][16q + 8h + j] and B[16q + 8h + j][col l32], j = 0..7 (the 32x32x16 operand maps). Every wave
 // runs the split and the barriers; waves without a column tile (NT < 4) skip only the MFMAs. The
 // result is unscaled before it is returned: the callers see acc = A . B in f32.
+#ifndef NAV_PF1
+#define NAV_PF1 2
+#endif
+constexpr int kPF1 = NAV_PF1;  // B prefetch distance of 32-row blocks
+
+// gemm_cols for 32-row blocks (small batches, latency-bound): the workgroup scales and splits
+// the whole layer's 32 x hp A values into the whole-layer stage at once (two k steps per pass of
+// the block, the same per-step layout and swizzle as the stage below), passes ONE barrier, and
+// every wave then runs all k steps from LDS with no barrier in the product; the per-step stage
+// cost a barrier + fragment-read round trip per k step (~640 cycles per step at hp = 224 vs the
+// step's 6 MFMAs, profiles/r06x). Same products, same order: bit-identical to the per-step form.
+template <int NT>
+NAV_DEV void gemm_cols_whole(const float* __restrict__ A, int S_, const float* __restrict__ img,
+                             _Float16* stage, f32x16 (&acc)[1][2]) {
+    constexpr int hp = NT * 32;
+    constexpr int nq = hp / 16;
+    constexpr size_t PL = (size_t)nq * 2 * hp;
+    constexpr size_t STEP = 2 * (size_t)hp;
+    constexpr int PP = 32 * 16;  // fp16 per plane per step
+    const int tid = threadIdx.x, lane = tid & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
+    const WaveCols<NT> wc(wv);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[0][j][i] = 0.f;
+    const int t0 = wc.has0 ? wc.t0 : 0, t1 = wc.has1 ? wc.t1 : t0;
+    const float* sl = amax_slots<32>(stage);
+    const int ea = pow2_exp(fmaxf(fmaxf(sl[0], sl[1]), fmaxf(sl[2], sl[3])));
+    const int* ex = image_exps(img, hp);
+    const int eb0 = ex[t0 * 32 + l32], eb1 = ex[t1 * 32 + l32];
+    const char* Bb = reinterpret_cast<const char*>(img);
+    const uint32_t o0 = (uint32_t)(h * hp + t0 * 32 + l32) * 16u;
+    const uint32_t o1 = (uint32_t)(h * hp + t1 * 32 + l32) * 16u;
+    auto ldB = [&](uint32_t o, int p, int q) {
+        return *reinterpret_cast<const f16x8*>(Bb + (o + (uint32_t)((p * PL + q * STEP) * 16)));
+    };
+    constexpr int PF = kPF1 < nq ? kPF1 : nq;
+    f16x8 bq0[PF + 1][2], bq1[PF + 1][2];
+#pragma unroll
+    for (int d = 0; d < PF; ++d)
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            bq0[d][p] = ldB(o0, p, d);
+            bq1[d][p] = ldB(o1, p, d);
+        }
+    // the split: thread (step parity qo, row sr, k offset sk) takes 4 values of steps qo, qo + 2, ..
+    _Float16* const whole = whole_stage(stage);
+    const int qo = tid >> 7, sr = (tid >> 2) & 31, sk = (tid & 3) * 4;
+    const float* src = A + sr * S_ + sk + 16 * qo;
+    _Float16* dst = whole + qo * 2 * PP + sr * 16 + ((((sk >> 3) ^ (sr >> 3)) & 1) << 3) + (sk & 7);
+    const float sa = ldexpf(1.f, ea);
+    float4 xs[nq / 2];
+#pragma unroll
+    for (int p = 0; p < nq / 2; ++p) xs[p] = *reinterpret_cast<const float4*>(src + 32 * p);
+#pragma unroll
+    for (int p = 0; p < nq / 2; ++p) {
+        const float v[4] = {xs[p].x * sa, xs[p].y * sa, xs[p].z * sa, xs[p].w * sa};
+        f16x4 ph, pl;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ph[j] = (_Float16)v[j];
+        pin_value(ph);  // lo from the stored hi's bits (mlp_common.h)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pl[j] = (_Float16)(v[j] - (float)ph[j]);
+        *reinterpret_cast<f16x4*>(dst + p * 4 * PP) = ph;
+        *reinterpret_cast<f16x4*>(dst + p * 4 * PP + PP) = pl;
+    }
+    __syncthreads();
+    const _Float16* frag = whole + l32 * 16 + (((h ^ (l32 >> 3)) & 1) << 3);
+    auto ldA = [&](int q) {
+        Split2 a;
+        a.h = *reinterpret_cast<const f16x8*>(frag + q * 2 * PP);
+        a.l = *reinterpret_cast<const f16x8*>(frag + q * 2 * PP + PP);
+        return a;
+    };
+    Split2 af = ldA(0);
+#pragma unroll
+    for (int q = 0; q < nq; ++q) {
+        if (q + PF < nq) {
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+                bq0[(q + PF) % (PF + 1)][p] = ldB(o0, p, q + PF);
+                bq1[(q + PF) % (PF + 1)][p] = ldB(o1, p, q + PF);
+            }
+        }
+        Split2 an;
+        if (q + 1 < nq) an = ldA(q + 1);
+        if (wc.has0) {  // wave-uniform
+            acc[0][0] = mfma_x3(af, bq0[q % (PF + 1)], acc[0][0]);
+            if (NT >= 8 || wc.has1) acc[0][1] = mfma_x3(af, bq1[q % (PF + 1)], acc[0][1]);
+        }
+        if (q + 1 < nq) af = an;
+        // a scheduling fence per k step (as in gemm_bits): without a barrier in the loop the
+        // scheduler sinks the prefetched loads down to their uses
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    const int u0 = -(ea + eb0), u1 = -(ea + eb1);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        acc[0][0][i] = ldexpf(acc[0][0][i], u0);
+        acc[0][1][i] = ldexpf(acc[0][1][i], u1);
+    }
+}
+
 template <int NT, int RT, int PFB = 1>
 NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const float* __restrict__ img,
                        _Float16* stage, f32x16 (&acc)[RT][2]) {
+    if constexpr (RT == 1 && kWholeStage1) {
+        gemm_cols_whole<NT>(A, S_, img, stage, acc);
+        return;
+    }
     constexpr int hp = NT * 32;
     constexpr int nq = hp / 16;
     constexpr int TM = RT * 32;
@@ -110,7 +229,7 @@ NAV_DEV void gemm_cols(const float* __restrict__ A, int S_, const float* __restr
     // B prefetch distance in k steps: 64-row blocks take the caller's PFB (2 in the critic row
     // kernel and the forward / tick launches, 1 in the 256-register actor row kernel, where a
     // second step of B fragments costs more than it hides: profiles/r05ap)
-    constexpr int PF = RT == 1 ? 2 : PFB;
+    constexpr int PF = RT == 1 ? kPF1 : PFB;
     f16x8 bq0[PF + 1][2], bq1[PF + 1][2];
 #pragma unroll
     for (int d = 0; d < PF; ++d)
@@ -349,7 +468,7 @@ NAV_DEV void gemm_bits(const float* scr, const float* __restrict__ img, f32x16 (
         return *reinterpret_cast<const f16x8*>(Bb + (o + (uint32_t)((p * PL + q * STEP) * 16)));
     };
     // B prefetch distance in k steps as gemm_cols
-    constexpr int PF = RT == 1 ? 2 : PFB;
+    constexpr int PF = RT == 1 ? kPF1 : PFB;
     f16x8 bq0[PF + 1][2], bq1[PF + 1][2];
 #pragma unroll
     for (int d = 0; d < PF; ++d)
@@ -501,19 +620,25 @@ __host__ __device__ constexpr int red_floats(int tm) { return 2 * kWaves * tm; }
 __host__ __device__ constexpr size_t stage_halves(int tm) {
     return (size_t)(tm == 32 && kStageDb1 ? 2 : 1) * 2 * tm * 16;
 }
-__host__ __device__ constexpr size_t stage_bytes(int tm) {
-    return stage_halves(tm) * 2 + 4 * kWaves * (tm / 32);
+// 32-row blocks also take the whole-layer stage past the slots (gemm_cols_whole): [hp / 16 k
+// steps][2 planes][32][16] fp16, hp * 128 bytes
+__host__ __device__ constexpr size_t stage_bytes(int tm, int hp) {
+    return stage_halves(tm) * 2 + 4 * kWaves * (tm / 32) +
+           (tm == 32 && kWholeStage1 ? (size_t)hp * 128 : 0);
 }
 template <int TM>
 NAV_DEV float* amax_slots(_Float16* stage) {
     return reinterpret_cast<float*>(stage + stage_halves(TM));
+}
+NAV_DEV _Float16* whole_stage(_Float16* stage) {
+    return stage + stage_halves(32) + 2 * kWaves;  // past the 32-row block's 4 slots (16 B)
 }
 
 // rows [tm][hp+4] + input/dy staging [tm][4] + output-layer partial sums, then the split stage
 __host__ __device__ constexpr size_t lds_floats(int hp, int tm) {
     return (size_t)tm * (hp + 4) + tm * 4 + red_floats(tm);
 }
-inline size_t lds_bytes(int hp, int tm) { return lds_floats(hp, tm) * 4 + stage_bytes(tm); }
+inline size_t lds_bytes(int hp, int tm) { return lds_floats(hp, tm) * 4 + stage_bytes(tm, hp); }
 
 
 // Store a layer's C-layout result into the LDS rows (the next layer's A operand) and its ReLU
@@ -894,9 +1019,11 @@ NAV_DEV void fwd_net(const MlpDev& net, float* act, _Float16* stage, const float
     for (int L = 1; L + 1 < nh; ++L) {
         f32x16 acc[RT][2];
         hidden_layer(L, acc);
+        NAV_TRACE_MARK(50);
         __syncthreads();  // every wave has finished reading the layer's input rows
         store_layer<NT, RT>(acc, act, SS, mask_of(L), rt0, amax_slots<RT * 32>(stage));
         __syncthreads();
+        NAV_TRACE_MARK(51);
         if (act_save && ((save_mask >> L) & 1u))
             copy_rows<NT, RT>(act, SS, act_save + (int64_t)L * M * hp, row0, M);
     }
@@ -1495,6 +1622,65 @@ NAV_DEV void sample_row(const float* rows, int64_t size, const int64_t* idx, uin
     hi = src[1];
 }
 
+// ---- L2 warmers for small grids ----
+// A 32-row workgroup streams every weight image it multiplies by (hp^2 + hp floats per layer)
+// and, alone on its XCD at small batches, each k step's B fragments arrive from beyond its L2 at
+// one CU's fetch rate (~75 GB/s: ~500 cycles per step of 6 MFMAs at hp = 224, flat in the
+// prefetch depth; profiles/r06za). The row kernels therefore launch, when the compute grid leaves
+// most CUs idle, extra workgroup rows (blockIdx.y >= y0) that only touch one 4-B word per 128-B
+// line of the launch's images, in the order the compute workgroups consume them, so the lines
+// are in each XCD's L2 before the compute workgroups ask. Blocks are dealt round-robin over the
+// 8 XCDs (MI355X_MICROARCH: b and b + 8 share one; speed only, never correctness): the warmers
+// with equal (index mod 8) split the image list between them.
+constexpr int kWarmMax = 16;         // image ranges per launch
+constexpr int kWarmPerXcd = 16;      // warmer workgroups per XCD
+constexpr int64_t kWarmGrid = 128;   // compute workgroups up to which warmers are launched
+struct WarmList {
+    int y0;                          // grid rows of compute workgroups (warmers: rows >= y0)
+    int n;                           // ranges (0: no warmers)
+    const char* p[kWarmMax];
+    uint32_t bytes[kWarmMax];
+};
+
+NAV_DEV void warm_l2(const WarmList& w) {
+    const uint32_t j = blockIdx.x + gridDim.x * (blockIdx.y - (uint32_t)w.y0);
+    const uint32_t nw = gridDim.x * (gridDim.y - (uint32_t)w.y0);
+    const uint32_t cnt = (nw - (j & 7u) + 7u) >> 3, rank = j >> 3;  // warmers of this XCD
+    uint32_t x = 0;
+    for (int i = 0; i < w.n; ++i) {
+        const uint32_t lines = (w.bytes[i] + 127u) >> 7;
+        const uint32_t per = (lines + cnt - 1u) / cnt;
+        const uint32_t l1 = min(lines, (rank + 1u) * per);
+        const char* p = w.p[i];
+#pragma unroll 4
+        for (uint32_t l = rank * per + threadIdx.x; l < l1; l += kBlock)
+            x ^= *reinterpret_cast<const uint32_t*>(p + ((size_t)l << 7));
+    }
+    asm volatile("" ::"v"(x));  // keeps the loads
+}
+
+// host: append [p, p + bytes) to the list; false when full
+inline bool warm_add(WarmList& w, const float* p, int64_t floats) {
+    if (w.n >= kWarmMax) return false;
+    w.p[w.n] = reinterpret_cast<const char*>(p);
+    w.bytes[w.n++] = (uint32_t)(floats * 4);
+    return true;
+}
+// host: a network's forward images (layers 1 .. nh-1), or its whole packed buffer (all images)
+inline bool warm_net(WarmList& w, const MlpDev& net, bool fwd_only) {
+    if (net.n_hidden < 2) return true;
+    const int64_t im = split_image_floats(net.hp);
+    if (!fwd_only) return warm_add(w, net.packed, (int64_t)(net.n_hidden - 1) * 2 * im);
+    for (int L = 1; L < net.n_hidden; ++L)
+        if (!warm_add(w, net.packed + (int64_t)(L - 1) * 2 * im, im)) return false;
+    return true;
+}
+// host: grid rows of warmers for a compute grid of gx x gy (0: none)
+inline unsigned warm_rows(const WarmList& w, unsigned gx, unsigned gy) {
+    if (w.n == 0 || (int64_t)gx * gy > kWarmGrid) return 0;
+    return (8u * kWarmPerXcd + gx - 1) / gx;
+}
+
 struct CriticRowsArgs {
     MlpDev actor_t, critic_t[2], critic[2];
     int64_t B;
@@ -1516,7 +1702,9 @@ struct CriticRowsArgs {
     int split_twins;      // grid.y = 2: workgroup y runs online critic y only (small batches)
     float* dz[2];         // [nh][B][hp] dz rows of dz_save_mask layers (row_backward)
     uint32_t dz_save_mask;
+    WarmList warm;        // set by the launcher
 };
+static_assert(sizeof(CriticRowsArgs) <= 4096, "kernel argument size");
 
 // train_critic (robot.py:329-361) for one block of TM batch rows: sample, target policy
 // smoothing through the target actor, twin target critics, TD target, then the twin online
@@ -1528,6 +1716,10 @@ struct CriticRowsArgs {
 template <int NT, int RT, int CBM>
 __global__ __launch_bounds__(kBlock, 1) void k_td3_critic_rows(CriticRowsArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
+    if (a.warm.n && (int)blockIdx.y >= a.warm.y0) {  // an L2 warmer row (small grids)
+        warm_l2(a.warm);
+        return;
+    }
     constexpr int hp = NT * 32, SS = hp + 4, TM = RT * 32;
     const int tid = threadIdx.x;
     const int64_t B = a.B, row0 = (int64_t)blockIdx.x * TM, rt0 = (int64_t)blockIdx.x * RT;
@@ -1664,6 +1856,7 @@ struct ActorRowsArgs {
     uint16_t* masks_c;
     float* eslab;        // actor edge partials
     int64_t ecount;
+    WarmList warm;       // set by the launcher
 };
 
 // train_actor (robot.py:382-390) for one block of TM batch rows: sample, actor forward,
@@ -1673,6 +1866,10 @@ struct ActorRowsArgs {
 template <int NT, int RT, int CBM>
 __global__ __launch_bounds__(kBlock, 1) void k_td3_actor_rows(ActorRowsArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
+    if (a.warm.n && (int)blockIdx.y >= a.warm.y0) {  // an L2 warmer row (small grids)
+        warm_l2(a.warm);
+        return;
+    }
     constexpr int hp = NT * 32, SS = hp + 4, TM = RT * 32;
     const int tid = threadIdx.x;
     const int64_t B = a.B, row0 = (int64_t)blockIdx.x * TM, rt0 = (int64_t)blockIdx.x * RT;
@@ -1804,25 +2001,43 @@ void launch_critic_rows_k(const CriticRowsArgs& a, hipStream_t st) {
     constexpr int TM = RT * 32;
     const size_t lds =
         ((size_t)TM * (NT * 32 + 4) + TM * 4 + red_floats(TM) + TM * 8 + TM + TM * 4) * 4 +
-        stage_bytes(TM);
+        stage_bytes(TM, NT * 32);
     // form 1 also for 2 hidden layers (its gemm_cols loop then runs no layer): the form-2
     // instantiation came out at 286 registers (one workgroup per CU), form 1 at 236
     auto k = a.critic[0].n_hidden == 1 ? k_td3_critic_rows<NT, RT, 0> : k_td3_critic_rows<NT, RT, 1>;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
-    hipLaunchKernelGGL(k, dim3((unsigned)((a.B + TM - 1) / TM), a.split_twins ? 2u : 1u),
-                       dim3(kBlock), lds, st, a);
+    const unsigned gx = (unsigned)((a.B + TM - 1) / TM), gy = a.split_twins ? 2u : 1u;
+    // the images in the order the compute workgroups consume them (targets: forward only)
+    CriticRowsArgs w = a;
+    w.warm = WarmList{};
+    bool ok = kWarmL2 && warm_net(w.warm, a.actor_t, true) && warm_net(w.warm, a.critic_t[0], true) &&
+              warm_net(w.warm, a.critic_t[1], true) && warm_net(w.warm, a.critic[0], false) &&
+              warm_net(w.warm, a.critic[1], false);
+    if (!ok) w.warm.n = 0;
+    w.warm.y0 = (int)gy;
+    const unsigned wy = warm_rows(w.warm, gx, gy);
+    if (wy == 0) w.warm.n = 0;
+    hipLaunchKernelGGL(k, dim3(gx, gy + wy), dim3(kBlock), lds, st, w);
 }
 
 template <int NT, int RT>
 void launch_actor_rows_k(const ActorRowsArgs& a, hipStream_t st) {
     constexpr int TM = RT * 32;
     const size_t lds = ((size_t)TM * (NT * 32 + 4) + TM * 4 + red_floats(TM) + TM * 8) * 4 +
-                       stage_bytes(TM);
+                       stage_bytes(TM, NT * 32);
     auto k = a.critic.n_hidden == 1 ? k_td3_actor_rows<NT, RT, 0> : k_td3_actor_rows<NT, RT, 1>;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
-    hipLaunchKernelGGL(k, dim3((unsigned)((a.B + TM - 1) / TM)), dim3(kBlock), lds, st, a);
+    const unsigned gx = (unsigned)((a.B + TM - 1) / TM);
+    ActorRowsArgs w = a;
+    w.warm = WarmList{};
+    const bool ok = kWarmL2 && warm_net(w.warm, a.actor, false) && warm_net(w.warm, a.critic, false);
+    if (!ok) w.warm.n = 0;
+    w.warm.y0 = 1;
+    const unsigned wy = warm_rows(w.warm, gx, 1u);
+    if (wy == 0) w.warm.n = 0;
+    hipLaunchKernelGGL(k, dim3(gx, 1u + wy), dim3(kBlock), lds, st, w);
 }
 
 template <int RT>
@@ -1869,7 +2084,8 @@ int NAV_CAT(nav_mlp_rows_, NAV_MLP_PART)(int fam, int rt, int in_mode, int out_m
                    : rows_rt<2>(fam, in_mode, out_mode, args, n_nets, st);
 }
 
-#if defined(NAV_PHASE_TRACE) && NAV_MLP_PART == 8
+// (a trace variant builds one part with NAV_PHASE_TRACE: tools/build_variant.sh)
+#if defined(NAV_PHASE_TRACE)
 extern "C" int nav_phase_trace_read(unsigned long long* host, int n) {
     const size_t bytes = sizeof(g_phase_trace);
     if (!host || (size_t)n * sizeof(unsigned long long) < bytes) return NAV_EINVAL;

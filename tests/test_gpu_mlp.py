@@ -187,6 +187,8 @@ def relu_bits(masks, nh, hp, hidden, M):
 @pytest.mark.parametrize("d_in,d_out,hidden,nh,M", [(4, 1, 200, 3, 100), (2, 2, 200, 3, 777),
                                                     (4, 1, 256, 2, 5000), (2, 2, 256, 2, 4096),
                                                     (4, 1, 64, 1, 300), (2, 2, 96, 4, 333),
+                                                    # 32-row wave ranges ending mid-chunk
+                                                    (4, 1, 200, 3, 33), (2, 2, 64, 3, 97),
                                                     # 64-row blocks (RT = 2, > 16 384 rows)
                                                     (4, 1, 256, 2, 16421), (2, 2, 200, 3, 16421),
                                                     (4, 1, 64, 1, 16421),

@@ -87,6 +87,11 @@ for step in "$@"; do
              run phase_${v}_16448 200 python "${W[@]}" tools/phase_trace.py --batch 16448
              run phase_${v}_tick 200 python "${W[@]}" tools/phase_trace.py --tick
            done ;;
+    phase1) for v in ${PV1:-trace7}; do
+              W=(tools/withlib.py "$ROOT/abl/libnavenv_$v.so")
+              run phase1_$v 200 python "${W[@]}" tools/phase_trace.py --batch 100 --hidden 200 --n-hidden 3 --n-envs 1024
+            done ;;
+    wtrace1) run wtrace1 200 python tools/withlib.py "$ROOT/abl/libnavenv_wtrace.so" tools/wgrad_trace.py --batch 100 --hidden 200 --n-hidden 3 --n-envs 1024 ;;
     wtrace) for v in ${TVARS:-wtrace}; do
               run ${v}_32k 200 python tools/withlib.py "$ROOT/abl/libnavenv_$v.so" tools/wgrad_trace.py &&
               run ${v}_16k 200 python tools/withlib.py "$ROOT/abl/libnavenv_$v.so" tools/wgrad_trace.py --batch 16384
@@ -104,6 +109,7 @@ for step in "$@"; do
     wgab) for r in 1 2 3; do for v in "" $WVARS; do tag=${v:-base}
             W=(); [ -n "$v" ] && W=(tools/withlib.py "$ROOT/abl/libnavenv_$v.so")
             run wgab_${tag}_$r 120 python "${W[@]}" tools/wgrad_bench.py; done; done ;;
+    c1prof) run c1prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/c1trace" -o run -- python tools/config1_run.py ;;
     config1) run config1 300 python tools/config1_run.py ;;
     mix) run mix 100 ./build/mix_probe ;;
     shape) run shape 200 ./build/mfma_shape_probe 512 2.5 0 && run shape_dz 200 ./build/mfma_shape_probe 512 2.5 1 ;;

@@ -5,7 +5,9 @@ bound through tools/withlib.py. Runs the bench trainer for a few steps, then rea
 4 traced workgroups (blocks 0, 1, 200, 511) x 4 waves and prints each phase's duration in
 cycles of that counter, per wave, plus the per-phase mean over the 16 traced waves.
 
-python tools/withlib.py abl/libnavenv_trace.so tools/phase_trace.py [--batch B]
+python tools/withlib.py abl/libnavenv_trace.so tools/phase_trace.py [--batch B] [--hidden H
+    --n-hidden L --n-envs N]  (config 1's learner: --batch 100 --hidden 200 --n-hidden 3, a
+    trace7 build)
 (--batch 16448: 257 workgroups of 64 rows, so the traced ones run alone on their CU)
 """
 import ctypes as C
@@ -58,11 +60,14 @@ def main():
     ap.add_argument("--wide", action="store_true",
                     help="a -DNAV_TRACE_WIDE build: 64 blocks (0, 8, 16, ...), per block its start "
                          "and end relative to the earliest traced start, plus the phase means")
+    ap.add_argument("--hidden", type=int, default=256)
+    ap.add_argument("--n-hidden", type=int, default=2)
+    ap.add_argument("--n-envs", type=int, default=65536)
     args = ap.parse_args()
     from nav._lib import lib_path
     from nav.trainer import VecTrainer
-    tr = VecTrainer(n_envs=65536, hidden=256, n_hidden=2, batch=args.batch, updates_per_step=2,
-                    envs_per_group=1024)
+    tr = VecTrainer(n_envs=args.n_envs, hidden=args.hidden, n_hidden=args.n_hidden,
+                    batch=args.batch, updates_per_step=2, envs_per_group=1024)
     for _ in range(4):
         tr.step()
     torch.cuda.synchronize()
@@ -90,6 +95,13 @@ def main():
         d = t[:, :, b] - t[:, :, a]
         out["marks"][f"{b:02d} {names[b]}"] = {"mean": float(d.mean()), "min": int(d.min()),
                                                "max": int(d.max())}
+    if not args.tick and (t[:, :, 50] != 0).any():
+        # a >= 3-layer forward's inner marks (the last forward of the block; twin 0 of block 0:
+        # critic1, marks 24 .. 25): layer-1 product + bias, store_layer + barriers, top product
+        w0 = t[0]
+        out["inner_fwd"] = {"gemm1": (w0[:, 50] - w0[:, 24]).tolist(),
+                            "store": (w0[:, 51] - w0[:, 50]).tolist(),
+                            "gemm2": (w0[:, 25] - w0[:, 51]).tolist()}
     print(json.dumps(out, indent=1))
 
 

@@ -33,10 +33,13 @@ def main():
     import argparse
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=32768)
+    ap.add_argument("--hidden", type=int, default=256)
+    ap.add_argument("--n-hidden", type=int, default=2)
+    ap.add_argument("--n-envs", type=int, default=65536)
     args = ap.parse_args()
     from nav._lib import lib_path
     from nav.trainer import VecTrainer
-    tr = VecTrainer(n_envs=65536, hidden=256, n_hidden=2, batch=args.batch, updates_per_step=2,
+    tr = VecTrainer(n_envs=args.n_envs, hidden=args.hidden, n_hidden=args.n_hidden, batch=args.batch, updates_per_step=2,
                     envs_per_group=1024)
     for _ in range(6):
         tr.step()
