@@ -109,7 +109,8 @@ for step in "$@"; do
     wgab) for r in 1 2 3; do for v in "" $WVARS; do tag=${v:-base}
             W=(); [ -n "$v" ] && W=(tools/withlib.py "$ROOT/abl/libnavenv_$v.so")
             run wgab_${tag}_$r 120 python "${W[@]}" tools/wgrad_bench.py; done; done ;;
-    c1prof) run c1prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/c1trace" -o run -- python tools/config1_run.py ;;
+    c1prof) run c1prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/c1trace" -o run -- python tools/config1_run.py
+            rm -f "$O/c1trace/run_kernel_trace.csv" ;;  # ~100 k rows: over gpurun's copy-back cap
     config1) run config1 300 python tools/config1_run.py ;;
     mix) run mix 100 ./build/mix_probe ;;
     shape) run shape 200 ./build/mfma_shape_probe 512 2.5 0 && run shape_dz 200 ./build/mfma_shape_probe 512 2.5 1 ;;
