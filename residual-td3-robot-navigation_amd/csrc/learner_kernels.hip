@@ -95,7 +95,11 @@ __host__ __device__ inline int wgrad_tile_n(int d_out, int hp, int n_hidden) {
 }
 
 // rows [r_lo, r_hi) of one wave into acc (tile n0.., k0.. of layer L of net y)
-template <bool PR, bool QR>
+// RA (k_wgrad_gen): the chunk's saved dz / h row values are loaded into registers before its
+// products (loaded at their use inside the product they exposed one memory round trip per row
+// pair: ~20 k cycles for 32 rows at config 1's shape, profiles/r06zj); k_wgrad, whose MFMA-operand
+// path holds 254 registers, keeps the loads at their use
+template <bool PR, bool QR, bool RA_ = false>
 NAV_DEV void wgrad_rows(const WgradArgs& a, int y, int L, int n0, int k0, int64_t r_lo,
                         int64_t r_hi, float* stage, f32x16 (&acc)[2][2]) {
     const MlpDev& net = a.net[y];
@@ -125,6 +129,9 @@ NAV_DEV void wgrad_rows(const WgradArgs& a, int y, int L, int n0, int k0, int64_
             b0[j] = bb[ck[j]];
         }
     }
+    // one saved operand only (two would not fit next to the accumulators), HS row pairs at a time
+    constexpr bool RA = RA_ && (PR != QR);
+    constexpr int HS = WG_CHUNK / 8;  // row pairs per register window
     const int NTm = hp >> 5;
     const uint16_t* mk = PR ? a.masks[y] + (size_t)(nh - 1) * mask_rowtiles(M) * NTm * 64 : nullptr;
     const int tm0 = n0 >> 5, tm1 = nv1 ? tm0 + 1 : tm0;
@@ -179,9 +186,28 @@ NAV_DEV void wgrad_rows(const WgradArgs& a, int y, int L, int n0, int k0, int64_
     for (int64_t rb = r_lo; rb < r_hi; rb += WG_CHUNK) {
         const bool more = rb + WG_CHUNK < r_hi;
         if (more) load(rb + WG_CHUNK);  // next chunk in flight under this one
+        float ps[RA && !PR ? HS : 1][2], qs[RA && !QR ? HS : 1][2];
+        auto window = [&](int s0) {  // the saved row values of row pairs s0 .. s0 + HS - 1
+#pragma unroll
+            for (int u = 0; u < HS; ++u) {
+                const int64_t r = rb + 2 * (s0 + u) + h;
+                const bool ok = r < r_hi;
+                const int64_t rc = ok ? r : r_lo;
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    if constexpr (!PR) ps[u][i] = ok ? Psv[rc * hp + cn[i]] : 0.f;
+                    if constexpr (!QR) qs[u][i] = ok ? Qsv[rc * hp + ck[i]] : 0.f;
+                }
+            }
+        };
 #pragma unroll
         for (int s = 0; s < WG_CHUNK / 2; ++s) {
-            if (rb + 2 * s >= r_hi) break;  // wave-uniform: a range's last chunk may be short
+            // wave-uniform: a range's last chunk may be short (RA stops at a window boundary: the
+            // window's rows past r_hi add exact zeros, and its row registers stay static)
+            if ((!RA || s % HS == 0) && rb + 2 * s >= r_hi) break;
+            if constexpr (RA) {
+                if (s % HS == 0) window(s);
+            }
             const int rr = 2 * s + h;  // row of this lane half inside the chunk
             float p[2], q[2];
             if (PR) {
@@ -194,6 +220,9 @@ NAV_DEV void wgrad_rows(const WgradArgs& a, int y, int L, int n0, int k0, int64_
                     const uint32_t bit = (mw[i][s >> 4] >> sh) & 1u;
                     p[i] = bit ? top_unit(g.x, g.y, wo[i][0], wo[i][1]) : 0.f;
                 }
+            } else if constexpr (RA) {
+#pragma unroll
+                for (int i = 0; i < 2; ++i) p[i] = ps[RA && !PR ? s % HS : 0][i];
             } else {
                 const int64_t r = rb + rr;
                 const bool ok = r < r_hi;
@@ -205,6 +234,9 @@ NAV_DEV void wgrad_rows(const WgradArgs& a, int y, int L, int n0, int k0, int64_
                 const float4 x = *reinterpret_cast<const float4*>(xs + rr * 4);
 #pragma unroll
                 for (int j = 0; j < 2; ++j) q[j] = layer0_unit(x, w0[j][0], w0[j][1], w0[j][2], w0[j][3], b0[j]);
+            } else if constexpr (RA) {
+#pragma unroll
+                for (int j = 0; j < 2; ++j) q[j] = qs[RA && !QR ? s % HS : 0][j];
             } else {
                 const int64_t r = rb + rr;
                 const bool ok = r < r_hi;
@@ -929,7 +961,9 @@ NAV_DEV void wgrad_tile_fact(const WgradArgs& a, const TileJob& t, float* smem, 
 }
 
 // The tile job's partial over its split's rows, written as one slab tile (8 waves' partials
-// summed in wave order)
+// summed in wave order). GEN (k_wgrad_gen, networks of >= 3 hidden layers, whose tiles never take
+// the MFMA-operand path): the generic rows only, with their saved rows loaded ahead (RA)
+template <bool GEN>
 NAV_DEV void wgrad_tile(const WgradArgs& a, const TileJob& t, float* smem) {
     WG_MARK(1, 0);
     const int y = t.y, split = t.split, L = t.L, n0 = t.n0, k0 = t.k0;
@@ -949,11 +983,18 @@ NAV_DEV void wgrad_tile(const WgradArgs& a, const TileJob& t, float* smem) {
         for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-    if (opnd) wgrad_rows_mfma(a, y, n0, k0, r_lo, r_hi, acc);
-    else if (pr && qr) wgrad_rows<true, true>(a, y, L, n0, k0, r_lo, r_hi, stage, acc);
-    else if (pr) wgrad_rows<true, false>(a, y, L, n0, k0, r_lo, r_hi, stage, acc);
-    else if (qr) wgrad_rows<false, true>(a, y, L, n0, k0, r_lo, r_hi, stage, acc);
-    else wgrad_rows<false, false>(a, y, L, n0, k0, r_lo, r_hi, stage, acc);
+    if constexpr (GEN) {
+        if (pr && qr) wgrad_rows<true, true, true>(a, y, L, n0, k0, r_lo, r_hi, stage, acc);
+        else if (pr) wgrad_rows<true, false, true>(a, y, L, n0, k0, r_lo, r_hi, stage, acc);
+        else if (qr) wgrad_rows<false, true, true>(a, y, L, n0, k0, r_lo, r_hi, stage, acc);
+        else wgrad_rows<false, false, true>(a, y, L, n0, k0, r_lo, r_hi, stage, acc);
+    } else {
+        if (opnd) wgrad_rows_mfma(a, y, n0, k0, r_lo, r_hi, acc);
+        else if (pr && qr) wgrad_rows<true, true>(a, y, L, n0, k0, r_lo, r_hi, stage, acc);
+        else if (pr) wgrad_rows<true, false>(a, y, L, n0, k0, r_lo, r_hi, stage, acc);
+        else if (qr) wgrad_rows<false, true>(a, y, L, n0, k0, r_lo, r_hi, stage, acc);
+        else wgrad_rows<false, false>(a, y, L, n0, k0, r_lo, r_hi, stage, acc);
+    }
     // the 8 partial tiles meet in LDS, summed in wave order
     WG_MARK(1, 5);
     wgrad_reduce_write<2>(a, y, split, L, n0, k0, acc, red);
@@ -964,7 +1005,11 @@ NAV_DEV void wgrad_tile(const WgradArgs& a, const TileJob& t, float* smem) {
 // register allocation)
 __global__ __launch_bounds__(WG_THREADS) void k_wgrad(WgradArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    wgrad_tile(a, wgrad_job(a, blockIdx.x, gridDim.x), smem);
+    wgrad_tile<false>(a, wgrad_job(a, blockIdx.x, gridDim.x), smem);
+}
+__global__ __launch_bounds__(WG_THREADS) void k_wgrad_gen(WgradArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    wgrad_tile<true>(a, wgrad_job(a, blockIdx.x, gridDim.x), smem);
 }
 template <int NI, int D>
 __global__ __launch_bounds__(WG_THREADS) void k_wgrad_fact(WgradArgs a) {
@@ -1504,8 +1549,10 @@ int nav_mlp_wgrad(const nav_mlp* nets, int32_t n_nets, int64_t M, const float* i
     const int64_t blocks = (int64_t)n_nets * a.n_hid * splits;
     // the factored kernel: its 4 KB fragment table is static, the dynamic part the reduce slots
     const size_t lds = a.fact ? (size_t)WG_WAVES * WG_TILE * WG_TILE * 4 : wgrad_lds_bytes();
-    void (*k)(WgradArgs) = !a.fact ? k_wgrad
-                           : a.tn == 128 ? k_wgrad_fact<4, 1> : k_wgrad_fact<2, 1>;
+    // >= 3 hidden layers: no tile is both the top and the first layer (no operand path)
+    void (*k)(WgradArgs) = a.fact                  ? (a.tn == 128 ? k_wgrad_fact<4, 1> : k_wgrad_fact<2, 1>)
+                           : a.net[0].n_hidden >= 3 ? k_wgrad_gen
+                                                    : k_wgrad;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(WG_THREADS), lds, S(stream), a);
