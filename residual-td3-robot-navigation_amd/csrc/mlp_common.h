@@ -79,6 +79,19 @@ inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 // v_max_f32 x, x first). Negative values and -0 give +0; finite results equal fmaxf(v, 0).
 NAV_DEV float relu(float v) { return __int_as_float(max(__float_as_int(v), 0)); }
 
+// On post-ReLU values (v >= +0, so the bit patterns order like the values): the ReLU bit as
+// min(bits, 1) (every positive float's pattern is >= 1; +0's is 0) and the running max as an
+// integer max (fmaxf quiets both operands first), one VALU each
+#ifndef NAV_NNBITS
+#define NAV_NNBITS 1
+#endif
+NAV_DEV uint32_t pos_bit(float v) {
+    return NAV_NNBITS ? min((uint32_t)__float_as_int(v), 1u) : (v > 0.f ? 1u : 0u);
+}
+NAV_DEV float max_nn(float m, float v) {
+    return NAV_NNBITS ? __int_as_float(max(__float_as_int(m), __float_as_int(v))) : fmaxf(m, v);
+}
+
 // One hidden unit of layer 0 (K = d_in <= 4; absent inputs and weights are 0). The forward and the
 // weight-gradient kernel's recompute of h_0 share this fma order, so both produce the same bits.
 NAV_DEV float layer0_unit(float4 x, float w0, float w1, float w2, float w3, float b) {

@@ -662,8 +662,8 @@ NAV_DEV void store_layer(f32x16 (&acc)[RT][2], float* act, int S_, uint16_t* mas
             for (int i = 0; i < 16; ++i) {
                 const float v = acc[rt][j][i];
                 col[(rt * 32 + (i & 3) + 8 * (i >> 2)) * S_] = v;
-                bits |= (v > 0.f ? 1u : 0u) << i;
-                m[rt] = fmaxf(m[rt], v);  // post-ReLU: v >= 0
+                bits |= pos_bit(v) << i;
+                m[rt] = max_nn(m[rt], v);  // post-ReLU: v >= 0
             }
             if (mask) mask[mask_idx(rt0 + rt, NT, t, lane)] = (uint16_t)bits;
         }
@@ -741,7 +741,7 @@ NAV_DEV void store_mask(const f32x16 (&acc)[RT][2], uint16_t* mask, int64_t rt0)
         for (int rt = 0; rt < RT; ++rt) {
             uint32_t bits = 0;
 #pragma unroll
-            for (int i = 0; i < 16; ++i) bits |= (acc[rt][j][i] > 0.f ? 1u : 0u) << i;
+            for (int i = 0; i < 16; ++i) bits |= pos_bit(acc[rt][j][i]) << i;  // post-ReLU
             mask[mask_idx(rt0 + rt, NT, t, lane)] = (uint16_t)bits;
         }
     }
@@ -985,8 +985,8 @@ NAV_DEV void fwd_net(const MlpDev& net, float* act, _Float16* stage, const float
                 for (int i = 0; i < 16; ++i) {
                     const float r = relu(v[i]);
                     col[(rt * 32 + (i & 3) + 8 * (i >> 2)) * SS] = r;
-                    bits |= (r > 0.f ? 1u : 0u) << i;
-                    m0[rt] = fmaxf(m0[rt], r);
+                    bits |= pos_bit(r) << i;
+                    m0[rt] = max_nn(m0[rt], r);
                 }
                 if (masks) masks[mask_idx(rt0 + rt, NT, t, lane)] = (uint16_t)bits;
             }
@@ -1049,7 +1049,7 @@ NAV_DEV void fwd_net(const MlpDev& net, float* act, _Float16* stage, const float
                 for (int rt = 0; rt < RT; ++rt) {
                     uint32_t bits = 0;
 #pragma unroll
-                    for (int i = 0; i < 16; ++i) bits |= (top[rt][j][i] > 0.f ? 1u : 0u) << i;
+                    for (int i = 0; i < 16; ++i) bits |= pos_bit(top[rt][j][i]) << i;  // post-ReLU
                     top_bits[rt * 2 + j] = has ? bits : 0u;
                     if (mk && has)
                         mk[mask_idx(rt0 + rt, NT, j == 0 ? wc.t0 : wc.t1, lane)] = (uint16_t)bits;
