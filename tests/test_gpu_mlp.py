@@ -461,7 +461,10 @@ def test_td3_update_vs_oracle_and_reference(nav):
 
 
 # 16 421 rows: the 64-row (RT = 2) form the bench's batch runs
-@pytest.mark.parametrize("hidden,nh,B", [(200, 3, 333), (256, 2, 2048), (256, 2, 16421)])
+# 333 / 2048: 32-row blocks with L2 warmer rows beside them (<= 128 compute workgroups); 4097:
+# 32-row blocks without (129); 16421: 64-row blocks
+@pytest.mark.parametrize("hidden,nh,B", [(200, 3, 333), (256, 2, 2048), (256, 2, 4097),
+                                         (256, 2, 16421)])
 def test_fused_row_kernels_match_unfused(nav, hidden, nh, B):
     """nav_td3_critic_rows / nav_td3_actor_rows (one launch each) produce bit-identical batches,
     targets, dq, losses, ReLU bits, dL/da and edge partials to the per-network kernels they
